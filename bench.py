@@ -1,0 +1,273 @@
+"""Benchmark of the sift-based-OD hot path on MI355X (driver contract: see DESIGN.md §Bench).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one pass of the whole hot path over one synthetic query image:
+BF k=2 matching of Nq queries against this rank's DB shard (bf16 MFMA) -> RCCL all-gather
++ global top-2 merge -> ratio test -> Hough pose + LDS-privatised vote histogram (own
+shard) -> RCCL all-reduce of bin counts / first touch -> valid-bin selection, members,
+PoseBin means -> per-bin affine LSQ + outlier rejection to a fixed point.
+
+Workload (weak scaling): every rank holds a 1M-row DB shard (1000 model
+images x 1000 keypoints), so N GPUs search an N*1M-row DB (N=8: config C4/C5, 50k x 8M);
+the query image has 50k keypoints (1000x800), bins 32x32x8x12, thresholds 5/4.
+
+value = descriptor pairs / s over the whole job = N * Nq * Nshard / step time (max over
+ranks).  Hough votes/s and per-stage times are reported beside it, the matcher kernel's
+achieved bf16 MFMA rate against the 2.5 PF/s dense peak in "roofline", and the CPU
+restatement (oracle, numpy/OpenBLAS on the host cores) on a bounded slice in
+"cpu_baseline".
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import sod_pkg  # noqa: E402
+
+sod_pkg.load()
+from sift_based_od_amd import _lib, synthetic  # noqa: E402
+
+METRIC = "descriptor-pair distances/sec + Hough votes/sec per query; 1/2/4/8 GPU"
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+FLOP_PER_PAIR = 2 * 128
+
+CONFIGS = {
+    # name: (queries, images per rank, keypoints per image, bins, run_affine)
+    "c3": (50000, 1000, 1000, (32, 32, 8, 12), True),
+    "c2": (10000, 100, 1000, (15, 15, 15, 15), False),
+    "c5": (50000, 1000, 1000, (32, 32, 8, 12), True),
+    "tiny": (2000, 20, 1000, (15, 15, 15, 15), True),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-queries", type=int, default=512)
+    return p.parse_args()
+
+
+class Dist:
+    """torch.distributed (gloo, host side) for rendezvous, barriers, the RCCL unique-id
+    broadcast and the max-over-ranks of the timings.  The data path uses RCCL inside
+    libsod; torch is only this plumbing."""
+
+    def __init__(self, n):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != n:
+            if n != 1 or self.world != 1:
+                raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (n, self.world))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def bcast_bytes(self, b):
+        if self.world == 1:
+            return b
+        import torch
+        t = torch.zeros(len(b) if b is not None else _lib.UNIQUE_ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            t[:] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        self.dist.broadcast(t, 0)
+        return bytes(t.numpy().tobytes())
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def device_sync(world):
+    # the whole step runs on libsod's own stream (ctx.synchronize() waits for it); with
+    # several ranks torch is loaded anyway and a device-wide sync is added on top
+    if world > 1:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+
+def cpu_baseline(queries, db_des, nq_sample):
+    """Oracle (numpy/OpenBLAS sgemm, exact) on a bounded slice: nq_sample queries against
+    the full shard.  Returns pairs/s."""
+    sys.path.insert(0, REPO)
+    from oracle import oracle as orc
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS")
+                  or os.cpu_count())
+    try:
+        from threadpoolctl import threadpool_info
+        nt = [i.get("num_threads") for i in threadpool_info() if i.get("internal_api") == "openblas"]
+        if nt:
+            threads = int(nt[0])
+    except Exception:
+        pass
+    q = queries[:nq_sample]
+    dbf = np.ascontiguousarray(db_des, dtype=np.float32)
+    t0 = time.perf_counter()
+    orc.knn2_match(q, dbf, chunk=64)
+    dt = time.perf_counter() - t0
+    return {"value": len(q) * len(db_des) / dt, "unit": "pairs/s", "cores": threads,
+            "kind": "port",
+            "sample": "oracle knn2 (numpy/OpenBLAS f32 GEMM + exact top-2) of %d queries x %d DB "
+                      "rows on the host, %.1f s" % (len(q), len(db_des), dt)}
+
+
+def main():
+    a = parse()
+    D = Dist(a.gpus)
+    nq, nimg, kpi, bins, run_affine = CONFIGS[a.config]
+    world, rank = D.world, D.rank
+
+    # ---- data: rank r holds DB images [r*nimg, (r+1)*nimg) of one seeded DB -------------
+    t0 = time.time()
+    # keypoints + image table of the WHOLE DB are replicated; descriptors
+    # are generated for this rank's shard only
+    parts = []
+    shard = None
+    for r in range(world):
+        if r == rank:
+            db = synthetic.make_database(nimg, kpi, seed=0, first_image=r * nimg)
+            shard = db.des
+            parts.append((db.kp, db.img, db.centroid, db.size))
+        else:
+            parts.append(synthetic.make_database(nimg, kpi, seed=0, first_image=r * nimg,
+                                                 descriptors=False))
+    x = np.concatenate([p[0].x for p in parts])
+    y = np.concatenate([p[0].y for p in parts])
+    ang = np.concatenate([p[0].angle for p in parts])
+    octv = np.concatenate([p[0].octave for p in parts])
+    img = np.concatenate([p[1] + r * nimg for r, p in enumerate(parts)])
+    cent = np.concatenate([p[2] for p in parts])
+    size = np.concatenate([p[3] for p in parts])
+    qs = synthetic.make_queries(nq, seed=1, db_seed=0, kp_per_image=kpi)
+    gen_s = time.time() - t0
+
+    ctx = _lib.Context(D.local)
+    from sift_based_od_amd.database import Keypoints
+    ctx.set_keypoints(Keypoints(x, y, ang, octv), img, cent, size)
+    n_shard = shard.shape[0]
+    ctx.upload_db(shard, row_offset=rank * n_shard)
+    ctx.upload_queries(qs.des, qs.kp)
+    if world > 1:
+        uid = _lib.unique_id() if rank == 0 else None
+        uid = D.bcast_bytes(uid)
+        ctx.comm_init(world, rank, uid)
+
+    def step():
+        ctx.pipeline(qs.shape, bins, ratio=0.75, vote_threshold=5, affine_threshold=4,
+                     x_factor=128.0, y_factor=128.0, run_affine=run_affine)
+
+    for _ in range(a.warmup):
+        step()
+    ctx.synchronize()
+
+    # ---- timed region ----------------------------------------------------------------
+    match_ms, stage = [], []
+    D.barrier()
+    ctx.synchronize()
+    device_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    ctx.synchronize()
+    device_sync(world)
+    D.barrier()
+    t1 = time.perf_counter()
+    el = D.max(t1 - t0)
+    ms_per_step = 1000.0 * el / a.steps
+
+    # ---- per-kernel timing (HIP events on the ctx stream), separate untimed steps -------
+    for _ in range(max(3, min(a.steps, 10))):
+        step()
+        ctx.synchronize()
+        match_ms.append(ctx.last_match_ms())
+        stage.append(ctx.stage_ms())
+    match_ms = float(np.mean(match_ms))
+    stage = np.mean(np.array(stage), axis=0)
+
+    V, M = ctx.valid_counts()
+    keys, votes = ctx.all_bins()
+    n_votes = int(votes.sum())
+    aff = ctx.affine_result() if run_affine else None
+    idx1, d1, d2, good = ctx.match_result()
+
+    pairs = float(world) * nq * n_shard
+    value = pairs / (ms_per_step / 1000.0)
+    achieved = FLOP_PER_PAIR * nq * n_shard / (match_ms / 1000.0) / 1e12
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (seeded SIFT-like uint8 descriptors, SURVEY.md §8(d))",
+        "config": {"workload": "%s: %d query x %d DB/GPU (total %d) + Hough %s%s" % (
+            a.config.upper(), nq, n_shard, world * n_shard, "x".join(map(str, bins)),
+            " + affine verify" if run_affine else ""),
+            "queries": nq, "db_rows_per_gpu": n_shard, "db_rows_total": world * n_shard,
+            "bins": list(bins), "parallelism": "db-shard%d" % world},
+        "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
+        "hough_votes": n_votes,
+        "good_matches": int(good.sum()),
+        "valid_bins": V,
+        "surviving_bins": int(aff["survived"].sum()) if aff else None,
+        "stage_ms": {"match_kernel": match_ms, "merge_gather_ratio": float(stage[1]),
+                     "hough_vote": float(stage[2]), "select": float(stage[3]),
+                     "affine": float(stage[4])},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
+                     "kernel": "match_kernel",
+                     "algorithmic": "256 flop/pair x %d x %d pairs per launch" % (nq, n_shard)},
+        "exact_order": ctx.exact_order(),
+        "datagen_s": gen_s,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(qs.des, shard, a.cpu_queries)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        D.dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

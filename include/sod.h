@@ -1,0 +1,160 @@
+/*
+ * sod.h -- C ABI of libsod.so, the MI355X-native hot path of torn8to/sift-based-OD.
+ *
+ * Path (BASELINE.json north_star):
+ *   brute-force SIFT matching k=2 + Lowe ratio  -> generalized-Hough pose-bin voting
+ *   -> per-bin affine least-squares verification with outlier rejection.
+ *
+ * The reference has no FFI: its boundary is Python calls (main.py:6-11 `from X import *`)
+ * plus OpenCV.  Each entry point below names the reference interface it replaces; the
+ * Python package sift-based-od_amd/ binds them with ctypes.
+ *
+ * Conventions
+ *   - Every function returns int status: SOD_OK (0) or a SOD_E* code; the message is
+ *     available from sod_last_error(ctx).  Nothing aborts.
+ *   - Host pointers are borrowed for the duration of the call, C-contiguous.
+ *   - Device memory is owned by the ctx.  "enqueue" functions only enqueue work on the
+ *     ctx's HIP stream; "get" functions synchronise the stream and copy to the host.
+ *   - One ctx = one GPU = one host thread.  Multi-GPU = one process per GPU, each with
+ *     its own ctx, joined by sod_comm_init (RCCL over xGMI).
+ *   - Descriptors must be integer valued in [0,255] (OpenCV SIFT); float input is
+ *     validated on the device and rejected otherwise (SOD_EINVAL).
+ */
+#ifndef SOD_H
+#define SOD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SOD_OK 0
+#define SOD_EINVAL 1   /* bad argument / invalid descriptor values            */
+#define SOD_EHIP 2     /* HIP runtime error                                    */
+#define SOD_ENOMEM 3   /* device allocation failed                             */
+#define SOD_ESTATE 4   /* call out of order (e.g. hough before match)          */
+#define SOD_ECOMM 5    /* RCCL error / communicator missing                    */
+
+#define SOD_DTYPE_U8 0
+#define SOD_DTYPE_F32 1
+
+#define SOD_UNIQUE_ID_BYTES 128
+
+typedef struct sod_ctx sod_ctx;
+
+/* ---- lifetime --------------------------------------------------------------------- */
+int sod_abi_version(void);
+int sod_create(int device, sod_ctx** out);
+void sod_destroy(sod_ctx* ctx);
+const char* sod_last_error(const sod_ctx* ctx);
+int sod_synchronize(sod_ctx* ctx);
+/* Kernel timing of the last enqueued matcher launch (ms), measured with HIP events on
+ * the ctx stream; and the launch geometry used. */
+int sod_last_match_ms(sod_ctx* ctx, float* ms);
+int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n); /* match,merge,hough,select,affine */
+
+/* ---- database (replaces main.py:36-66 flattening + GenerateDatabaseInfo.py format) --
+ * Keypoints and the per-image table cover the WHOLE database (replicated on every
+ * rank); descriptors may be a shard: rows [row_offset, row_offset + n) of it. */
+int sod_db_set_keypoints(sod_ctx* ctx, int64_t n_total, const float* x, const float* y,
+                         const float* angle, const int32_t* octave, const int32_t* img,
+                         int32_t n_images, const double* centroid /* [n_images*2] */,
+                         const int32_t* size /* [n_images*2] (w,h) */);
+int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t n,
+                              int64_t row_offset);
+
+/* ---- query image features (replaces main.py:43 detectAndCompute output) ---------- */
+int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq,
+                     const float* x, const float* y, const float* angle,
+                     const int32_t* octave);   /* des may be NULL: keypoints only */
+
+/* ---- A1/A2: cv2.BFMatcher().knnMatch(des_query, des, k=2) + ratio test ------------
+ * main.py:70-86.  enqueue: local shard top-2 (exact squared distances), merged over
+ * this ctx's descriptor shard. */
+int sod_match_enqueue(sod_ctx* ctx);
+/* multi-GPU: RCCL all-gather of every rank's per-query (d1^2, idx1, d2^2) and the
+ * global merge.  No-op on a single rank. */
+int sod_match_allgather_enqueue(sod_ctx* ctx);
+/* ratio test on the merged top-2: good = (double)d1 < ratio * (double)d2 (main.py:82). */
+int sod_ratio_enqueue(sod_ctx* ctx, double ratio);
+int sod_match_get(sod_ctx* ctx, int32_t* idx1, float* d1, float* d2, uint8_t* good);
+/* Set the match state directly (Main.matching_keypoints assigned by the caller,
+ * main.py:29,85): idx1[q] = trainIdx (global row), good[q] = keep.  nq must equal the
+ * uploaded query count.  Hough/select/affine then run on these matches. */
+int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t* good);
+/* 1 if every distance is provably < 2048 (sqrtf then injective on the squared
+ * distances, so squared-distance ordering == OpenCV's float ordering), else 0. */
+int sod_match_exact_order(sod_ctx* ctx, int* exact);
+
+/* ---- A5-A8: estimate_object_pose / calculate_bin_index / vote loop / PoseBin -------
+ * HoughTransformHelperFunctions.py:4-72, main.py:89-119, PoseBin.py:6-51.
+ * query_shape = rgb_query.shape[:2] = (H, W).  bins[4] = (x, y, theta, sigma) bins,
+ * each in [1,255] (the live code passes one scalar for all four).  Votes are cast only
+ * for good matches whose idx1 lies in [own_lo, own_hi) (this rank's shard). */
+int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int32_t bins[4],
+                      int64_t own_lo, int64_t own_hi);
+/* multi-GPU: RCCL all-reduce (sum) of the partial bin counts and (min) of the
+ * first-touch ordinals.  No-op on a single rank. */
+int sod_hough_allreduce_enqueue(sod_ctx* ctx);
+/* A10: bins with votes >= threshold in first-touch (dict insertion) order
+ * (main.py:121-132), their member lists in match order, and the PoseBin running means
+ * (centroid x,y, angle, scale, img_size w,h) in vote order. */
+int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold);
+int sod_valid_counts(sod_ctx* ctx, int64_t* n_valid, int64_t* n_members);
+int sod_valid_get(sod_ctx* ctx, int32_t* keys /* [V*4] */, int32_t* votes /* [V] */,
+                  int64_t* offsets /* [V+1] */, int32_t* members /* [M] query idx */,
+                  double* means /* [V*6] */);
+/* all occupied bins (counts), first-touch order: keys[B*4], votes[B] */
+int sod_bins_count(sod_ctx* ctx, int64_t* n_bins);
+int sod_bins_get(sod_ctx* ctx, int32_t* keys, int32_t* votes);
+
+/* ---- A11-A13: AffineParameters / remove_outliers / apply_affine_parameters -------
+ * AffineParameters.py:89-160, main.py:139-157: per valid bin, fixed point of
+ * {x = pinv(A^T A) A^T b ; drop members with |residual| > W*pose[3]/xf (x) or
+ *  H*pose[3]/yf (y)} until nothing is dropped; survivors keep votes >= threshold. */
+int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_factor,
+                       double y_factor, int32_t threshold);
+int sod_affine_get(sod_ctx* ctx, uint8_t* survived /* [V] */, int32_t* votes /* [V] */,
+                   double* params /* [V*6] m1,m2,m3,m4,tx,ty */,
+                   uint8_t* member_alive /* [M] */);
+
+/* ---- whole pipeline on one stream (bench / Main fast path) ------------------------ */
+typedef struct sod_pipeline_args {
+  double ratio;           /* 0.75  main.py:82            */
+  int32_t query_h, query_w;
+  int32_t bins[4];        /* 15,15,15,15 main.py:183      */
+  int32_t vote_threshold; /* 5     main.py:184            */
+  int32_t affine_threshold; /* 4   main.py:185            */
+  double x_factor, y_factor; /* 128 = pos_factor*4 main.py:141,150 */
+  int32_t run_affine;
+} sod_pipeline_args;
+int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* args);
+
+/* ---- stateless batch forms of the per-item reference functions -------------------- */
+/* estimate_object_pose + calculate_bin_index for n (model kp, query kp, centroid)
+ * triples: pose[n*4] = (x, y, alpha, scale_factor), idx[n*4] = (ix, iy, itheta, isigma). */
+int sod_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
+                   const float* mangle, const int32_t* moctave, const float* qx,
+                   const float* qy, const float* qangle, const int32_t* qoctave,
+                   const double* cx, const double* cy, int32_t query_h, int32_t query_w,
+                   const int32_t bins[4], double* pose, int32_t* idx);
+/* AffineParameters + remove_outliers fixed point for host-provided bins (CSR):
+ * model/query points per member (f32, as cv2.KeyPoint.pt), i_sigma = pose[3] per bin.
+ * max_iter = 1 runs exactly one {AffineParameters; remove_outliers} round. */
+int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets,
+                     const float* mx, const float* my, const float* qx, const float* qy,
+                     const int32_t* i_sigma, int32_t query_w, int32_t query_h,
+                     double x_factor, double y_factor, int32_t threshold, int32_t max_iter,
+                     uint8_t* survived, int32_t* votes, double* params,
+                     uint8_t* member_alive);
+
+/* ---- multi-GPU (RCCL over xGMI) --------------------------------------------------- */
+int sod_comm_unique_id(uint8_t out[SOD_UNIQUE_ID_BYTES]);
+int sod_comm_init(sod_ctx* ctx, int32_t nranks, int32_t rank,
+                  const uint8_t id[SOD_UNIQUE_ID_BYTES]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SOD_H */

@@ -1,0 +1,386 @@
+"""ctypes binding of libsod.so (C ABI declared in include/sod.h).
+
+Loading fails loudly: there is no CPU fallback anywhere in this package.  Build the
+library with ``__graft_entry__.build()`` (or ``make -C sift-based-od_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsod.so")
+
+SOD_OK, SOD_EINVAL, SOD_EHIP, SOD_ENOMEM, SOD_ESTATE, SOD_ECOMM = range(6)
+DTYPE_U8, DTYPE_F32 = 0, 1
+UNIQUE_ID_BYTES = 128
+
+_ERRNAMES = {SOD_EINVAL: "EINVAL", SOD_EHIP: "EHIP", SOD_ENOMEM: "ENOMEM",
+             SOD_ESTATE: "ESTATE", SOD_ECOMM: "ECOMM"}
+
+c_f32p = C.POINTER(C.c_float)
+c_f64p = C.POINTER(C.c_double)
+c_i32p = C.POINTER(C.c_int32)
+c_i64p = C.POINTER(C.c_int64)
+c_u8p = C.POINTER(C.c_uint8)
+c_vp = C.c_void_p
+c_ctx = C.c_void_p
+
+
+class PipelineArgs(C.Structure):
+    _fields_ = [("ratio", C.c_double), ("query_h", C.c_int32), ("query_w", C.c_int32),
+                ("bins", C.c_int32 * 4), ("vote_threshold", C.c_int32),
+                ("affine_threshold", C.c_int32), ("x_factor", C.c_double),
+                ("y_factor", C.c_double), ("run_affine", C.c_int32)]
+
+
+# name -> (restype, argtypes); must mirror include/sod.h exactly (tests check the symbols)
+SIGNATURES = {
+    "sod_abi_version": (C.c_int, []),
+    "sod_create": (C.c_int, [C.c_int, C.POINTER(c_ctx)]),
+    "sod_destroy": (None, [c_ctx]),
+    "sod_last_error": (C.c_char_p, [c_ctx]),
+    "sod_synchronize": (C.c_int, [c_ctx]),
+    "sod_last_match_ms": (C.c_int, [c_ctx, c_f32p]),
+    "sod_last_stage_ms": (C.c_int, [c_ctx, c_f32p, C.c_int]),
+    "sod_db_set_keypoints": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_i32p,
+                                       C.c_int32, c_f64p, c_i32p]),
+    "sod_db_upload_descriptors": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int64, C.c_int64]),
+    "sod_query_upload": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int32, c_f32p, c_f32p, c_f32p,
+                                   c_i32p]),
+    "sod_match_enqueue": (C.c_int, [c_ctx]),
+    "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
+    "sod_ratio_enqueue": (C.c_int, [c_ctx, C.c_double]),
+    "sod_match_get": (C.c_int, [c_ctx, c_i32p, c_f32p, c_f32p, c_u8p]),
+    "sod_matches_set": (C.c_int, [c_ctx, C.c_int32, c_i32p, c_u8p]),
+    "sod_match_exact_order": (C.c_int, [c_ctx, C.POINTER(C.c_int)]),
+    "sod_hough_enqueue": (C.c_int, [c_ctx, C.c_int32, C.c_int32, c_i32p, C.c_int64, C.c_int64]),
+    "sod_hough_allreduce_enqueue": (C.c_int, [c_ctx]),
+    "sod_select_enqueue": (C.c_int, [c_ctx, C.c_int32]),
+    "sod_valid_counts": (C.c_int, [c_ctx, c_i64p, c_i64p]),
+    "sod_valid_get": (C.c_int, [c_ctx, c_i32p, c_i32p, c_i64p, c_i32p, c_f64p]),
+    "sod_bins_count": (C.c_int, [c_ctx, c_i64p]),
+    "sod_bins_get": (C.c_int, [c_ctx, c_i32p, c_i32p]),
+    "sod_affine_enqueue": (C.c_int, [c_ctx, C.c_int32, C.c_int32, C.c_double, C.c_double,
+                                     C.c_int32]),
+    "sod_affine_get": (C.c_int, [c_ctx, c_u8p, c_i32p, c_f64p, c_u8p]),
+    "sod_pipeline_enqueue": (C.c_int, [c_ctx, C.POINTER(PipelineArgs)]),
+    "sod_pose_batch": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_f32p, c_f32p,
+                                 c_f32p, c_i32p, c_f64p, c_f64p, C.c_int32, C.c_int32, c_i32p,
+                                 c_f64p, c_i32p]),
+    "sod_affine_batch": (C.c_int, [c_ctx, C.c_int64, c_i64p, c_f32p, c_f32p, c_f32p, c_f32p,
+                                   c_i32p, C.c_int32, C.c_int32, C.c_double, C.c_double,
+                                   C.c_int32, C.c_int32, c_u8p, c_i32p, c_f64p, c_u8p]),
+    "sod_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
+    "sod_comm_init": (C.c_int, [c_ctx, C.c_int32, C.c_int32, C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class SodError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libsod %s (%d): %s" % (_ERRNAMES.get(code, "?"), code, msg))
+        self.code = code
+
+
+def lib():
+    """The loaded libsod.so; raises if it is missing (no fallback)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    "libsod.so not found at %s -- build it with __graft_entry__.build() "
+                    "(hipcc --offload-arch=gfx950); this package has no CPU fallback" % LIB_PATH)
+            L = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+        return _lib
+
+
+def ptr(a, ctype):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def unique_id():
+    buf = (C.c_uint8 * UNIQUE_ID_BYTES)()
+    rc = lib().sod_comm_unique_id(C.byref(buf))
+    if rc != SOD_OK:
+        raise SodError(rc, lib().sod_last_error(None).decode())
+    return bytes(buf)
+
+
+class Context:
+    """One libsod context = one GPU (HIP device ``device``) driven by this thread."""
+
+    def __init__(self, device=0):
+        self._L = lib()
+        h = c_ctx()
+        rc = self._L.sod_create(int(device), C.byref(h))
+        if rc != SOD_OK:
+            raise SodError(rc, self._L.sod_last_error(None).decode())
+        self._h = h
+        self.device = device
+        self.nq = 0
+        self.n_total = 0
+        self.bins = None
+
+    # -- plumbing --
+    def _chk(self, rc):
+        if rc != SOD_OK:
+            raise SodError(rc, self._L.sod_last_error(self._h).decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.sod_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def synchronize(self):
+        self._chk(self._L.sod_synchronize(self._h))
+
+    # -- data --
+    def set_keypoints(self, kp, img, centroid, size):
+        self._kp_keep = (_c(kp.x, np.float32), _c(kp.y, np.float32), _c(kp.angle, np.float32),
+                         _c(kp.octave, np.int32), _c(img, np.int32),
+                         _c(centroid, np.float64).reshape(-1), _c(size, np.int32).reshape(-1))
+        x, y, a, o, im, ce, sz = self._kp_keep
+        self._chk(self._L.sod_db_set_keypoints(
+            self._h, len(x), ptr(x, C.c_float), ptr(y, C.c_float), ptr(a, C.c_float),
+            ptr(o, C.c_int32), ptr(im, C.c_int32), len(ce) // 2, ptr(ce, C.c_double),
+            ptr(sz, C.c_int32)))
+        self.n_total = len(x)
+        del self._kp_keep
+
+    @staticmethod
+    def _des(des):
+        des = np.asarray(des)
+        if des.ndim != 2 or des.shape[1] != 128:
+            raise ValueError("descriptors must be [N,128]")
+        if des.dtype == np.uint8:
+            return np.ascontiguousarray(des), DTYPE_U8
+        return np.ascontiguousarray(des, dtype=np.float32), DTYPE_F32
+
+    def upload_db(self, des, row_offset=0):
+        d, dt = self._des(des)
+        self._chk(self._L.sod_db_upload_descriptors(self._h, d.ctypes.data_as(c_vp), dt,
+                                                     d.shape[0], int(row_offset)))
+        self.n_shard = d.shape[0]
+        self.row_offset = int(row_offset)
+
+    def upload_queries(self, des, kp=None):
+        if des is None:
+            if kp is None:
+                raise ValueError("need descriptors or keypoints")
+            d, dt, n = None, DTYPE_U8, len(kp)
+        else:
+            d, dt = self._des(des)
+            n = d.shape[0]
+        if kp is not None:
+            x, y, a, o = (_c(kp.x, np.float32), _c(kp.y, np.float32), _c(kp.angle, np.float32),
+                          _c(kp.octave, np.int32))
+            if len(x) != n:
+                raise ValueError("query keypoints and descriptors differ in count")
+            args = (ptr(x, C.c_float), ptr(y, C.c_float), ptr(a, C.c_float), ptr(o, C.c_int32))
+        else:
+            args = (None, None, None, None)
+        self._chk(self._L.sod_query_upload(self._h, None if d is None else d.ctypes.data_as(c_vp),
+                                           dt, n, *args))
+        self.nq = n
+
+    def set_matches(self, idx1, good):
+        i = _c(idx1, np.int32)
+        g = _c(np.asarray(good).astype(np.uint8), np.uint8)
+        self._chk(self._L.sod_matches_set(self._h, len(i), ptr(i, C.c_int32), ptr(g, C.c_uint8)))
+
+    # -- stages --
+    def match(self):
+        self._chk(self._L.sod_match_enqueue(self._h))
+
+    def match_allgather(self):
+        self._chk(self._L.sod_match_allgather_enqueue(self._h))
+
+    def ratio(self, ratio=0.75):
+        self._chk(self._L.sod_ratio_enqueue(self._h, float(ratio)))
+
+    def match_result(self):
+        n = self.nq
+        idx1 = np.empty(n, np.int32)
+        d1 = np.empty(n, np.float32)
+        d2 = np.empty(n, np.float32)
+        good = np.empty(n, np.uint8)
+        self._chk(self._L.sod_match_get(self._h, ptr(idx1, C.c_int32), ptr(d1, C.c_float),
+                                        ptr(d2, C.c_float), ptr(good, C.c_uint8)))
+        return idx1, d1, d2, good.astype(bool)
+
+    def exact_order(self):
+        v = C.c_int()
+        self._chk(self._L.sod_match_exact_order(self._h, C.byref(v)))
+        return bool(v.value)
+
+    def hough(self, query_shape, bins, own=None):
+        b = np.ascontiguousarray(bins4(bins), np.int32)
+        lo, hi = own if own is not None else (0, self.n_total)
+        self._chk(self._L.sod_hough_enqueue(self._h, int(query_shape[0]), int(query_shape[1]),
+                                            ptr(b, C.c_int32), int(lo), int(hi)))
+        self.bins = tuple(int(v) for v in b)
+
+    def hough_allreduce(self):
+        self._chk(self._L.sod_hough_allreduce_enqueue(self._h))
+
+    def select(self, vote_threshold=5):
+        self._chk(self._L.sod_select_enqueue(self._h, int(vote_threshold)))
+
+    def valid_counts(self):
+        v, m = C.c_int64(), C.c_int64()
+        self._chk(self._L.sod_valid_counts(self._h, C.byref(v), C.byref(m)))
+        return v.value, m.value
+
+    def valid_result(self):
+        V, M = self.valid_counts()
+        keys = np.empty((V, 4), np.int32)
+        votes = np.empty(V, np.int32)
+        off = np.empty(V + 1, np.int64)
+        mem = np.empty(M, np.int32)
+        means = np.empty((V, 6), np.float64)
+        self._chk(self._L.sod_valid_get(self._h, ptr(keys, C.c_int32), ptr(votes, C.c_int32),
+                                        ptr(off, C.c_int64), ptr(mem, C.c_int32),
+                                        ptr(means, C.c_double)))
+        return {"keys": keys, "votes": votes, "offsets": off, "members": mem, "means": means}
+
+    def all_bins(self):
+        n = C.c_int64()
+        self._chk(self._L.sod_bins_count(self._h, C.byref(n)))
+        keys = np.empty((n.value, 4), np.int32)
+        votes = np.empty(n.value, np.int32)
+        self._chk(self._L.sod_bins_get(self._h, ptr(keys, C.c_int32), ptr(votes, C.c_int32)))
+        return keys, votes
+
+    def affine(self, query_size, x_factor=128.0, y_factor=128.0, threshold=4):
+        self._chk(self._L.sod_affine_enqueue(self._h, int(query_size[0]), int(query_size[1]),
+                                             float(x_factor), float(y_factor), int(threshold)))
+
+    def affine_result(self):
+        V, M = self.valid_counts()
+        surv = np.empty(V, np.uint8)
+        votes = np.empty(V, np.int32)
+        params = np.empty((V, 6), np.float64)
+        alive = np.empty(M, np.uint8)
+        self._chk(self._L.sod_affine_get(self._h, ptr(surv, C.c_uint8), ptr(votes, C.c_int32),
+                                         ptr(params, C.c_double), ptr(alive, C.c_uint8)))
+        return {"survived": surv.astype(bool), "votes": votes, "params": params,
+                "alive": alive.astype(bool)}
+
+    def pipeline(self, query_shape, bins=15, ratio=0.75, vote_threshold=5, affine_threshold=4,
+                 x_factor=128.0, y_factor=128.0, run_affine=True):
+        a = PipelineArgs()
+        a.ratio = float(ratio)
+        a.query_h, a.query_w = int(query_shape[0]), int(query_shape[1])
+        for i, v in enumerate(bins4(bins)):
+            a.bins[i] = int(v)
+        a.vote_threshold = int(vote_threshold)
+        a.affine_threshold = int(affine_threshold)
+        a.x_factor, a.y_factor = float(x_factor), float(y_factor)
+        a.run_affine = 1 if run_affine else 0
+        self._chk(self._L.sod_pipeline_enqueue(self._h, C.byref(a)))
+        self.bins = bins4(bins)
+
+    def last_match_ms(self):
+        v = C.c_float()
+        self._chk(self._L.sod_last_match_ms(self._h, C.byref(v)))
+        return v.value
+
+    def stage_ms(self):
+        out = np.zeros(5, np.float32)
+        self._chk(self._L.sod_last_stage_ms(self._h, ptr(out, C.c_float), 5))
+        return out
+
+    # -- stateless batch forms --
+    def pose_batch(self, mx, my, mang, moct, qx, qy, qang, qoct, cx, cy, query_shape, bins):
+        arr = [_c(mx, np.float32), _c(my, np.float32), _c(mang, np.float32), _c(moct, np.int32),
+               _c(qx, np.float32), _c(qy, np.float32), _c(qang, np.float32), _c(qoct, np.int32),
+               _c(cx, np.float64), _c(cy, np.float64)]
+        n = len(arr[0])
+        if any(len(a) != n for a in arr):
+            raise ValueError("pose_batch arrays differ in length")
+        b = np.ascontiguousarray(bins4(bins), np.int32)
+        pose = np.empty((n, 4), np.float64)
+        idx = np.empty((n, 4), np.int32)
+        ct = [C.c_float, C.c_float, C.c_float, C.c_int32, C.c_float, C.c_float, C.c_float,
+              C.c_int32, C.c_double, C.c_double]
+        self._chk(self._L.sod_pose_batch(self._h, n, *[ptr(a, t) for a, t in zip(arr, ct)],
+                                         int(query_shape[0]), int(query_shape[1]),
+                                         ptr(b, C.c_int32), ptr(pose, C.c_double),
+                                         ptr(idx, C.c_int32)))
+        return pose, idx
+
+    def affine_batch(self, offsets, mx, my, qx, qy, i_sigma, query_size, x_factor=128.0,
+                     y_factor=128.0, threshold=4, max_iter=1 << 30):
+        off = _c(offsets, np.int64)
+        nb = len(off) - 1
+        pts = [_c(v, np.float32) for v in (mx, my, qx, qy)]
+        isg = _c(i_sigma, np.int32)
+        M = int(off[-1]) if nb >= 0 else 0
+        surv = np.empty(nb, np.uint8)
+        votes = np.empty(nb, np.int32)
+        params = np.empty((nb, 6), np.float64)
+        alive = np.empty(M, np.uint8)
+        self._chk(self._L.sod_affine_batch(
+            self._h, nb, ptr(off, C.c_int64), *[ptr(p, C.c_float) for p in pts],
+            ptr(isg, C.c_int32), int(query_size[0]), int(query_size[1]), float(x_factor),
+            float(y_factor), int(threshold), int(max_iter), ptr(surv, C.c_uint8),
+            ptr(votes, C.c_int32), ptr(params, C.c_double), ptr(alive, C.c_uint8)))
+        return {"survived": surv.astype(bool), "votes": votes, "params": params,
+                "alive": alive.astype(bool)}
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (C.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        self._chk(self._L.sod_comm_init(self._h, int(nranks), int(rank), C.byref(buf)))
+
+
+def bins4(bins):
+    """``bins`` as the live code passes it (one int, main.py:183) or per axis
+    (x, y, theta, sigma) following ``HoughTransform.py:8``."""
+    if isinstance(bins, (tuple, list, np.ndarray)):
+        b = tuple(int(v) for v in bins)
+        if len(b) != 4:
+            raise ValueError("bins must be an int or a 4-tuple (x, y, theta, sigma)")
+        return b
+    b = int(bins)
+    return (b, b, b, b)
+
+
+_default = {}
+
+
+def default_context(device=0):
+    """Process-wide context for the drop-in functions (one per device)."""
+    ctx = _default.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _default[device] = ctx
+    return ctx

@@ -1,0 +1,599 @@
+// api.hip -- extern "C" entry points of libsod.so (declared in include/sod.h).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "sod_internal.h"
+
+int sod_fail(sod_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+namespace {
+thread_local std::string g_err;  // errors before a ctx exists
+
+int set_dev(sod_ctx* ctx) {
+  if (!ctx) return SOD_EINVAL;
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  return SOD_OK;
+}
+
+template <typename T>
+int upload(sod_ctx* ctx, DevBuf<T>& b, const T* src, size_t n) {
+  SOD_TRY(sod_reserve(ctx, b, n));
+  if (n) SOD_HIP(ctx, hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  return SOD_OK;
+}
+
+template <typename T>
+int download(sod_ctx* ctx, T* dst, const T* src, size_t n) {
+  if (n && dst) SOD_HIP(ctx, hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+  return SOD_OK;
+}
+
+int check_bins(sod_ctx* ctx, const int32_t bins[4]) {
+  for (int i = 0; i < 4; ++i)
+    if (bins[i] < 1 || bins[i] > 255)
+      return sod_fail(ctx, SOD_EINVAL, "bins must be in [1,255] per axis");
+  const int64_t nb = (int64_t)bins[0] * bins[1] * bins[2] * bins[3];
+  const bool changed_sigma = bins[3] != ctx->bins[3] || !ctx->sig_lut.p;
+  std::memcpy(ctx->bins, bins, sizeof(ctx->bins));
+  ctx->nbins = nb;
+  if (changed_sigma) SOD_TRY(sod_build_sigma_lut(ctx, bins[3]));
+  return SOD_OK;
+}
+
+int flags_reset(sod_ctx* ctx) {
+  SOD_TRY(sod_reserve(ctx, ctx->flags, 4));
+  return SOD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int sod_abi_version(void) { return 1; }
+
+int sod_create(int device, sod_ctx** out) {
+  if (!out) return SOD_EINVAL;
+  *out = nullptr;
+  sod_ctx* ctx = new sod_ctx();
+  ctx->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) {
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
+  }
+  for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
+  if (e != hipSuccess) {
+    g_err = std::string("sod_create: ") + hipGetErrorString(e);
+    delete ctx;
+    return SOD_EHIP;
+  }
+  if (sod_reserve(ctx, ctx->flags, 4) != SOD_OK ||
+      hipMemsetAsync(ctx->flags.p, 0, 16, ctx->stream) != hipSuccess) {
+    g_err = ctx->err;
+    sod_destroy(ctx);
+    return SOD_ENOMEM;
+  }
+  *out = ctx;
+  return SOD_OK;
+}
+
+void sod_destroy(sod_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  sod_release(ctx->mx); sod_release(ctx->my); sod_release(ctx->mang);
+  sod_release(ctx->moct); sod_release(ctx->mimg); sod_release(ctx->cent); sod_release(ctx->isize);
+  sod_release(ctx->dbpack); sod_release(ctx->dn); sod_release(ctx->qpack); sod_release(ctx->qn);
+  sod_release(ctx->qx); sod_release(ctx->qy); sod_release(ctx->qang); sod_release(ctx->qoct);
+  sod_release(ctx->stage_u8); sod_release(ctx->stage_f32);
+  sod_release(ctx->pd1); sod_release(ctx->pd2); sod_release(ctx->pidx);
+  sod_release(ctx->cd1); sod_release(ctx->cd2); sod_release(ctx->cidx);
+  sod_release(ctx->gd1); sod_release(ctx->gd2); sod_release(ctx->gidx);
+  sod_release(ctx->d1); sod_release(ctx->d2); sod_release(ctx->idx1); sod_release(ctx->good);
+  sod_release(ctx->flags); sod_release(ctx->sig_lut); sod_release(ctx->counts);
+  sod_release(ctx->first); sod_release(ctx->basekey); sod_release(ctx->vmask);
+  sod_release(ctx->pose); sod_release(ctx->blk); sod_release(ctx->scal); sod_release(ctx->vbin);
+  sod_release(ctx->voff); sod_release(ctx->members); sod_release(ctx->means);
+  sod_release(ctx->allbin); sod_release(ctx->amx); sod_release(ctx->amy); sod_release(ctx->aqx);
+  sod_release(ctx->aqy); sod_release(ctx->aisig); sod_release(ctx->surv);
+  sod_release(ctx->fvotes); sod_release(ctx->params); sod_release(ctx->alive);
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* sod_last_error(const sod_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_err.c_str();
+}
+
+int sod_synchronize(sod_ctx* ctx) {
+  SOD_TRY(set_dev(ctx));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return SOD_OK;
+}
+
+int sod_last_match_ms(sod_ctx* ctx, float* ms) {
+  SOD_TRY(set_dev(ctx));
+  if (!ms) return sod_fail(ctx, SOD_EINVAL, "null output");
+  if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "no matcher launch yet");
+  SOD_HIP(ctx, hipEventSynchronize(ctx->ev[1]));
+  SOD_HIP(ctx, hipEventElapsedTime(ms, ctx->ev[0], ctx->ev[1]));
+  return SOD_OK;
+}
+
+int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n) {
+  // [match kernel, merge+allgather+ratio, hough vote (+allreduce), select, affine]
+  SOD_TRY(set_dev(ctx));
+  if (!ms_out) return sod_fail(ctx, SOD_EINVAL, "null output");
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const bool rec[6] = {ctx->matched, ctx->matched, ctx->houghed, ctx->houghed, ctx->selected,
+                       ctx->affined};
+  for (int i = 0; i < n && i < 5; ++i) {
+    float ms = 0.f;
+    if (rec[i] && rec[i + 1] && hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) != hipSuccess)
+      ms = 0.f;
+    ms_out[i] = ms;
+  }
+  return SOD_OK;
+}
+
+// ---- database -------------------------------------------------------------------------
+int sod_db_set_keypoints(sod_ctx* ctx, int64_t n_total, const float* x, const float* y,
+                         const float* angle, const int32_t* octave, const int32_t* img,
+                         int32_t n_images, const double* centroid, const int32_t* size) {
+  SOD_TRY(set_dev(ctx));
+  if (n_total < 0 || n_images < 1 || !x || !y || !angle || !octave || !img || !centroid || !size)
+    return sod_fail(ctx, SOD_EINVAL, "sod_db_set_keypoints: bad arguments");
+  for (int64_t i = 0; i < n_total; ++i)
+    if (img[i] < 0 || img[i] >= n_images)
+      return sod_fail(ctx, SOD_EINVAL, "keypoint image id out of range");
+  SOD_TRY(upload(ctx, ctx->mx, x, (size_t)n_total));
+  SOD_TRY(upload(ctx, ctx->my, y, (size_t)n_total));
+  SOD_TRY(upload(ctx, ctx->mang, angle, (size_t)n_total));
+  SOD_TRY(upload(ctx, ctx->moct, octave, (size_t)n_total));
+  SOD_TRY(upload(ctx, ctx->mimg, img, (size_t)n_total));
+  SOD_TRY(upload(ctx, ctx->cent, centroid, (size_t)n_images * 2));
+  SOD_TRY(upload(ctx, ctx->isize, size, (size_t)n_images * 2));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->n_total = n_total;
+  ctx->n_images = n_images;
+  return SOD_OK;
+}
+
+static int upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t n, bool db) {
+  if (!des || n < 0 || (dtype != SOD_DTYPE_U8 && dtype != SOD_DTYPE_F32))
+    return sod_fail(ctx, SOD_EINVAL, "bad descriptor arguments");
+  const size_t elems = (size_t)n * kDim;
+  const void* dsrc;
+  if (dtype == SOD_DTYPE_U8) {
+    SOD_TRY(upload(ctx, ctx->stage_u8, (const uint8_t*)des, elems));
+    dsrc = ctx->stage_u8.p;
+  } else {
+    SOD_TRY(upload(ctx, ctx->stage_f32, (const float*)des, elems));
+    dsrc = ctx->stage_f32.p;
+  }
+  SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p, 0, 4, ctx->stream));  // invalid count
+  if (db)
+    SOD_TRY(launch_pack_db(ctx, dsrc, dtype, n));
+  else
+    SOD_TRY(launch_pack_queries(ctx, dsrc, dtype, (int32_t)n));
+  uint32_t bad = 0;
+  SOD_HIP(ctx, hipMemcpyAsync(&bad, ctx->flags.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // staging is only needed during the upload
+  if (dtype == SOD_DTYPE_U8) sod_release(ctx->stage_u8); else sod_release(ctx->stage_f32);
+  if (bad)
+    return sod_fail(ctx, SOD_EINVAL, std::to_string(bad) +
+                                         " descriptor chunk(s) hold values that are not integers in "
+                                         "[0,255] (OpenCV SIFT descriptors are)");
+  return SOD_OK;
+}
+
+int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t n,
+                              int64_t row_offset) {
+  SOD_TRY(set_dev(ctx));
+  if (n < 1 || row_offset < 0 || row_offset + n > (int64_t)0x7fffffff)
+    return sod_fail(ctx, SOD_EINVAL, "descriptor rows out of range");
+  SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p + 1, 0, 4, ctx->stream));
+  SOD_TRY(upload_descriptors(ctx, des, dtype, n, true));
+  ctx->n_shard = n;
+  ctx->row_offset = row_offset;
+  ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq, const float* x,
+                     const float* y, const float* angle, const int32_t* octave) {
+  SOD_TRY(set_dev(ctx));
+  if (nq < 1 || nq > (1 << 27)) return sod_fail(ctx, SOD_EINVAL, "query count out of range");
+  if (des) {
+    SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p + 2, 0, 4, ctx->stream));
+    SOD_TRY(upload_descriptors(ctx, des, dtype, nq, false));
+  } else {
+    ctx->nqt = 0;  // keypoints only: hough on externally set matches
+  }
+  ctx->nq = nq;
+  if (x && y && angle && octave) {
+    SOD_TRY(upload(ctx, ctx->qx, x, (size_t)nq));
+    SOD_TRY(upload(ctx, ctx->qy, y, (size_t)nq));
+    SOD_TRY(upload(ctx, ctx->qang, angle, (size_t)nq));
+    SOD_TRY(upload(ctx, ctx->qoct, octave, (size_t)nq));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+// ---- matcher --------------------------------------------------------------------------
+int sod_match_enqueue(sod_ctx* ctx) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
+  if (ctx->nranks == 1 && ctx->n_shard < 2)
+    return sod_fail(ctx, SOD_EINVAL, "knnMatch(k=2) needs at least 2 train descriptors");
+  SOD_TRY(launch_match(ctx));
+  ctx->matched = true;
+  ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_match_allgather_enqueue(sod_ctx* ctx) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
+  if (ctx->nranks <= 1) return SOD_OK;
+  if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
+  const size_t nq_pad = (size_t)ctx->nqt * kSubRows;
+  const size_t tot = nq_pad * ctx->nranks;
+  SOD_TRY(sod_reserve(ctx, ctx->gd1, tot));
+  SOD_TRY(sod_reserve(ctx, ctx->gd2, tot));
+  SOD_TRY(sod_reserve(ctx, ctx->gidx, tot));
+  ncclResult_t r = ncclGroupStart();
+  if (r == ncclSuccess) r = ncclAllGather(ctx->cd1.p, ctx->gd1.p, nq_pad, ncclFloat32, ctx->comm, ctx->stream);
+  if (r == ncclSuccess) r = ncclAllGather(ctx->cidx.p, ctx->gidx.p, nq_pad, ncclInt32, ctx->comm, ctx->stream);
+  if (r == ncclSuccess) r = ncclAllGather(ctx->cd2.p, ctx->gd2.p, nq_pad, ncclFloat32, ctx->comm, ctx->stream);
+  ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return sod_fail(ctx, SOD_ECOMM, std::string("ncclAllGather: ") +
+                                        ncclGetErrorString(r != ncclSuccess ? r : r2));
+  // global merge in rank order (lexicographic on (d^2, trainIdx): order-independent anyway)
+  return launch_merge(ctx, ctx->gd1.p, ctx->gidx.p, ctx->gd2.p, ctx->nranks, (int64_t)nq_pad);
+}
+
+int sod_ratio_enqueue(sod_ctx* ctx, double ratio) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
+  SOD_TRY(launch_ratio(ctx, ratio));
+  ctx->ratio_done = true;
+  return SOD_OK;
+}
+
+int sod_match_get(sod_ctx* ctx, int32_t* idx1, float* d1, float* d2, uint8_t* good) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "sod_ratio_enqueue first");
+  const size_t n = (size_t)ctx->nq;
+  SOD_TRY(download(ctx, idx1, ctx->idx1.p, n));
+  SOD_TRY(download(ctx, d1, ctx->d1.p, n));
+  SOD_TRY(download(ctx, d2, ctx->d2.p, n));
+  SOD_TRY(download(ctx, good, ctx->good.p, n));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return SOD_OK;
+}
+
+int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t* good) {
+  SOD_TRY(set_dev(ctx));
+  if (!idx1 || !good || nq != ctx->nq || nq < 1)
+    return sod_fail(ctx, SOD_EINVAL, "sod_matches_set: nq must equal the uploaded query count");
+  for (int32_t q = 0; q < nq; ++q)
+    if (good[q] && (idx1[q] < 0 || idx1[q] >= ctx->n_total))
+      return sod_fail(ctx, SOD_EINVAL, "sod_matches_set: trainIdx out of range");
+  SOD_TRY(upload(ctx, ctx->idx1, idx1, (size_t)nq));
+  SOD_TRY(upload(ctx, ctx->good, good, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->d1, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->d2, (size_t)nq));
+  SOD_HIP(ctx, hipMemsetAsync(ctx->d1.p, 0, (size_t)nq * 4, ctx->stream));
+  SOD_HIP(ctx, hipMemsetAsync(ctx->d2.p, 0, (size_t)nq * 4, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->matched = ctx->ratio_done = true;
+  ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_match_exact_order(sod_ctx* ctx, int* exact) {
+  SOD_TRY(set_dev(ctx));
+  uint32_t f[4];
+  SOD_HIP(ctx, hipMemcpyAsync(f, ctx->flags.p, 16, hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  float dn, qn;
+  std::memcpy(&dn, &f[1], 4);
+  std::memcpy(&qn, &f[2], 4);
+  // every distance <= |q| + |d| <= 2048  =>  squared distances <= 2^22, where distinct
+  // integers have distinct correctly rounded float square roots
+  *exact = (std::sqrt((double)dn) + std::sqrt((double)qn) <= 2048.0) ? 1 : 0;
+  return SOD_OK;
+}
+
+// ---- hough ----------------------------------------------------------------------------
+int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int32_t bins[4],
+                      int64_t own_lo, int64_t own_hi) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "match + ratio first");
+  if (!ctx->n_total || !ctx->qx.p) return sod_fail(ctx, SOD_ESTATE, "keypoints not uploaded");
+  if (query_h < 1 || query_w < 1) return sod_fail(ctx, SOD_EINVAL, "bad query image shape");
+  SOD_TRY(check_bins(ctx, bins));
+  ctx->qh = query_h;
+  ctx->qw = query_w;
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+  SOD_TRY(launch_hough(ctx, own_lo, own_hi));
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+  ctx->houghed = true;
+  ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_hough_allreduce_enqueue(sod_ctx* ctx) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  if (ctx->nranks <= 1) return SOD_OK;
+  if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
+  ncclResult_t r = ncclGroupStart();
+  if (r == ncclSuccess)
+    r = ncclAllReduce(ctx->counts.p, ctx->counts.p, ctx->nbins, ncclUint32, ncclSum, ctx->comm, ctx->stream);
+  if (r == ncclSuccess)
+    r = ncclAllReduce(ctx->first.p, ctx->first.p, ctx->nbins, ncclUint32, ncclMin, ctx->comm, ctx->stream);
+  ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return sod_fail(ctx, SOD_ECOMM, std::string("ncclAllReduce: ") +
+                                        ncclGetErrorString(r != ncclSuccess ? r : r2));
+  return SOD_OK;
+}
+
+int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  SOD_TRY(launch_select(ctx, vote_threshold));
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+  ctx->vote_thr = vote_threshold;
+  ctx->selected = true;
+  ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_valid_counts(sod_ctx* ctx, int64_t* n_valid, int64_t* n_members) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->selected) return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
+  uint32_t s[2];
+  SOD_HIP(ctx, hipMemcpyAsync(s, ctx->scal.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (n_valid) *n_valid = s[0];
+  if (n_members) *n_members = s[1];
+  return SOD_OK;
+}
+
+static void decode_keys(const sod_ctx* ctx, const std::vector<uint32_t>& lin, int32_t* keys) {
+  const int by = ctx->bins[1], bt = ctx->bins[2], bs = ctx->bins[3];
+  for (size_t i = 0; i < lin.size(); ++i) {
+    const uint32_t l = lin[i];
+    keys[4 * i + 3] = l % bs;
+    keys[4 * i + 2] = (l / bs) % bt;
+    keys[4 * i + 1] = (l / (bs * bt)) % by;
+    keys[4 * i + 0] = l / (bs * bt * by);
+  }
+}
+
+int sod_valid_get(sod_ctx* ctx, int32_t* keys, int32_t* votes, int64_t* offsets,
+                  int32_t* members, double* means) {
+  int64_t V, M;
+  SOD_TRY(sod_valid_counts(ctx, &V, &M));
+  std::vector<uint32_t> lin((size_t)V);
+  SOD_TRY(download(ctx, lin.data(), ctx->vbin.p, (size_t)V));
+  std::vector<int64_t> off((size_t)V + 1);
+  SOD_TRY(download(ctx, off.data(), ctx->voff.p, (size_t)V + 1));
+  SOD_TRY(download(ctx, members, ctx->members.p, (size_t)M));
+  SOD_TRY(download(ctx, means, ctx->means.p, (size_t)V * 6));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (keys) decode_keys(ctx, lin, keys);
+  if (votes)
+    for (int64_t i = 0; i < V; ++i) votes[i] = (int32_t)(off[i + 1] - off[i]);
+  if (offsets) std::memcpy(offsets, off.data(), off.size() * sizeof(int64_t));
+  return SOD_OK;
+}
+
+int sod_bins_count(sod_ctx* ctx, int64_t* n_bins) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  SOD_TRY(launch_all_bins(ctx));
+  uint32_t b = 0;
+  SOD_HIP(ctx, hipMemcpyAsync(&b, ctx->scal.p + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  *n_bins = b;
+  return SOD_OK;
+}
+
+int sod_bins_get(sod_ctx* ctx, int32_t* keys, int32_t* votes) {
+  int64_t B;
+  SOD_TRY(sod_bins_count(ctx, &B));
+  std::vector<uint32_t> lin((size_t)B);
+  SOD_TRY(download(ctx, lin.data(), ctx->allbin.p, (size_t)B));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  std::vector<uint32_t> cnt((size_t)ctx->nbins);
+  SOD_TRY(download(ctx, cnt.data(), ctx->counts.p, (size_t)ctx->nbins));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (keys) decode_keys(ctx, lin, keys);
+  if (votes)
+    for (int64_t i = 0; i < B; ++i) votes[i] = (int32_t)cnt[lin[i]];
+  return SOD_OK;
+}
+
+// ---- affine ---------------------------------------------------------------------------
+int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_factor,
+                       double y_factor, int32_t threshold) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->selected) return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
+  if (!(x_factor != 0.0) || !(y_factor != 0.0)) return sod_fail(ctx, SOD_EINVAL, "zero factor");
+  SOD_TRY(launch_affine_gather(ctx));
+  SOD_TRY(sod_reserve(ctx, ctx->surv, (size_t)ctx->vmax));
+  SOD_TRY(sod_reserve(ctx, ctx->fvotes, (size_t)ctx->vmax));
+  SOD_TRY(sod_reserve(ctx, ctx->params, (size_t)ctx->vmax * 6));
+  SOD_TRY(sod_reserve(ctx, ctx->alive, (size_t)ctx->mmax));
+  SOD_TRY(launch_affine(ctx, 0, true, ctx->voff.p, ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p,
+                        ctx->aisig.p, query_w, query_h, x_factor, y_factor, threshold, 1 << 30,
+                        ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p, ctx->scal.p));
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+  ctx->affined = true;
+  return SOD_OK;
+}
+
+int sod_affine_get(sod_ctx* ctx, uint8_t* survived, int32_t* votes, double* params,
+                   uint8_t* member_alive) {
+  int64_t V, M;
+  SOD_TRY(sod_valid_counts(ctx, &V, &M));
+  if (!ctx->affined) return sod_fail(ctx, SOD_ESTATE, "sod_affine_enqueue first");
+  SOD_TRY(download(ctx, survived, ctx->surv.p, (size_t)V));
+  SOD_TRY(download(ctx, votes, ctx->fvotes.p, (size_t)V));
+  SOD_TRY(download(ctx, params, ctx->params.p, (size_t)V * 6));
+  SOD_TRY(download(ctx, member_alive, ctx->alive.p, (size_t)M));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return SOD_OK;
+}
+
+// ---- fused pipeline -------------------------------------------------------------------
+int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* a) {
+  SOD_TRY(set_dev(ctx));
+  if (!a) return sod_fail(ctx, SOD_EINVAL, "null args");
+  SOD_TRY(sod_match_enqueue(ctx));
+  SOD_TRY(sod_match_allgather_enqueue(ctx));
+  SOD_TRY(sod_ratio_enqueue(ctx, a->ratio));
+  const int64_t lo = ctx->nranks > 1 ? ctx->row_offset : 0;
+  const int64_t hi = ctx->nranks > 1 ? ctx->row_offset + ctx->n_shard : ctx->n_total;
+  SOD_TRY(sod_hough_enqueue(ctx, a->query_h, a->query_w, a->bins, lo, hi));
+  SOD_TRY(sod_hough_allreduce_enqueue(ctx));
+  SOD_TRY(sod_select_enqueue(ctx, a->vote_threshold));
+  if (a->run_affine)
+    SOD_TRY(sod_affine_enqueue(ctx, a->query_w, a->query_h, a->x_factor, a->y_factor,
+                               a->affine_threshold));
+  return SOD_OK;
+}
+
+// ---- stateless batch forms ------------------------------------------------------------
+int sod_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my, const float* mangle,
+                   const int32_t* moctave, const float* qx, const float* qy, const float* qangle,
+                   const int32_t* qoctave, const double* cx, const double* cy, int32_t query_h,
+                   int32_t query_w, const int32_t bins[4], double* pose, int32_t* idx) {
+  SOD_TRY(set_dev(ctx));
+  if (n < 0 || query_h < 1 || query_w < 1) return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  if (n == 0) return SOD_OK;
+  SOD_TRY(check_bins(ctx, bins));
+  ctx->qh = query_h;
+  ctx->qw = query_w;
+  DevBuf<float> f[6];
+  DevBuf<int32_t> o[2];
+  DevBuf<double> c[2], dp;
+  DevBuf<int32_t> di;
+  int rc = SOD_OK;
+  const float* fs[6] = {mx, my, mangle, qx, qy, qangle};
+  for (int i = 0; i < 6 && rc == SOD_OK; ++i) rc = upload(ctx, f[i], fs[i], (size_t)n);
+  if (rc == SOD_OK) rc = upload(ctx, o[0], moctave, (size_t)n);
+  if (rc == SOD_OK) rc = upload(ctx, o[1], qoctave, (size_t)n);
+  if (rc == SOD_OK) rc = upload(ctx, c[0], cx, (size_t)n);
+  if (rc == SOD_OK) rc = upload(ctx, c[1], cy, (size_t)n);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, dp, (size_t)n * 4);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, di, (size_t)n * 4);
+  if (rc == SOD_OK)
+    rc = launch_pose_batch(ctx, n, f[0].p, f[1].p, f[2].p, o[0].p, f[3].p, f[4].p, f[5].p, o[1].p,
+                           c[0].p, c[1].p, dp.p, di.p);
+  if (rc == SOD_OK) rc = download(ctx, pose, dp.p, (size_t)n * 4);
+  if (rc == SOD_OK) rc = download(ctx, idx, di.p, (size_t)n * 4);
+  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "pose batch failed");
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& b : f) sod_release(b);
+  for (auto& b : o) sod_release(b);
+  for (auto& b : c) sod_release(b);
+  sod_release(dp);
+  sod_release(di);
+  return rc;
+}
+
+int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets, const float* mx,
+                     const float* my, const float* qx, const float* qy, const int32_t* i_sigma,
+                     int32_t query_w, int32_t query_h, double x_factor, double y_factor,
+                     int32_t threshold, int32_t max_iter, uint8_t* survived, int32_t* votes,
+                     double* params, uint8_t* member_alive) {
+  SOD_TRY(set_dev(ctx));
+  if (n_bins < 0 || !offsets || max_iter < 1 || !(x_factor != 0.0) || !(y_factor != 0.0))
+    return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  if (n_bins == 0) return SOD_OK;
+  const int64_t M = offsets[n_bins];
+  for (int64_t i = 0; i < n_bins; ++i)
+    if (offsets[i + 1] < offsets[i]) return sod_fail(ctx, SOD_EINVAL, "offsets not monotone");
+  DevBuf<int64_t> off;
+  DevBuf<float> p[4];
+  DevBuf<int32_t> is, vo;
+  DevBuf<uint8_t> sv, al;
+  DevBuf<double> pr;
+  int rc = upload(ctx, off, offsets, (size_t)n_bins + 1);
+  const float* ps[4] = {mx, my, qx, qy};
+  for (int i = 0; i < 4 && rc == SOD_OK; ++i) rc = upload(ctx, p[i], ps[i], (size_t)M);
+  if (rc == SOD_OK) rc = upload(ctx, is, i_sigma, (size_t)n_bins);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, vo, (size_t)n_bins);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, sv, (size_t)n_bins);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, al, (size_t)M);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, pr, (size_t)n_bins * 6);
+  if (rc == SOD_OK)
+    rc = launch_affine(ctx, n_bins, false, off.p, p[0].p, p[1].p, p[2].p, p[3].p, is.p, query_w,
+                       query_h, x_factor, y_factor, threshold, max_iter, sv.p, vo.p, pr.p, al.p,
+                       nullptr);
+  if (rc == SOD_OK) rc = download(ctx, survived, sv.p, (size_t)n_bins);
+  if (rc == SOD_OK) rc = download(ctx, votes, vo.p, (size_t)n_bins);
+  if (rc == SOD_OK) rc = download(ctx, params, pr.p, (size_t)n_bins * 6);
+  if (rc == SOD_OK) rc = download(ctx, member_alive, al.p, (size_t)M);
+  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "affine batch failed");
+  (void)hipStreamSynchronize(ctx->stream);
+  sod_release(off);
+  for (auto& b : p) sod_release(b);
+  sod_release(is); sod_release(vo); sod_release(sv); sod_release(al); sod_release(pr);
+  return rc;
+}
+
+// ---- RCCL -----------------------------------------------------------------------------
+int sod_comm_unique_id(uint8_t out[SOD_UNIQUE_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == SOD_UNIQUE_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    g_err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+    return SOD_ECOMM;
+  }
+  std::memcpy(out, &id, sizeof(id));
+  return SOD_OK;
+}
+
+int sod_comm_init(sod_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[SOD_UNIQUE_ID_BYTES]) {
+  SOD_TRY(set_dev(ctx));
+  if (nranks < 1 || rank < 0 || rank >= nranks) return sod_fail(ctx, SOD_EINVAL, "bad rank");
+  if (ctx->comm) {
+    ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  if (nranks == 1) return SOD_OK;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    ctx->comm = nullptr;
+    return sod_fail(ctx, SOD_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  return SOD_OK;
+}
+
+}  // extern "C"

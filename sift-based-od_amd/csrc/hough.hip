@@ -1,0 +1,681 @@
+// hough.hip -- generalized-Hough pose voting, valid-bin selection, PoseBin means and the
+// per-bin affine verification, for gfx950.
+//
+// Compiled with -ffp-contract=off: every f64 expression below is evaluated exactly as the
+// reference's Python floats are (one rounding per operation, no FMA), so bin indices are
+// bit-exact.  Reference: HoughTransformHelperFunctions.py:4-72, main.py:89-157,
+// PoseBin.py:6-51, AffineParameters.py:89-160, SiftHelperFunctions.py:25-40.
+//
+// Data flow (all device resident, one stream, no host round trip):
+//   pose_kernel      per query q with a good match: pose (x,y,alpha,s) f64, base bin
+//                    (ix,iy,it,is) packed in a u32, 16-bit mask of the in-range votes
+//   hist_kernel      LDS-privatised histogram over a slab of bins: counts + first-touch
+//                    ordinal (q*16 + slot = dict insertion order), flushed with integer
+//                    atomics (deterministic)
+//   select_*         votes that are the first touch of a bin with >= thr votes, compacted
+//                    in ordinal order = dict insertion order of main.py:126
+//   members_kernel   one wave per valid bin collects its member queries in query order
+//   means_kernel     PoseBin running means, sequential per bin (PoseBin.py:19-43)
+//   affine_kernel    one wave per bin: decoupled 3x3 normal equations, pinv by Jacobi,
+//                    outlier rejection, fixed point (AffineParameters.py:89-160)
+#include "sod_internal.h"
+
+namespace {
+
+constexpr double kPi = 3.141592653589793;        // Py_MATH_PI
+constexpr double kDeg2Rad = kPi / 180.0;         // math.radians factor (CPython degToRad)
+constexpr double kTwoPi = 2 * kPi;
+
+struct Bins {
+  int x, y, t, s;
+};
+
+__device__ __forceinline__ int unpack_octave(int packed) {  // SiftHelperFunctions.py:31-35
+  int o = packed & 0xFF;
+  return o >= 128 ? o - 256 : o;
+}
+
+// Python int() of a float that is then clamped to [0, b-1] after a -1 (HTHF:49-58).
+__device__ __forceinline__ int xy_index(double v, int b) {
+  long long i;
+  if (!(v == v)) i = 0;                 // NaN: unreachable for finite inputs
+  else if (v > 1e9) i = 1000000000LL;
+  else if (v < -1e9) i = -1000000000LL;
+  else i = (long long)v;                // truncation toward zero == Python int()
+  i = i - 1;
+  if (i < 0) i = 0;
+  if (i > b - 1) i = b - 1;
+  return (int)i;
+}
+
+// estimate_object_pose (HTHF:4-37) + calculate_bin_index (HTHF:39-72)
+__device__ __forceinline__ void pose_bins(float mx, float my, float ma, int mo, float qx, float qy,
+                                          float qa, int qo, double cx, double cy, int H, int W,
+                                          Bins b, const int* __restrict__ lut, double pose[4],
+                                          int idx[4]) {
+  const int k = unpack_octave(qo) - unpack_octave(mo);  // m_scale / q_scale = 2^(oQ-oM), exact
+  const double s = ldexp(1.0, k);
+  const double tx = (cx - (double)mx) * s;
+  const double ty = (cy - (double)my) * s;
+  double a = ((double)qa - (double)ma) * kDeg2Rad;
+  a = fmod(a + kTwoPi, kTwoPi);   // argument > 0, so Python % == C fmod
+  const double ca = cos(a), sa = sin(a);
+  const double x = (ca * tx - sa * ty) + (double)qx;
+  const double y = (sa * tx + ca * ty) + (double)qy;
+  pose[0] = x;
+  pose[1] = y;
+  pose[2] = a;
+  pose[3] = s;
+  idx[0] = xy_index((x * b.x) / W, b.x);
+  idx[1] = xy_index((y * b.y) / H, b.y);
+  idx[2] = (int)fmod((a * b.t) / kTwoPi, (double)b.t);
+  idx[3] = lut[k + kSigmaLutHalf];
+}
+
+__device__ __forceinline__ uint32_t lin_bin(int ix, int iy, int it, int is, Bins b) {
+  return (uint32_t)(((ix * b.y + iy) * b.t + it) * b.s + is);
+}
+
+__global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
+                            const int* __restrict__ idx1, const float* __restrict__ qx,
+                            const float* __restrict__ qy, const float* __restrict__ qa,
+                            const int* __restrict__ qo, const float* __restrict__ mx,
+                            const float* __restrict__ my, const float* __restrict__ ma,
+                            const int* __restrict__ mo, const int* __restrict__ mimg,
+                            const double* __restrict__ cent, int H, int W, Bins b,
+                            const int* __restrict__ lut, int64_t own_lo, int64_t own_hi,
+                            double* __restrict__ pose, uint32_t* __restrict__ basekey,
+                            uint32_t* __restrict__ vmask) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  if (!good[q]) {
+    vmask[q] = 0;
+    return;
+  }
+  const int m = idx1[q];
+  const int im = mimg[m];
+  double p[4];
+  int ix[4];
+  pose_bins(mx[m], my[m], ma[m], mo[m], qx[q], qy[q], qa[q], qo[q], cent[2 * im], cent[2 * im + 1],
+            H, W, b, lut, p, ix);
+  pose[4 * q + 0] = p[0];
+  pose[4 * q + 1] = p[1];
+  pose[4 * q + 2] = p[2];
+  pose[4 * q + 3] = p[3];
+  basekey[q] = (uint32_t)ix[0] | ((uint32_t)ix[1] << 8) | ((uint32_t)ix[2] << 16) |
+               ((uint32_t)ix[3] << 24);
+  // main.py:105-110: 16 votes, kept when every index is < bins (no theta wrap)
+  uint32_t mask = 0;
+#pragma unroll
+  for (int slot = 0; slot < 16; ++slot) {
+    const int w = (slot >> 3) & 1, x = (slot >> 2) & 1, y = (slot >> 1) & 1, z = slot & 1;
+    if (ix[0] + w < b.x && ix[1] + x < b.y && ix[2] + y < b.t && ix[3] + z < b.s)
+      mask |= 1u << slot;
+  }
+  const bool own = (m >= own_lo) && (m < own_hi);
+  vmask[q] = mask | (own ? 0x10000u : 0u);
+}
+
+__global__ void pose_batch_kernel(int64_t n, const float* __restrict__ mx,
+                                  const float* __restrict__ my, const float* __restrict__ ma,
+                                  const int* __restrict__ mo, const float* __restrict__ qx,
+                                  const float* __restrict__ qy, const float* __restrict__ qa,
+                                  const int* __restrict__ qo, const double* __restrict__ cx,
+                                  const double* __restrict__ cy, int H, int W, Bins b,
+                                  const int* __restrict__ lut, double* __restrict__ pose,
+                                  int* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double p[4];
+  int ix[4];
+  pose_bins(mx[i], my[i], ma[i], mo[i], qx[i], qy[i], qa[i], qo[i], cx[i], cy[i], H, W, b, lut, p, ix);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pose[4 * i + j] = p[j];
+    idx[4 * i + j] = ix[j];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// LDS-privatised histogram.  blockIdx.x = bin slab, blockIdx.y = query chunk.
+constexpr int kSlab = 8192;     // bins per workgroup: 2 x 32 KiB of LDS
+constexpr int kChunk = 4096;    // queries per workgroup
+constexpr int kHistThreads = 512;
+
+__global__ __launch_bounds__(kHistThreads) void hist_kernel(
+    int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
+    int64_t nbins, uint32_t* __restrict__ gcount, uint32_t* __restrict__ gfirst) {
+  __shared__ uint32_t cnt[kSlab];
+  __shared__ uint32_t fst[kSlab];
+  const uint32_t slab0 = blockIdx.x * kSlab;
+  for (int i = threadIdx.x; i < kSlab; i += kHistThreads) {
+    cnt[i] = 0;
+    fst[i] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  const int64_t q0 = (int64_t)blockIdx.y * kChunk;
+  const int64_t q1 = min(nq, q0 + kChunk);
+  for (int64_t q = q0 + threadIdx.x; q < q1; q += kHistThreads) {
+    const uint32_t m = vmask[q];
+    if (!(m & 0x10000u)) continue;  // no vote, or the match's DB row is not in this shard
+    const uint32_t key = basekey[q];
+    const int ix = key & 0xFF, iy = (key >> 8) & 0xFF, it = (key >> 16) & 0xFF, is = key >> 24;
+#pragma unroll
+    for (int slot = 0; slot < 16; ++slot) {
+      if (!((m >> slot) & 1u)) continue;
+      const uint32_t lb = lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                  it + ((slot >> 1) & 1), is + (slot & 1), b) - slab0;
+      if (lb < (uint32_t)kSlab) {
+        atomicAdd(&cnt[lb], 1u);
+        atomicMin(&fst[lb], (uint32_t)(q * 16 + slot));
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kSlab; i += kHistThreads) {
+    const uint32_t c = cnt[i];
+    if (c && slab0 + i < nbins) {
+      atomicAdd(&gcount[slab0 + i], c);
+      atomicMin(&gfirst[slab0 + i], fst[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Ordered compaction of "first touch of a bin with >= thr votes" over ordinals q*16+slot.
+constexpr int kSelThreads = 256;   // one thread per query, 256 queries per block
+
+__device__ __forceinline__ uint32_t first_touch_slots(int64_t q, const uint32_t* basekey,
+                                                      const uint32_t* vmask,
+                                                      const uint32_t* gcount,
+                                                      const uint32_t* gfirst, Bins b,
+                                                      uint32_t thr, uint32_t bins_out[16]) {
+  const uint32_t m = vmask[q] & 0xFFFFu;
+  uint32_t n = 0;
+  if (!m) return 0;
+  const uint32_t key = basekey[q];
+  const int ix = key & 0xFF, iy = (key >> 8) & 0xFF, it = (key >> 16) & 0xFF, is = key >> 24;
+  for (int slot = 0; slot < 16; ++slot) {
+    if (!((m >> slot) & 1u)) continue;
+    const uint32_t lb = lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                it + ((slot >> 1) & 1), is + (slot & 1), b);
+    if (gcount[lb] >= thr && gfirst[lb] == (uint32_t)(q * 16 + slot)) bins_out[n++] = lb;
+  }
+  return n;
+}
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+  // kSelThreads-wide exclusive scan (4 waves): wave prefix via shuffles, then wave offsets
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (int i = 0; i < kSelThreads / 64; ++i) {
+    if (i < w) off += sh[i];
+    tot += sh[i];
+  }
+  __syncthreads();
+  *total = tot;
+  return off + x - v;
+}
+
+__global__ __launch_bounds__(kSelThreads) void select_count_kernel(
+    int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
+    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b, uint32_t thr,
+    uint32_t* __restrict__ blk) {
+  __shared__ uint32_t sh[kSelThreads / 64];
+  const int64_t q = (int64_t)blockIdx.x * kSelThreads + threadIdx.x;
+  uint32_t tmp[16];
+  const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, thr, tmp) : 0;
+  uint32_t tot;
+  block_excl_scan(n, sh, &tot);
+  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+// single-workgroup exclusive scan, in place; total -> *out_total
+__global__ __launch_bounds__(1024) void scan_u32_kernel(uint32_t* __restrict__ a, int64_t n,
+                                                        uint32_t* __restrict__ out_total) {
+  __shared__ uint32_t sh[16];
+  __shared__ uint32_t carry_s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const uint32_t v = i < n ? a[i] : 0;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) off += sh[k];
+      tot += sh[k];
+    }
+    const uint32_t c = carry_s;
+    if (i < n) a[i] = c + off + x - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s = c + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out_total = carry_s;
+}
+
+__global__ __launch_bounds__(kSelThreads) void select_write_kernel(
+    int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
+    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b, uint32_t thr,
+    const uint32_t* __restrict__ blk, uint32_t* __restrict__ out) {
+  __shared__ uint32_t sh[kSelThreads / 64];
+  const int64_t q = (int64_t)blockIdx.x * kSelThreads + threadIdx.x;
+  uint32_t tmp[16];
+  const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, thr, tmp) : 0;
+  uint32_t tot;
+  const uint32_t pos = blk[blockIdx.x] + block_excl_scan(n, sh, &tot);
+  for (uint32_t i = 0; i < n; ++i) out[pos + i] = tmp[i];
+}
+
+// member offsets: voff[i] = sum_{j<i} count[vbin[j]], voff[V] = total (single workgroup)
+__global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __restrict__ vbin,
+                                                              const uint32_t* __restrict__ gcount,
+                                                              uint32_t* __restrict__ scal,
+                                                              int64_t* __restrict__ voff) {
+  __shared__ uint32_t sh[16];
+  __shared__ int64_t carry_s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t n = scal[0];
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const uint32_t v = i < n ? gcount[vbin[i]] : 0;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) off += sh[k];
+      tot += sh[k];
+    }
+    const int64_t c = carry_s;
+    if (i < n) voff[i] = c + off + x - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s = c + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    voff[n] = carry_s;
+    scal[1] = (uint32_t)carry_s;
+  }
+}
+
+// one wave per valid bin: members = matches voting for it, in query order
+__global__ __launch_bounds__(256) void members_kernel(
+    int64_t nq, const uint32_t* __restrict__ scal, const uint32_t* __restrict__ vbin,
+    const int64_t* __restrict__ voff, const uint32_t* __restrict__ gcount,
+    const uint32_t* __restrict__ gfirst, const uint32_t* __restrict__ basekey,
+    const uint32_t* __restrict__ vmask, Bins b, int32_t* __restrict__ members) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t V = scal[0];
+  for (int64_t v = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < V; v += nwaves) {
+    const uint32_t lb = vbin[v];
+    const int bs_ = lb % b.s, bt_ = (lb / b.s) % b.t, by_ = (lb / (b.s * b.t)) % b.y,
+              bx_ = lb / (b.s * b.t * b.y);
+    const uint32_t need = gcount[lb];
+    const int64_t off = voff[v];
+    uint32_t got = 0;
+    for (int64_t q0 = gfirst[lb] >> 4; got < need && q0 < nq; q0 += 64) {
+      const int64_t q = q0 + lane;
+      bool mem = false;
+      if (q < nq) {
+        const uint32_t m = vmask[q] & 0xFFFFu;
+        if (m) {
+          const uint32_t key = basekey[q];
+          const int dx = bx_ - (int)(key & 0xFF), dy = by_ - (int)((key >> 8) & 0xFF),
+                    dt = bt_ - (int)((key >> 16) & 0xFF), ds = bs_ - (int)(key >> 24);
+          if ((unsigned)dx <= 1u && (unsigned)dy <= 1u && (unsigned)dt <= 1u && (unsigned)ds <= 1u)
+            mem = (m >> (dx * 8 + dy * 4 + dt * 2 + ds)) & 1u;
+        }
+      }
+      const uint64_t bal = __ballot(mem);
+      if (mem) {
+        const uint32_t pos = __popcll(bal & ((1ull << lane) - 1ull));
+        members[off + got + pos] = (int32_t)q;
+      }
+      got += __popcll(bal);
+    }
+  }
+}
+
+// PoseBin running means in vote order (PoseBin.py:19-43): one thread per valid bin
+__global__ void means_kernel(const uint32_t* __restrict__ scal, const int64_t* __restrict__ voff,
+                             const int32_t* __restrict__ members, const double* __restrict__ pose,
+                             const int* __restrict__ idx1, const int* __restrict__ mimg,
+                             const int* __restrict__ isize, double* __restrict__ means) {
+  const int64_t V = scal[0];
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = voff[v], e = voff[v + 1];
+    double cx = 0, cy = 0, an = 0, sc = 0, w = 0, h = 0;
+    for (int64_t j = a; j < e; ++j) {
+      const int q = members[j];
+      const double* p = pose + 4 * (int64_t)q;
+      const int im = mimg[idx1[q]];
+      const double iw = (double)isize[2 * im], ih = (double)isize[2 * im + 1];
+      if (j == a) {
+        cx = p[0]; cy = p[1]; an = p[2]; sc = p[3]; w = iw; h = ih;
+      } else {
+        const double n = (double)(j - a), n1 = (double)(j - a + 1);
+        cx = (cx * n + p[0]) / n1;
+        cy = (cy * n + p[1]) / n1;
+        an = (an * n + p[2]) / n1;
+        sc = (sc * n + p[3]) / n1;
+        w = (w * n + iw) / n1;
+        h = (h * n + ih) / n1;
+      }
+    }
+    double* o = means + 6 * v;
+    o[0] = cx; o[1] = cy; o[2] = an; o[3] = sc; o[4] = w; o[5] = h;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// affine verification
+__global__ void affine_gather_kernel(const uint32_t* __restrict__ scal,
+                                     const int32_t* __restrict__ members,
+                                     const int* __restrict__ idx1, const float* __restrict__ mx,
+                                     const float* __restrict__ my, const float* __restrict__ qx,
+                                     const float* __restrict__ qy, const uint32_t* __restrict__ vbin,
+                                     Bins b, float* __restrict__ amx, float* __restrict__ amy,
+                                     float* __restrict__ aqx, float* __restrict__ aqy,
+                                     int32_t* __restrict__ aisig) {
+  const int64_t M = scal[1], V = scal[0];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += stride) {
+    const int q = members[e];
+    const int m = idx1[q];
+    amx[e] = mx[m];
+    amy[e] = my[m];
+    aqx[e] = qx[q];
+    aqy[e] = qy[q];
+  }
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += stride)
+    aisig[v] = (int32_t)(vbin[v] % b.s);
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+  return x;
+}
+
+// pinv of a symmetric 3x3 (numpy.linalg.pinv default rcond 1e-15 relative to the largest
+// singular value; for a symmetric matrix the singular values are |eigenvalues|).
+__device__ void pinv3_sym(const double g[3][3], double p[3][3]) {
+  double a[3][3], v[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      a[i][j] = g[i][j];
+      v[i][j] = (i == j) ? 1.0 : 0.0;
+    }
+  for (int sweep = 0; sweep < 32; ++sweep) {
+    const double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+    const double dia = a[0][0] * a[0][0] + a[1][1] * a[1][1] + a[2][2] * a[2][2];
+    if (off <= 1e-36 * dia || off == 0.0) break;
+    for (int pq = 0; pq < 3; ++pq) {
+      const int p_ = pq == 2 ? 1 : 0, q_ = pq == 0 ? 1 : 2;
+      const double apq = a[p_][q_];
+      if (apq == 0.0) continue;
+      const double theta = (a[q_][q_] - a[p_][p_]) / (2.0 * apq);
+      const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+      const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+      for (int k = 0; k < 3; ++k) {  // A <- A J (columns p, q)
+        const double akp = a[k][p_], akq = a[k][q_];
+        a[k][p_] = c * akp - s * akq;
+        a[k][q_] = s * akp + c * akq;
+      }
+      for (int k = 0; k < 3; ++k) {  // A <- J^T A (rows p, q)
+        const double apk = a[p_][k], aqk = a[q_][k];
+        a[p_][k] = c * apk - s * aqk;
+        a[q_][k] = s * apk + c * aqk;
+      }
+      for (int k = 0; k < 3; ++k) {
+        const double vkp = v[k][p_], vkq = v[k][q_];
+        v[k][p_] = c * vkp - s * vkq;
+        v[k][q_] = s * vkp + c * vkq;
+      }
+    }
+  }
+  const double l[3] = {a[0][0], a[1][1], a[2][2]};
+  const double lmax = fmax(fabs(l[0]), fmax(fabs(l[1]), fabs(l[2])));
+  const double cut = 1e-15 * lmax;
+  double inv[3];
+  for (int i = 0; i < 3; ++i) inv[i] = (fabs(l[i]) > cut) ? 1.0 / l[i] : 0.0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      p[i][j] = v[i][0] * inv[0] * v[j][0] + v[i][1] * inv[1] * v[j][1] + v[i][2] * inv[2] * v[j][2];
+}
+
+__global__ __launch_bounds__(256) void affine_kernel(
+    int64_t nb_host, const uint32_t* __restrict__ nb_dev, const int64_t* __restrict__ off,
+    const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
+    const float* __restrict__ qy, const int32_t* __restrict__ isig, int qw, int qh, double xf,
+    double yf, int thr, int max_iter, uint8_t* __restrict__ surv, int32_t* __restrict__ votes,
+    double* __restrict__ params, uint8_t* __restrict__ alive) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t NB = nb_dev ? (int64_t)nb_dev[0] : nb_host;
+  for (int64_t v = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < NB; v += nwaves) {
+    const int64_t a = off[v], e = off[v + 1];
+    for (int64_t j = a + lane; j < e; j += 64) alive[j] = 1;
+    // AffineParameters.py:120-121: tolerance scales with the scale-bin INDEX pose[3]
+    const double xref = (double)((int64_t)qw * isig[v]) / xf;
+    const double yref = (double)((int64_t)qh * isig[v]) / yf;
+    int64_t n = e - a;
+    double prm[6] = {0, 0, 0, 0, 0, 0};
+    bool ok = false;
+    for (int it = 0; it < max_iter; ++it) {
+      double s[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (int64_t j = a + lane; j < e; j += 64) {
+        if (!alive[j]) continue;
+        const double x = mx[j], y = my[j], u = qx[j], w = qy[j];
+        s[0] += x * x; s[1] += x * y; s[2] += x; s[3] += y * y; s[4] += y; s[5] += 1.0;
+        s[6] += x * u; s[7] += y * u; s[8] += u; s[9] += x * w; s[10] += y * w; s[11] += w;
+      }
+#pragma unroll
+      for (int k = 0; k < 12; ++k) s[k] = wave_sum(s[k]);
+      if (n > 0) {  // AffineParameters.py:105: no-op for an empty bin
+        const double g[3][3] = {{s[0], s[1], s[2]}, {s[1], s[3], s[4]}, {s[2], s[4], s[5]}};
+        double p[3][3];
+        pinv3_sym(g, p);
+        // x = [m1 m2 m3 m4 tx ty]: (m1,m2,tx) from the u rows, (m3,m4,ty) from the v rows
+        prm[0] = p[0][0] * s[6] + p[0][1] * s[7] + p[0][2] * s[8];
+        prm[1] = p[1][0] * s[6] + p[1][1] * s[7] + p[1][2] * s[8];
+        prm[4] = p[2][0] * s[6] + p[2][1] * s[7] + p[2][2] * s[8];
+        prm[2] = p[0][0] * s[9] + p[0][1] * s[10] + p[0][2] * s[11];
+        prm[3] = p[1][0] * s[9] + p[1][1] * s[10] + p[1][2] * s[11];
+        prm[5] = p[2][0] * s[9] + p[2][1] * s[10] + p[2][2] * s[11];
+      }
+      // remove_outliers, AffineParameters.py:134-159
+      int dropped = 0;
+      for (int64_t j = a + lane; j < e; j += 64) {
+        if (!alive[j]) continue;
+        const double x = mx[j], y = my[j];
+        const double up = (prm[0] * x + prm[1] * y) + prm[4];
+        const double vp = (prm[2] * x + prm[3] * y) + prm[5];
+        if (fabs(up - (double)qx[j]) > xref || fabs(vp - (double)qy[j]) > yref) {
+          alive[j] = 0;
+          ++dropped;
+        }
+      }
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) dropped += __shfl_xor(dropped, m);
+      n -= dropped;
+      if (n < thr) {  // main.py:152
+        ok = false;
+        break;
+      }
+      ok = true;
+      if (dropped == 0) break;  // main.py:151 fixed point
+    }
+    if (lane == 0) {
+      surv[v] = ok ? 1 : 0;
+      votes[v] = (int32_t)n;
+      for (int k = 0; k < 6; ++k) params[6 * v + k] = prm[k];
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static Bins ctx_bins(const sod_ctx* c) { return Bins{c->bins[0], c->bins[1], c->bins[2], c->bins[3]}; }
+
+int sod_build_sigma_lut(sod_ctx* ctx, int32_t bs) {
+  // HTHF:66-70 evaluated with the same libm calls CPython's math.log(x, 2) makes:
+  // log(x) / log(2.0), then / (2*(n_oct-1)+0.5) * bins, int() truncation, clamp.
+  int32_t lut[kSigmaLutSize];
+  for (int k = -kSigmaLutHalf; k <= kSigmaLutHalf; ++k) {
+    const double s = ldexp(1.0, k);
+    const double lg = log(s) / log(2.0);
+    const double v = lg / 6.5 * (double)bs;
+    long long i = (long long)v;
+    if (i < 0) i = 0;
+    if (i > bs - 1) i = bs - 1;
+    lut[k + kSigmaLutHalf] = (int32_t)i;
+  }
+  SOD_TRY(sod_reserve(ctx, ctx->sig_lut, kSigmaLutSize));
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->sig_lut.p, lut, sizeof(lut), hipMemcpyHostToDevice, ctx->stream));
+  // the host array dies with this frame: make the copy complete before returning
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return SOD_OK;
+}
+
+int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my, const float* ma,
+                      const int32_t* mo, const float* qx, const float* qy, const float* qa,
+                      const int32_t* qo, const double* cx, const double* cy, double* pose,
+                      int32_t* idx) {
+  const int bs = 256;
+  hipLaunchKernelGGL(pose_batch_kernel, dim3((unsigned)cdiv(n, bs)), dim3(bs), 0, ctx->stream, n,
+                     mx, my, ma, mo, qx, qy, qa, qo, cx, cy, ctx->qh, ctx->qw, ctx_bins(ctx),
+                     ctx->sig_lut.p, pose, idx);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
+  const int64_t nq = ctx->nq;
+  SOD_TRY(sod_reserve(ctx, ctx->pose, (size_t)nq * 4));
+  SOD_TRY(sod_reserve(ctx, ctx->basekey, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->vmask, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->counts, (size_t)ctx->nbins));
+  SOD_TRY(sod_reserve(ctx, ctx->first, (size_t)ctx->nbins));
+  SOD_HIP(ctx, hipMemsetAsync(ctx->counts.p, 0, ctx->nbins * 4, ctx->stream));
+  SOD_HIP(ctx, hipMemsetAsync(ctx->first.p, 0xFF, ctx->nbins * 4, ctx->stream));
+  const int bs = 256;
+  hipLaunchKernelGGL(pose_kernel, dim3((unsigned)cdiv(nq, bs)), dim3(bs), 0, ctx->stream, nq,
+                     ctx->good.p, ctx->idx1.p, ctx->qx.p, ctx->qy.p, ctx->qang.p, ctx->qoct.p,
+                     ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p,
+                     ctx->qh, ctx->qw, ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
+                     ctx->basekey.p, ctx->vmask.p);
+  SOD_HIP(ctx, hipGetLastError());
+  dim3 grid((unsigned)cdiv(ctx->nbins, kSlab), (unsigned)cdiv(nq, kChunk));
+  hipLaunchKernelGGL(hist_kernel, grid, dim3(kHistThreads), 0, ctx->stream, nq, ctx->basekey.p,
+                     ctx->vmask.p, ctx_bins(ctx), ctx->nbins, ctx->counts.p, ctx->first.p);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* total_slot) {
+  const int64_t nq = ctx->nq;
+  const int64_t nblk = cdiv(nq, kSelThreads);
+  SOD_TRY(sod_reserve(ctx, ctx->blk, (size_t)nblk));
+  hipLaunchKernelGGL(select_count_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream,
+                     nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
+                     thr, ctx->blk.p);
+  SOD_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(scan_u32_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->blk.p, nblk,
+                     total_slot);
+  SOD_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(select_write_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream,
+                     nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
+                     thr, ctx->blk.p, out);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_select(sod_ctx* ctx, int32_t thr) {
+  const int64_t nq = ctx->nq;
+  if (thr < 1) thr = 1;  // a bin exists only once voted for
+  ctx->vmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * nq));
+  ctx->mmax = std::max<int64_t>(1, 16 * nq);
+  SOD_TRY(sod_reserve(ctx, ctx->scal, 4));
+  SOD_TRY(sod_reserve(ctx, ctx->vbin, (size_t)ctx->vmax));
+  SOD_TRY(sod_reserve(ctx, ctx->voff, (size_t)ctx->vmax + 1));
+  SOD_TRY(sod_reserve(ctx, ctx->members, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->means, (size_t)ctx->vmax * 6));
+  SOD_TRY(run_compaction(ctx, (uint32_t)thr, ctx->vbin.p, ctx->scal.p + 0));
+  hipLaunchKernelGGL(member_offsets_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->vbin.p,
+                     ctx->counts.p, ctx->scal.p, ctx->voff.p);
+  SOD_HIP(ctx, hipGetLastError());
+  const int wg = std::max(1, ctx->num_cus * 4);
+  hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
+                     ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
+                     ctx->vmask.p, ctx_bins(ctx), ctx->members.p);
+  SOD_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus)), dim3(64), 0, ctx->stream,
+                     ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->pose.p, ctx->idx1.p,
+                     ctx->mimg.p, ctx->isize.p, ctx->means.p);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_all_bins(sod_ctx* ctx) {
+  const int64_t bmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * (int64_t)ctx->nq));
+  SOD_TRY(sod_reserve(ctx, ctx->scal, 4));
+  SOD_TRY(sod_reserve(ctx, ctx->allbin, (size_t)bmax));
+  return run_compaction(ctx, 1u, ctx->allbin.p, ctx->scal.p + 2);
+}
+
+int launch_affine_gather(sod_ctx* ctx) {
+  SOD_TRY(sod_reserve(ctx, ctx->amx, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->amy, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->aqx, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->aqy, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->aisig, (size_t)ctx->vmax));
+  hipLaunchKernelGGL(affine_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
+                     ctx->stream, ctx->scal.p, ctx->members.p, ctx->idx1.p, ctx->mx.p, ctx->my.p,
+                     ctx->qx.p, ctx->qy.p, ctx->vbin.p, ctx_bins(ctx), ctx->amx.p, ctx->amy.p,
+                     ctx->aqx.p, ctx->aqy.p, ctx->aisig.p);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_affine(sod_ctx* ctx, int64_t nb_host, bool count_on_device, const int64_t* offsets,
+                  const float* mx, const float* my, const float* qx, const float* qy,
+                  const int32_t* isig, int32_t qw, int32_t qh, double xf, double yf, int32_t thr,
+                  int32_t max_iter, uint8_t* surv, int32_t* votes, double* params, uint8_t* alive,
+                  const uint32_t* dev_count) {
+  const int wg = std::max(1, ctx->num_cus * 4);
+  hipLaunchKernelGGL(affine_kernel, dim3(wg), dim3(256), 0, ctx->stream, nb_host,
+                     count_on_device ? dev_count : nullptr, offsets, mx, my, qx, qy, isig, qw, qh,
+                     xf, yf, thr, max_iter, surv, votes, params, alive);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}

@@ -1,0 +1,360 @@
+// match.hip -- brute-force k=2 SIFT matcher for gfx950 (replaces cv2.BFMatcher().knnMatch,
+// main.py:70-71) and the ratio test (main.py:81-86).
+//
+// Exactness.  SIFT descriptors are integers 0..255 (OpenCV saturate_cast<uchar>), exact in
+// bf16, and -2*d is exact too.  The MFMA accumulates dn - 2 q.d with every partial sum an
+// integer of magnitude < 2^24, so the f32 result is exact whatever order the hardware adds in;
+// q.q is added once at the end (still < 2^24).  Squared distances are therefore exact
+// integers and sqrtf (correctly rounded) reproduces OpenCV's float distance bit for bit.
+//
+// Layout.  D = A.B with A = DB rows (16-row subtiles), B = queries (16-query tiles),
+// v_mfma_f32_16x16x32_bf16: lane l holds A[row l&15][k 8(l>>4)..+7] and B[k..][col l&15];
+// the result register r of lane l is row (l>>4)*4+r, column l&15.  So a lane owns ONE query
+// and walks DB rows in increasing order: the k=2 reduction is lane-local (no shuffles) and
+// strict '<' keeps the lowest trainIdx on ties, as OpenCV's insertion does.  Subtiles are
+// pre-packed in HBM in exactly the fragment order ([kstep][lane][16 B]), so the LDS image of
+// a stage is a straight copy and every ds_read_b128 is a contiguous, conflict-free 1 KiB.
+//
+// ||d||^2 is folded into the accumulator init (C operand = the 4 row norms of the lane), so
+// the MFMA output is already dn - 2 q.d: no epilogue add.  Epilogue per 16x16 tile: a 2-op min
+// of the lane's 4 values against its running 2nd-best (wave-uniform branch); only when some
+// lane can improve does the exact top-2 update run (rare after the first few thousand rows).
+//
+// Decomposition.  A workgroup = NW waves x QT query tiles (512 queries) kept in VGPRs for
+// the whole launch; it streams one DB split through a 2-stage LDS ring (register staging,
+// one barrier per stage).  Grid = query blocks x DB splits, sized to fill every CU twice;
+// per-split partial top-2 are merged by merge_kernel (also used for the multi-GPU merge).
+#include "sod_internal.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace {
+
+constexpr int QT = 8;    // 16-query tiles per wave
+constexpr int NW = 4;    // waves per workgroup
+constexpr int SPS = 4;   // 16-row subtiles per LDS stage (64 rows = 16 KiB)
+constexpr int NT = NW * 64;
+constexpr int kStageBytes = SPS * kSubBytes;
+constexpr int kStageNorm = SPS * kSubRows * 4;
+constexpr int kStageU4 = kStageBytes / 16 / NT;  // uint4 per thread per stage
+constexpr float kInit = 3.0e38f;
+
+static_assert(kStageBytes % (16 * NT) == 0, "stage must split evenly over the workgroup");
+static_assert(kStageNorm / 16 <= NT, "norm copy uses one uint4 per thread");
+
+// ---------------------------------------------------------------------------------------
+// pack: rows -> MFMA-fragment order, bf16 (x scale), plus exact squared norms.
+// One thread per (row, 8-dim chunk c).  Fragment: subtile r/16, kstep c/4,
+// lane (r%16) + 16*(c%4), 16 bytes.
+template <typename TIn>
+__global__ void pack_rows_kernel(const TIn* __restrict__ src, int64_t n, int64_t npad,
+                                 float scale, uint8_t* __restrict__ pack,
+                                 float* __restrict__ norms, float padnorm,
+                                 uint32_t* __restrict__ flags, int max_slot) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = t >> 4;
+  const int c = (int)(t & 15);
+  if (row >= npad) return;  // npad*16 threads is a multiple of 64: whole waves exit
+  float v[8];
+  uint32_t bad = 0;
+  if (row < n) {
+    if constexpr (sizeof(TIn) == 1) {
+      const uint2 raw = *reinterpret_cast<const uint2*>(src + row * kDim + c * 8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (float)((raw.x >> (8 * j)) & 0xFF);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 + j] = (float)((raw.y >> (8 * j)) & 0xFF);
+    } else {
+      const float4 a = *reinterpret_cast<const float4*>(src + row * kDim + c * 8);
+      const float4 b = *reinterpret_cast<const float4*>(src + row * kDim + c * 8 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = (v[j] >= 0.f) && (v[j] <= 255.f) && (v[j] == truncf(v[j]));
+        bad |= ok ? 0u : 1u;
+        if (!ok) v[j] = 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  }
+  float ss = 0.f;
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ss += v[j] * v[j];  // integers, < 2^24: exact in any order
+    o[j] = (__bf16)(v[j] * scale);
+  }
+  // the 16 chunks of one row are 16 consecutive lanes
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) ss += __shfl_xor(ss, m, 16);
+  const int64_t sub = row >> 4;
+  const int rr = (int)(row & 15);
+  const int64_t off = sub * kSubBytes + (c >> 2) * 1024 + (rr + 16 * (c & 3)) * 16;
+  *reinterpret_cast<bf16x8*>(pack + off) = o;
+  if (c == 0) {
+    norms[row] = (row < n) ? ss : padnorm;
+    if (row < n) atomicMax(&flags[max_slot], __float_as_uint(ss));
+  }
+  if (bad) atomicAdd(&flags[0], 1u);
+}
+
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void merge2(float& v1, int& i1, float& v2, float o1, int oi, float o2) {
+  // lexicographic (distance, trainIdx) on the best, plain min on the second
+  if (o1 < v1 || (o1 == v1 && oi < i1)) {
+    v2 = fminf(v1, o2);
+    v1 = o1;
+    i1 = oi;
+  } else {
+    v2 = fminf(v2, o1);
+  }
+}
+
+__global__ __launch_bounds__(NT, 2) void match_kernel(
+    const uint8_t* __restrict__ dbpack, const float* __restrict__ dn, int64_t nsub,
+    const uint8_t* __restrict__ qpack, const float* __restrict__ qn, int nqt, int64_t nq_pad,
+    int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
+    int* __restrict__ pidx, float* __restrict__ pd2) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2][kStageBytes + kStageNorm];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int sp = blockIdx.x % split;
+  const int qb = blockIdx.x / split;
+  const int qt0 = (qb * NW + wave) * QT;
+
+  // queries: B fragments stay in registers for the whole launch
+  bf16x8 bq[QT][4];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int qt = qt0 + t;
+      if (qt < nqt)
+        bq[t][k] = *reinterpret_cast<const bf16x8*>(qpack + ((int64_t)qt * 4 + k) * 1024 + lane * 16);
+      else
+        bq[t][k] = bf16x8{};
+    }
+  }
+  float v1[QT], v2[QT];
+  int id[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    v1[t] = kInit;
+    v2[t] = kInit;
+    id[t] = 0x7fffffff;
+  }
+
+  const int64_t s_lo = (int64_t)sp * sub_per_split;
+  const int64_t s_hi = min(nsub, s_lo + sub_per_split);
+  const int64_t nst = (s_hi - s_lo) / SPS;  // nsub and sub_per_split are multiples of SPS
+
+  uint4 st[kStageU4];
+  uint4 stn = make_uint4(0, 0, 0, 0);
+  auto gload = [&](int64_t sub0) {
+    const uint4* src = reinterpret_cast<const uint4*>(dbpack + sub0 * kSubBytes);
+#pragma unroll
+    for (int j = 0; j < kStageU4; ++j) st[j] = src[j * NT + tid];
+    if (tid < kStageNorm / 16) stn = reinterpret_cast<const uint4*>(dn + sub0 * kSubRows)[tid];
+  };
+  auto lstore = [&](int buf) {
+    uint4* dst = reinterpret_cast<uint4*>(lds[buf]);
+#pragma unroll
+    for (int j = 0; j < kStageU4; ++j) dst[j * NT + tid] = st[j];
+    if (tid < kStageNorm / 16) reinterpret_cast<uint4*>(lds[buf] + kStageBytes)[tid] = stn;
+  };
+
+  if (nst > 0) {
+    gload(s_lo);
+    lstore(0);
+  }
+  __syncthreads();
+
+  for (int64_t s = 0; s < nst; ++s) {
+    const int buf = (int)(s & 1);
+    if (s + 1 < nst) gload(s_lo + (s + 1) * SPS);
+    const uint8_t* sb = lds[buf];
+#pragma unroll
+    for (int u = 0; u < SPS; ++u) {
+      const uint8_t* base = sb + u * kSubBytes + lane * 16;
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(base);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(base + 1024);
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(base + 2048);
+      const bf16x8 a3 = *reinterpret_cast<const bf16x8*>(base + 3072);
+      const f32x4 cn = *reinterpret_cast<const f32x4*>(sb + kStageBytes + u * 64 + (lane >> 4) * 16);
+      const int rowb = row_offset + (int)((s_lo + s * SPS + u) * kSubRows) + (lane >> 4) * 4;
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[t][0], cn, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bq[t][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bq[t][2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, bq[t][3], acc, 0, 0, 0);
+        const float m = fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3]));
+        if (__any(m < v2[t])) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = acc[r];
+            const bool lt = x < v1[t];
+            v2[t] = __builtin_amdgcn_fmed3f(v1[t], v2[t], x);
+            id[t] = lt ? rowb + r : id[t];
+            v1[t] = fminf(v1[t], x);
+          }
+        }
+      }
+    }
+    if (s + 1 < nst) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // merge the 4 row groups of each query (lanes l, l^16, l^32, l^48)
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      const float o1 = __shfl_xor(v1[t], m);
+      const int oi = __shfl_xor(id[t], m);
+      const float o2 = __shfl_xor(v2[t], m);
+      merge2(v1[t], id[t], v2[t], o1, oi, o2);
+    }
+    const int qt = qt0 + t;
+    if (lane < 16 && qt < nqt) {
+      const int64_t q = (int64_t)qt * 16 + lane;
+      const float n2 = qn[q];
+      const int64_t o = (int64_t)sp * nq_pad + q;
+      pd1[o] = v1[t] + n2;
+      pidx[o] = id[t];
+      pd2[o] = v2[t] + n2;
+    }
+  }
+}
+
+__global__ void merge_kernel(const float* __restrict__ d1, const int* __restrict__ idx,
+                             const float* __restrict__ d2, int nparts, int64_t stride, int64_t nq,
+                             float* __restrict__ od1, int* __restrict__ oidx,
+                             float* __restrict__ od2) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  float v1 = d1[q], v2 = d2[q];
+  int i1 = idx[q];
+  for (int p = 1; p < nparts; ++p)
+    merge2(v1, i1, v2, d1[p * stride + q], idx[p * stride + q], d2[p * stride + q]);
+  od1[q] = v1;
+  oidx[q] = i1;
+  od2[q] = v2;
+}
+
+__global__ void ratio_kernel(const float* __restrict__ cd1, const int* __restrict__ cidx,
+                             const float* __restrict__ cd2, int64_t nq, double ratio,
+                             float* __restrict__ d1, float* __restrict__ d2,
+                             int* __restrict__ idx1, uint8_t* __restrict__ good) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const float a = __fsqrt_rn(cd1[q]);   // OpenCV: std::sqrt(float) of the exact sum
+  const float b = __fsqrt_rn(cd2[q]);
+  d1[q] = a;
+  d2[q] = b;
+  idx1[q] = cidx[q];
+  good[q] = ((double)a < ratio * (double)b) ? 1 : 0;   // main.py:82, Python floats
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+int launch_pack_db(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n) {
+  const int64_t npad = ceil_div(n, SPS * kSubRows) * SPS * kSubRows;
+  ctx->nsub = npad / kSubRows;
+  SOD_TRY(sod_reserve(ctx, ctx->dbpack, (size_t)ctx->nsub * kSubBytes));
+  SOD_TRY(sod_reserve(ctx, ctx->dn, (size_t)npad));
+  const int64_t threads = npad * 16;
+  const int bs = 256;
+  const int64_t grid = ceil_div(threads, bs);
+  if (dtype == SOD_DTYPE_U8)
+    hipLaunchKernelGGL(pack_rows_kernel<uint8_t>, dim3((unsigned)grid), dim3(bs), 0, ctx->stream,
+                       (const uint8_t*)dsrc, n, npad, -2.0f, ctx->dbpack.p, ctx->dn.p, kPadNorm,
+                       ctx->flags.p, 1);
+  else
+    hipLaunchKernelGGL(pack_rows_kernel<float>, dim3((unsigned)grid), dim3(bs), 0, ctx->stream,
+                       (const float*)dsrc, n, npad, -2.0f, ctx->dbpack.p, ctx->dn.p, kPadNorm,
+                       ctx->flags.p, 1);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_pack_queries(sod_ctx* ctx, const void* dsrc, int dtype, int32_t nq) {
+  const int64_t npad = ceil_div(nq, kSubRows) * kSubRows;
+  ctx->nqt = (int32_t)(npad / kSubRows);
+  SOD_TRY(sod_reserve(ctx, ctx->qpack, (size_t)ctx->nqt * kSubBytes));
+  SOD_TRY(sod_reserve(ctx, ctx->qn, (size_t)npad));
+  const int64_t threads = npad * 16;
+  const int bs = 256;
+  const int64_t grid = ceil_div(threads, bs);
+  if (dtype == SOD_DTYPE_U8)
+    hipLaunchKernelGGL(pack_rows_kernel<uint8_t>, dim3((unsigned)grid), dim3(bs), 0, ctx->stream,
+                       (const uint8_t*)dsrc, (int64_t)nq, npad, 1.0f, ctx->qpack.p, ctx->qn.p, 0.0f,
+                       ctx->flags.p, 2);
+  else
+    hipLaunchKernelGGL(pack_rows_kernel<float>, dim3((unsigned)grid), dim3(bs), 0, ctx->stream,
+                       (const float*)dsrc, (int64_t)nq, npad, 1.0f, ctx->qpack.p, ctx->qn.p, 0.0f,
+                       ctx->flags.p, 2);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_match(sod_ctx* ctx) {
+  const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
+  const int qtiles_per_wg = NW * QT;
+  const int64_t qblocks = ceil_div(ctx->nqt, qtiles_per_wg);
+  const int64_t nstages = ctx->nsub / SPS;
+  // fill every CU twice (2 workgroups of 4 waves per CU); each split >= 1 stage
+  int64_t target = 2LL * ctx->num_cus;
+  int64_t split = std::max<int64_t>(1, (target + qblocks / 2) / qblocks);
+  split = std::min<int64_t>(split, nstages);
+  const int64_t st_per_split = ceil_div(nstages, split);
+  split = ceil_div(nstages, st_per_split);
+  ctx->split = (int)split;
+  SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(split * nq_pad)));
+  SOD_TRY(sod_reserve(ctx, ctx->pd2, (size_t)(split * nq_pad)));
+  SOD_TRY(sod_reserve(ctx, ctx->pidx, (size_t)(split * nq_pad)));
+  SOD_TRY(sod_reserve(ctx, ctx->cd1, (size_t)nq_pad));
+  SOD_TRY(sod_reserve(ctx, ctx->cd2, (size_t)nq_pad));
+  SOD_TRY(sod_reserve(ctx, ctx->cidx, (size_t)nq_pad));
+  const int64_t grid = qblocks * split;
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+  hipLaunchKernelGGL(match_kernel, dim3((unsigned)grid), dim3(NT), 0, ctx->stream,
+                     ctx->dbpack.p, ctx->dn.p, ctx->nsub, ctx->qpack.p, ctx->qn.p, ctx->nqt,
+                     nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset, ctx->pd1.p,
+                     ctx->pidx.p, ctx->pd2.p);
+  SOD_HIP(ctx, hipGetLastError());
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+  return launch_merge(ctx, ctx->pd1.p, ctx->pidx.p, ctx->pd2.p, (int)split, nq_pad);
+}
+
+int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2, int nparts,
+                 int64_t stride) {
+  const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
+  const int bs = 256;
+  hipLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, bs)), dim3(bs), 0, ctx->stream,
+                     d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p, ctx->cd2.p);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_ratio(sod_ctx* ctx, double ratio) {
+  SOD_TRY(sod_reserve(ctx, ctx->d1, (size_t)ctx->nq));
+  SOD_TRY(sod_reserve(ctx, ctx->d2, (size_t)ctx->nq));
+  SOD_TRY(sod_reserve(ctx, ctx->idx1, (size_t)ctx->nq));
+  SOD_TRY(sod_reserve(ctx, ctx->good, (size_t)ctx->nq));
+  const int bs = 256;
+  hipLaunchKernelGGL(ratio_kernel, dim3((unsigned)ceil_div(ctx->nq, bs)), dim3(bs), 0, ctx->stream,
+                     ctx->cd1.p, ctx->cidx.p, ctx->cd2.p, (int64_t)ctx->nq, ratio, ctx->d1.p,
+                     ctx->d2.p, ctx->idx1.p, ctx->good.p);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}

@@ -1,0 +1,171 @@
+// sod_internal.h -- device state of one libsod context (one GPU) and shared helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/sod.h"
+
+// ---------------------------------------------------------------------------------------
+// Matcher geometry (see match.hip for the rationale).
+//   subtile = 16 DB rows x 128 dims, stored in MFMA-fragment order: [kstep 4][lane 64][8 bf16]
+//   = 4 KiB.  The same packing is used for 16-query tiles.
+constexpr int kDim = 128;
+constexpr int kSubRows = 16;
+constexpr int kSubBytes = kSubRows * kDim * 2;   // 4096
+constexpr float kPadNorm = 1.0e30f;              // ||d||^2 of padding rows: never selected
+
+// Hough
+constexpr int kSigmaLutHalf = 255;               // i_sigma LUT over k = oQ - oM in [-255,255]
+constexpr int kSigmaLutSize = 2 * kSigmaLutHalf + 1;
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;  // capacity in elements
+};
+
+struct sod_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int num_cus = 256;
+
+  // ---- database (keypoints replicated, descriptors = shard) ----
+  int64_t n_total = 0;          // keypoints in the whole DB
+  int32_t n_images = 0;
+  DevBuf<float> mx, my, mang;
+  DevBuf<int32_t> moct, mimg;
+  DevBuf<double> cent;          // [n_images*2]
+  DevBuf<int32_t> isize;        // [n_images*2]
+  int64_t n_shard = 0;          // descriptor rows held here
+  int64_t row_offset = 0;       // global index of shard row 0
+  int64_t nsub = 0;             // 16-row subtiles (padded)
+  DevBuf<uint8_t> dbpack;       // nsub * 4096 bytes
+  DevBuf<float> dn;             // nsub * 16
+
+  // ---- query ----
+  int32_t nq = 0;
+  int32_t nqt = 0;              // 16-query tiles
+  DevBuf<uint8_t> qpack;        // nqt * 4096
+  DevBuf<float> qn;             // nqt * 16
+  DevBuf<float> qx, qy, qang;
+  DevBuf<int32_t> qoct;
+  DevBuf<uint8_t> stage_u8;     // upload staging for descriptors
+  DevBuf<float> stage_f32;
+
+  // ---- matcher outputs ----
+  int split = 1;                // DB splits of the current launch
+  DevBuf<float> pd1, pd2;       // [split * nq_pad]
+  DevBuf<int32_t> pidx;
+  DevBuf<float> cd1, cd2;       // merged (this shard / after allgather: global)  [nq_pad]
+  DevBuf<int32_t> cidx;
+  DevBuf<float> gd1, gd2;       // allgather landing [nranks * nq_pad]
+  DevBuf<int32_t> gidx;
+  DevBuf<float> d1, d2;         // sqrt distances [nq]
+  DevBuf<int32_t> idx1;         // [nq]
+  DevBuf<uint8_t> good;         // [nq]
+  DevBuf<uint32_t> flags;       // [0]=invalid descriptor count, [1]=max dn bits, [2]=max qn bits
+  bool matched = false, ratio_done = false;
+
+  // ---- hough ----
+  int32_t bins[4] = {0, 0, 0, 0};
+  int64_t nbins = 0;
+  int32_t qh = 0, qw = 0;
+  DevBuf<int32_t> sig_lut;      // [511]
+  DevBuf<uint32_t> counts;      // [nbins]
+  DevBuf<uint32_t> first;       // [nbins] min vote ordinal q*16+slot
+  DevBuf<uint32_t> basekey;     // [nq] ix | iy<<8 | it<<16 | is<<24
+  DevBuf<uint32_t> vmask;       // [nq] 16-bit vote mask (0 = no vote)
+  DevBuf<double> pose;          // [nq*4]
+  bool houghed = false;
+
+  // ---- select / CSR / means ----
+  DevBuf<uint32_t> blk;         // block counts / offsets for compaction
+  DevBuf<uint32_t> scal;        // device scalars: [0]=V, [1]=total members, [2]=B (all bins)
+  DevBuf<uint32_t> vbin;        // [vmax] linear bin id, first-touch order
+  DevBuf<int64_t> voff;         // [vmax+1]
+  DevBuf<int32_t> members;      // [mmax] query index
+  DevBuf<double> means;         // [vmax*6]
+  DevBuf<uint32_t> allbin;      // [bmax] all occupied bins, first-touch order
+  int64_t vmax = 0, mmax = 0;
+  int32_t vote_thr = 0;
+  bool selected = false;
+
+  // ---- affine ----
+  DevBuf<float> amx, amy, aqx, aqy;  // per-member points [mmax]
+  DevBuf<int32_t> aisig;        // per-bin i_sigma [vmax]
+  DevBuf<uint8_t> surv;         // [vmax]
+  DevBuf<int32_t> fvotes;       // [vmax]
+  DevBuf<double> params;        // [vmax*6]
+  DevBuf<uint8_t> alive;        // [mmax]
+  bool affined = false;
+
+  // ---- comm ----
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+
+  // ---- timing ----
+  hipEvent_t ev[8] = {};
+  float last_ms[6] = {0, 0, 0, 0, 0, 0};
+};
+
+// error helpers ---------------------------------------------------------------------------
+int sod_fail(sod_ctx* ctx, int code, const std::string& msg);
+#define SOD_HIP(ctx, call)                                                          \
+  do {                                                                              \
+    hipError_t e_ = (call);                                                         \
+    if (e_ != hipSuccess)                                                           \
+      return sod_fail((ctx), SOD_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define SOD_TRY(x)          \
+  do {                      \
+    int r_ = (x);           \
+    if (r_ != SOD_OK) return r_; \
+  } while (0)
+
+template <typename T>
+int sod_reserve(sod_ctx* ctx, DevBuf<T>& b, size_t n) {
+  if (n == 0) n = 1;
+  if (b.n >= n) return SOD_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+  hipError_t e = hipMalloc((void**)&b.p, n * sizeof(T));
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    return sod_fail(ctx, SOD_ENOMEM, "hipMalloc(" + std::to_string(n * sizeof(T)) + " B): " +
+                                          hipGetErrorString(e));
+  }
+  b.n = n;
+  return SOD_OK;
+}
+template <typename T>
+void sod_release(DevBuf<T>& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+}
+
+// kernel launchers implemented in the .hip files ----------------------------------------
+int launch_pack_db(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n);
+int launch_pack_queries(sod_ctx* ctx, const void* dsrc, int dtype, int32_t nq);
+int launch_match(sod_ctx* ctx);
+int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2,
+                 int nparts, int64_t stride);
+int launch_ratio(sod_ctx* ctx, double ratio);
+int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi);
+int launch_select(sod_ctx* ctx, int32_t thr);
+int launch_all_bins(sod_ctx* ctx);
+int launch_affine_gather(sod_ctx* ctx);
+int launch_affine(sod_ctx* ctx, int64_t nbins_dev_scalar_or_host, bool count_on_device,
+                  const int64_t* offsets, const float* mx, const float* my, const float* qx,
+                  const float* qy, const int32_t* isig, int32_t qw, int32_t qh, double xf,
+                  double yf, int32_t thr, int32_t max_iter, uint8_t* surv, int32_t* votes,
+                  double* params, uint8_t* alive, const uint32_t* dev_count);
+int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
+                      const float* ma, const int32_t* mo, const float* qx, const float* qy,
+                      const float* qa, const int32_t* qo, const double* cx, const double* cy,
+                      double* pose, int32_t* idx);
+int sod_build_sigma_lut(sod_ctx* ctx, int32_t bins_sigma);

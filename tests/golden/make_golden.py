@@ -1,0 +1,301 @@
+"""Generate the committed golden fixtures by running the REFERENCE'S OWN Python
+code (build container only; ``/root/reference`` does not exist on the GPU box).
+
+    python tests/golden/make_golden.py
+
+The reference modules import ``cv2`` (OpenCV, absent here), so a stub module
+providing only ``cv2.KeyPoint`` is injected (the hot-path modules touch nothing
+else of cv2 at import or in the stages used: ``SiftHelperFunctions.py:47``).
+``Main()`` needs matplotlib (present; Agg backend).  Inputs are seeded synthetic
+workloads; matches are produced by the oracle's exact brute-force matcher
+(OpenCV's matcher is not available -- see oracle/oracle.py header) and fed to
+``Main.matching_keypoints`` in the reference's tuple format
+(``main.py:85-86``).  The reference stages then run unchanged:
+``apply_hough_transform`` -> ``get_valid_bins`` -> ``apply_affine_parameters``
+(-> ``post_process``), and their outputs are stored as plain arrays (.npz,
+no pickles).
+
+Only data is written: inputs and the reference's outputs.
+"""
+import math
+import os
+import sys
+import types
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+
+class KeyPoint:
+    """Stand-in for cv2.KeyPoint: pt/size/angle/response are float32 fields in
+    OpenCV (cv::Point2f, float), octave/class_id ints."""
+
+    def __init__(self, x=0.0, y=0.0, _size=0.0, _angle=-1.0, _response=0.0,
+                 _octave=0, _class_id=-1):
+        self.pt = (float(np.float32(x)), float(np.float32(y)))
+        self.size = float(np.float32(_size))
+        self.angle = float(np.float32(_angle))
+        self.response = float(np.float32(_response))
+        self.octave = int(_octave)
+        self.class_id = int(_class_id)
+
+
+def import_reference():
+    import matplotlib
+    matplotlib.use("Agg")
+    cv2 = types.ModuleType("cv2")
+    cv2.KeyPoint = KeyPoint
+    sys.modules["cv2"] = cv2
+    sys.path.insert(0, REF)
+    import main as ref_main  # noqa: E402
+    import HoughTransformHelperFunctions as ref_ht  # noqa: E402
+    return ref_main, ref_ht
+
+
+def kp_objects(kp):
+    return [KeyPoint(x=float(kp.x[i]), y=float(kp.y[i]), _size=2.0,
+                     _angle=float(kp.angle[i]), _octave=int(kp.octave[i]))
+            for i in range(len(kp))]
+
+
+def run_reference(ref_main, qkp, dbkp, db_img, centroid, size, matches, shape, bins,
+                  vote_thr=5, affine_thr=4, post=True):
+    """Drive the reference stages on a given match list [(q, m), ...]."""
+    M = ref_main.Main()
+    M.rgb_query = types.SimpleNamespace(shape=tuple(shape))
+    M.image_query_size = (shape[1], shape[0])        # main.py:45 (width, height)
+    kq = kp_objects(qkp)
+    km = kp_objects(dbkp)
+    ident = {}
+    for q, m in matches:
+        im = int(db_img[m])
+        tup = (km[m], kq[q], (int(size[im][0]), int(size[im][1])),
+               (float(centroid[im][0]), float(centroid[im][1])))
+        M.matching_keypoints.append(tup)
+        ident[(id(km[m]), id(kq[q]))] = (q, m)
+
+    M.apply_hough_transform(bins)
+    keys = list(M.hough_transform.keys())
+    table_keys = np.array(keys, np.int32).reshape(-1, 4)
+    table_votes = np.array([M.hough_transform[k].votes for k in keys], np.int32)
+
+    M.get_valid_bins(vote_thr)
+    vb = M.valid_bins
+    v_keys = np.array([b.pose for b in vb], np.int32).reshape(-1, 4)
+    v_votes = np.array([b.votes for b in vb], np.int32)
+    v_off = np.zeros(len(vb) + 1, np.int64)
+    v_mem = []
+    for i, b in enumerate(vb):
+        mem = [ident[(id(p[0]), id(p[1]))][0] for p in b.keypoint_pairs]
+        v_mem.extend(mem)
+        v_off[i + 1] = len(v_mem)
+    v_means = np.array([[b.centroid[0], b.centroid[1], b.angle, b.scale,
+                         float(b.img_size[0]), float(b.img_size[1])] for b in vb],
+                       np.float64).reshape(-1, 6)
+
+    pre_poses = [b.pose for b in vb]
+    M.apply_affine_parameters(affine_thr)
+    sv = M.valid_bins
+    s_keys = np.array([b.pose for b in sv], np.int32).reshape(-1, 4)
+    s_index = np.array([pre_poses.index(b.pose) for b in sv], np.int32)
+    s_votes = np.array([b.votes for b in sv], np.int32)
+    s_params = np.array([list(map(float, b.affine_parameters)) for b in sv],
+                        np.float64).reshape(-1, 6)
+    s_off = np.zeros(len(sv) + 1, np.int64)
+    s_mem = []
+    for i, b in enumerate(sv):
+        s_mem.extend(ident[(id(p[0]), id(p[1]))][0] for p in b.keypoint_pairs)
+        s_off[i + 1] = len(s_mem)
+    out = dict(table_keys=table_keys, table_votes=table_votes,
+               valid_keys=v_keys, valid_votes=v_votes, valid_off=v_off,
+               valid_members=np.array(v_mem, np.int32), valid_means=v_means,
+               surv_keys=s_keys, surv_index=s_index, surv_votes=s_votes,
+               surv_params=s_params, surv_off=s_off,
+               surv_members=np.array(s_mem, np.int32))
+    if post:
+        try:
+            M.post_process()
+            fp = M.final_pose
+            out["final_pose"] = np.array(
+                [[p[0][0], p[0][1], p[1], p[2], float(p[3][0]), float(p[3][1])] for p in fp],
+                np.float64).reshape(-1, 6)
+        except Exception as e:  # post-processing is out of scope; record only
+            print("post_process failed:", e)
+    return out
+
+
+def pose_sweep(ref_ht, rng, n, bins_list, shape):
+    """Per-element golden vectors for estimate_object_pose/calculate_bin_index."""
+    mx = rng.uniform(-50, 1600, n).astype(np.float32)
+    my = rng.uniform(-50, 1300, n).astype(np.float32)
+    qx = rng.uniform(-100, 1100, n).astype(np.float32)
+    qy = rng.uniform(-100, 900, n).astype(np.float32)
+    ma = rng.uniform(0, 360, n).astype(np.float32)
+    qa = rng.uniform(0, 360, n).astype(np.float32)
+    # exact-angle edge cases: equal angles, 0/360-ish, theta near bin edges
+    ma[:64] = qa[:64]
+    qa[64:96] = 0.0
+    ma[64:96] = np.float32(359.99997)
+    moct = rng.integers(-1, 8, n)
+    qoct = rng.integers(-1, 8, n)
+    moct[:200] = rng.integers(-128, 127, 200)
+    qoct[:200] = rng.integers(-128, 127, 200)
+    mlay = rng.integers(0, 4, n)
+    qlay = rng.integers(0, 4, n)
+    mo = ((moct & 0xFF) | (mlay << 8)).astype(np.int32)
+    qo = ((qoct & 0xFF) | (qlay << 8)).astype(np.int32)
+    cx = rng.uniform(0, 1500, n)
+    cy = rng.uniform(0, 1200, n)
+    poses = np.zeros((n, 4), np.float64)
+    idx = np.zeros((len(bins_list), n, 4), np.int32)
+    for i in range(n):
+        kM = KeyPoint(x=mx[i], y=my[i], _angle=ma[i], _octave=int(mo[i]))
+        kQ = KeyPoint(x=qx[i], y=qy[i], _angle=qa[i], _octave=int(qo[i]))
+        p = ref_ht.estimate_object_pose((kM, kQ, (1500, 1000), (cx[i], cy[i])))
+        poses[i] = p
+        for j, b in enumerate(bins_list):
+            idx[j, i] = ref_ht.calculate_bin_index(p, b, shape)
+    return dict(mx=mx, my=my, ma=ma, mo=mo, qx=qx, qy=qy, qa=qa, qo=qo, cx=cx, cy=cy,
+                poses=poses, idx=idx, bins=np.array(bins_list, np.int32),
+                shape=np.array(shape, np.int32))
+
+
+def edge_case(rng):
+    """Hand-shaped matches: a tight planted cluster with outliers, a cluster of
+    queries all matched to ONE model keypoint (rank-deficient A^T A), a cluster
+    whose scale bin is 0 (zero outlier tolerance), off-image poses and theta
+    near 2*pi."""
+    from sift_based_od_amd.database import Keypoints
+    nimg = 2
+    size = np.array([[1500, 1000], [1500, 900]], np.int32)
+    nm = 400
+    mx = rng.uniform(0, 1500, nm).astype(np.float32)
+    my = rng.uniform(0, 900, nm).astype(np.float32)
+    ma = rng.uniform(0, 360, nm).astype(np.float32)
+    mo = np.zeros(nm, np.int32) | (1 << 8)
+    img = (np.arange(nm) >= 200).astype(np.int32)
+    cen = np.array([[float(np.cumsum(mx[:200].astype(np.float64))[-1]) / 200,
+                     float(np.cumsum(my[:200].astype(np.float64))[-1]) / 200],
+                    [float(np.cumsum(mx[200:].astype(np.float64))[-1]) / 200,
+                     float(np.cumsum(my[200:].astype(np.float64))[-1]) / 200]])
+    qx, qy, qa, qo, mlist = [], [], [], [], []
+
+    def add(m, x, y, a, o):
+        mlist.append(m); qx.append(x); qy.append(y); qa.append(a); qo.append(o)
+
+    # (1) planted similarity cluster, scale 2 (octave +1), theta 30deg, + outliers
+    th = math.radians(30.0)
+    for m in range(0, 60):
+        dx, dy = float(mx[m]) - cen[0, 0], float(my[m]) - cen[0, 1]
+        add(m, 500 + 2 * (math.cos(th) * dx - math.sin(th) * dy) + rng.normal(0, 0.5),
+            400 + 2 * (math.sin(th) * dx + math.cos(th) * dy) + rng.normal(0, 0.5),
+            (float(ma[m]) + 30.0) % 360.0, 2 | (1 << 8))
+    for m in range(60, 70):   # gross outliers inside the same pose bin
+        dx, dy = float(mx[m]) - cen[0, 0], float(my[m]) - cen[0, 1]
+        add(m, 500 + 2 * (math.cos(th) * dx - math.sin(th) * dy) + rng.normal(0, 40),
+            400 + 2 * (math.sin(th) * dx + math.cos(th) * dy) + rng.normal(0, 40),
+            (float(ma[m]) + 30.0) % 360.0, 2 | (1 << 8))
+    # (2) twelve queries all matched to model keypoint 210 (same model point)
+    for j in range(12):
+        add(210, 300 + rng.normal(0, 0.3), 200 + rng.normal(0, 0.3),
+            (float(ma[210]) + 359.9) % 360.0, 1 | (2 << 8))
+    # (3) scale bin 0 cluster: query octave <= model octave
+    for m in range(220, 250):
+        dx, dy = float(mx[m]) - cen[1, 0], float(my[m]) - cen[1, 1]
+        add(m, 700 + 0.5 * dx, 300 + 0.5 * dy, float(ma[m]), 0xFF)
+    # (4) off-image poses (negative / beyond width) and theta wrap
+    for m in range(250, 280):
+        add(m, float(rng.uniform(-400, 0)), float(rng.uniform(1000, 1500)),
+            float(rng.uniform(0, 360)), int(rng.integers(0, 4)))
+    n = len(mlist)
+    qkp = Keypoints(np.array(qx, np.float32), np.array(qy, np.float32),
+                    np.array(qa, np.float32), np.array(qo, np.int32))
+    dbkp = Keypoints(mx, my, ma, mo)
+    matches = [(i, mlist[i]) for i in range(n)]
+    return qkp, dbkp, img, cen, size, matches
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def kp_arrays(prefix, kp):
+    return {prefix + "x": kp.x, prefix + "y": kp.y, prefix + "angle": kp.angle,
+            prefix + "octave": kp.octave}
+
+
+def main():
+    import sod_pkg
+    sod_pkg.load()
+    from sift_based_od_amd import synthetic
+    from oracle import oracle as orc
+
+    ref_main, ref_ht = import_reference()
+
+    # ---- per-element pose / bin-index sweep (A4-A6) ----
+    rng = np.random.default_rng(1234)
+    sweep = pose_sweep(ref_ht, rng, 20000, [15, 12, 8, 32], (800, 1000, 3))
+    save("pose_sweep", **sweep)
+
+    # ---- end-to-end cases (A2, A7-A13) ----
+    cases = [
+        # name, n_images, kp/img, n_queries, planted, bins
+        ("c1_b15", 2, 250, 500, 0.3, 15),
+        ("planted_b15", 4, 500, 3000, 0.3, 15),
+        ("planted_b12", 6, 400, 2500, 0.4, 12),
+    ]
+    for name, nimg, kpi, nq, pf, bins in cases:
+        db = synthetic.make_database(nimg, kpi, seed=7)
+        qs = synthetic.make_queries(nq, seed=8, db_seed=7, kp_per_image=kpi,
+                                    planted_frac=pf, n_objects=min(4, nimg))
+        idx1, d1, d2 = orc.knn2_match(qs.des, db.des)
+        i2, e1, e2 = orc.knn2_match_int(qs.des, db.des)
+        assert np.array_equal(idx1, i2) and np.array_equal(d1, e1) and np.array_equal(d2, e2)
+        good = orc.ratio_test(d1, d2)
+        matches = [(int(q), int(idx1[q])) for q in np.nonzero(good)[0]]
+        out = run_reference(ref_main, qs.kp, db.kp, db.img, db.centroid, db.size,
+                            matches, qs.shape, bins)
+        print(name, "matches", len(matches), "bins", len(out["table_votes"]),
+              "valid", len(out["valid_votes"]), "surv", len(out["surv_votes"]))
+        save(name, q_des=qs.des, db_des=db.des, db_img=db.img, centroid=db.centroid,
+             size=db.size, shape=np.array(qs.shape, np.int32), bins=np.int32(bins),
+             idx1=idx1, d1=d1, d2=d2, good=good,
+             **kp_arrays("q_", qs.kp), **kp_arrays("db_", db.kp), **out)
+
+    # ---- hand-shaped Hough/affine edge case (matches given directly) ----
+    qkp, dbkp, img, cen, size, matches = edge_case(np.random.default_rng(99))
+    for bins in (15, 6):
+        out = run_reference(ref_main, qkp, dbkp, img, cen, size, matches,
+                            (1000, 1200, 3), bins)
+        print("edge", bins, "bins", len(out["table_votes"]), "valid",
+              len(out["valid_votes"]), "surv", len(out["surv_votes"]))
+        save("edge_b%d" % bins, db_img=img, centroid=cen, size=size,
+             shape=np.array((1000, 1200, 3), np.int32), bins=np.int32(bins),
+             match_q=np.array([q for q, _ in matches], np.int32),
+             match_m=np.array([m for _, m in matches], np.int32),
+             **kp_arrays("q_", qkp), **kp_arrays("db_", dbkp), **out)
+
+    # ---- matcher edge cases (int64 brute force; OpenCV absent: unpinned) ----
+    rng = np.random.default_rng(5)
+    db = rng.integers(0, 256, (300, 128)).astype(np.uint8)
+    db[150] = db[20]          # exact duplicate rows -> tie, lower index wins
+    db[151] = db[20]
+    q = rng.integers(0, 256, (200, 128)).astype(np.uint8)
+    q[:10] = db[20]           # d1 == 0, tie between rows 20/150/151
+    q[10:20] = db[:10]        # exact hits
+    q[20] = 255               # extremes
+    q[21] = 0
+    i1, e1, e2 = orc.knn2_match_int(q, db)
+    save("matcher_edges", q_des=q, db_des=db, idx1=i1, d1=e1, d2=e2,
+         good=orc.ratio_test(e1, e2))
+
+
+if __name__ == "__main__":
+    main()
