@@ -101,6 +101,7 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->first); sod_release(ctx->basekey); sod_release(ctx->vmask);
   sod_release(ctx->pose); sod_release(ctx->blk); sod_release(ctx->scal); sod_release(ctx->vbin);
   sod_release(ctx->voff); sod_release(ctx->members); sod_release(ctx->means);
+  sod_release(ctx->mq);
   sod_release(ctx->allbin); sod_release(ctx->amx); sod_release(ctx->amy); sod_release(ctx->aqx);
   sod_release(ctx->aqy); sod_release(ctx->aisig); sod_release(ctx->surv);
   sod_release(ctx->fvotes); sod_release(ctx->params); sod_release(ctx->alive);

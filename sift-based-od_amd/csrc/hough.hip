@@ -362,35 +362,48 @@ __global__ __launch_bounds__(256) void members_kernel(
   }
 }
 
-// PoseBin running means in vote order (PoseBin.py:19-43): one thread per valid bin
+// PoseBin running means in vote order (PoseBin.py:19-43).  The recurrence
+//   v' = (v*n + new) / (n+1)
+// rounds at every step, so each bin's chain is inherently sequential; but the six
+// quantities are independent chains and their inputs can be fetched in parallel first:
+// means_gather_kernel writes per-member SoA values (x, y, alpha, s, w, h), then
+// means_kernel runs one thread per (bin, quantity) streaming contiguous memory.
+__global__ void means_gather_kernel(const uint32_t* __restrict__ scal,
+                                    const int32_t* __restrict__ members,
+                                    const double* __restrict__ pose, const int* __restrict__ idx1,
+                                    const int* __restrict__ mimg, const int* __restrict__ isize,
+                                    int64_t mstride, double* __restrict__ mq) {
+  const int64_t M = scal[1];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = members[e];
+    const double* p = pose + 4 * (int64_t)q;
+    const int im = mimg[idx1[q]];
+    mq[0 * mstride + e] = p[0];
+    mq[1 * mstride + e] = p[1];
+    mq[2 * mstride + e] = p[2];
+    mq[3 * mstride + e] = p[3];
+    mq[4 * mstride + e] = (double)isize[2 * im];
+    mq[5 * mstride + e] = (double)isize[2 * im + 1];
+  }
+}
+
 __global__ void means_kernel(const uint32_t* __restrict__ scal, const int64_t* __restrict__ voff,
-                             const int32_t* __restrict__ members, const double* __restrict__ pose,
-                             const int* __restrict__ idx1, const int* __restrict__ mimg,
-                             const int* __restrict__ isize, double* __restrict__ means) {
+                             const double* __restrict__ mq, int64_t mstride,
+                             double* __restrict__ means) {
   const int64_t V = scal[0];
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
-       v += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < 6 * V;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = t / 6;
+    const int k = (int)(t % 6);
     const int64_t a = voff[v], e = voff[v + 1];
-    double cx = 0, cy = 0, an = 0, sc = 0, w = 0, h = 0;
-    for (int64_t j = a; j < e; ++j) {
-      const int q = members[j];
-      const double* p = pose + 4 * (int64_t)q;
-      const int im = mimg[idx1[q]];
-      const double iw = (double)isize[2 * im], ih = (double)isize[2 * im + 1];
-      if (j == a) {
-        cx = p[0]; cy = p[1]; an = p[2]; sc = p[3]; w = iw; h = ih;
-      } else {
-        const double n = (double)(j - a), n1 = (double)(j - a + 1);
-        cx = (cx * n + p[0]) / n1;
-        cy = (cy * n + p[1]) / n1;
-        an = (an * n + p[2]) / n1;
-        sc = (sc * n + p[3]) / n1;
-        w = (w * n + iw) / n1;
-        h = (h * n + ih) / n1;
-      }
+    const double* x = mq + k * mstride;
+    double m = x[a];                       // first vote: mean = pose / model size
+    for (int64_t j = a + 1; j < e; ++j) {
+      const double n = (double)(j - a);
+      m = (m * n + x[j]) / (n + 1.0);      // n + 1 is an exact small integer
     }
-    double* o = means + 6 * v;
-    o[0] = cx; o[1] = cy; o[2] = an; o[3] = sc; o[4] = w; o[5] = h;
+    means[6 * v + k] = m;
   }
 }
 
@@ -639,9 +652,13 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
                      ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
                      ctx->vmask.p, ctx_bins(ctx), ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus)), dim3(64), 0, ctx->stream,
-                     ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->pose.p, ctx->idx1.p,
-                     ctx->mimg.p, ctx->isize.p, ctx->means.p);
+  SOD_TRY(sod_reserve(ctx, ctx->mq, (size_t)ctx->mmax * 6));
+  hipLaunchKernelGGL(means_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
+                     ctx->stream, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p,
+                     ctx->mimg.p, ctx->isize.p, ctx->mmax, ctx->mq.p);
+  SOD_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus * 2)), dim3(64), 0, ctx->stream,
+                     ctx->scal.p, ctx->voff.p, ctx->mq.p, ctx->mmax, ctx->means.p);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }

@@ -21,8 +21,10 @@
 // lane can improve does the exact top-2 update run (rare after the first few thousand rows).
 //
 // Decomposition.  A workgroup = NW waves x QT query tiles (512 queries) kept in VGPRs for
-// the whole launch; it streams one DB split through a 2-stage LDS ring (register staging,
-// one barrier per stage).  Grid = query blocks x DB splits, sized to fill every CU twice;
+// the whole launch; it streams one DB split through a 3-slot LDS ring filled by LDS-DMA
+// (global_load_lds, two stages in flight, counted vmcnt + raw s_barrier, one barrier per
+// 64-row stage).  Per 16-row subtile a wave issues 32 MFMAs into 8 independent
+// accumulators, then one compare pass and ONE wave-uniform branch.  Grid = query blocks x DB splits, sized to fill every CU twice;
 // per-split partial top-2 are merged by merge_kernel (also used for the multi-GPU merge).
 #include "sod_internal.h"
 
@@ -37,11 +39,8 @@ constexpr int SPS = 4;   // 16-row subtiles per LDS stage (64 rows = 16 KiB)
 constexpr int NT = NW * 64;
 constexpr int kStageBytes = SPS * kSubBytes;
 constexpr int kStageNorm = SPS * kSubRows * 4;
-constexpr int kStageU4 = kStageBytes / 16 / NT;  // uint4 per thread per stage
 constexpr float kInit = 3.0e38f;
 
-static_assert(kStageBytes % (16 * NT) == 0, "stage must split evenly over the workgroup");
-static_assert(kStageNorm / 16 <= NT, "norm copy uses one uint4 per thread");
 
 // ---------------------------------------------------------------------------------------
 // pack: rows -> MFMA-fragment order, bf16 (x scale), plus exact squared norms.
@@ -114,12 +113,42 @@ __device__ __forceinline__ void merge2(float& v1, int& i1, float& v2, float o1, 
   }
 }
 
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void glds16(const void* g, uint8_t* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_base, 16, 0, 0);
+}
+
+// LDS-DMA ring: stage s lives in buffer s % kRing.  Every wave issues kGldsPerStage
+// wave-instructions per stage (4 x 1 KiB of fragments + 1 x 64 B of row norms), so a
+// counted vmcnt says exactly which stage has landed (MI355X: vmcnt counts LDS-DMA in order).
+constexpr int kRing = 3;
+constexpr int kStageSlot = kStageBytes + kStageNorm;   // 16640 B, a multiple of 16
+constexpr int kGldsPerStage = kStageBytes / 1024 / NW + 1;
+static_assert(kStageBytes / 1024 % NW == 0, "fragment pieces split evenly over waves");
+static_assert(kGldsPerStage == 5, "vmcnt immediates below assume 5 LDS-DMA per stage");
+
+__device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
+                                            const float* __restrict__ dn, int64_t sub0,
+                                            uint8_t* slot, int wave, int lane) {
+  const uint8_t* src = dbpack + sub0 * kSubBytes;
+#pragma unroll
+  for (int j = 0; j < kStageBytes / 1024 / NW; ++j) {
+    const int piece = wave * (kStageBytes / 1024 / NW) + j;
+    glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
+  }
+  // row norms: 64 rows x 4 B = 256 B, 64 B (4 lanes) per wave
+  const float* nsrc = dn + sub0 * kSubRows + wave * 16 + lane * 4;
+  if (lane < 4) glds16(nsrc, slot + kStageBytes + wave * 64);
+}
+
 __global__ __launch_bounds__(NT, 2) void match_kernel(
     const uint8_t* __restrict__ dbpack, const float* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const float* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2][kStageBytes + kStageNorm];
+  // ONE __shared__ array (a second one can make hipcc drain vmcnt before every ds_read)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageSlot];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -127,6 +156,14 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
   const int sp = blockIdx.x % split;
   const int qb = blockIdx.x / split;
   const int qt0 = (qb * NW + wave) * QT;
+
+  const int64_t s_lo = (int64_t)sp * sub_per_split;
+  const int64_t s_hi = min(nsub, s_lo + sub_per_split);
+  const int64_t nst = (s_hi - s_lo) / SPS;  // nsub and sub_per_split are multiples of SPS
+
+  // prologue: two stages in flight before the queries are even loaded
+  if (nst > 0) issue_stage(dbpack, dn, s_lo, lds, wave, lane);
+  if (nst > 1) issue_stage(dbpack, dn, s_lo + SPS, lds + kStageSlot, wave, lane);
 
   // queries: B fragments stay in registers for the whole launch
   bf16x8 bq[QT][4];
@@ -150,35 +187,17 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
     id[t] = 0x7fffffff;
   }
 
-  const int64_t s_lo = (int64_t)sp * sub_per_split;
-  const int64_t s_hi = min(nsub, s_lo + sub_per_split);
-  const int64_t nst = (s_hi - s_lo) / SPS;  // nsub and sub_per_split are multiples of SPS
-
-  uint4 st[kStageU4];
-  uint4 stn = make_uint4(0, 0, 0, 0);
-  auto gload = [&](int64_t sub0) {
-    const uint4* src = reinterpret_cast<const uint4*>(dbpack + sub0 * kSubBytes);
-#pragma unroll
-    for (int j = 0; j < kStageU4; ++j) st[j] = src[j * NT + tid];
-    if (tid < kStageNorm / 16) stn = reinterpret_cast<const uint4*>(dn + sub0 * kSubRows)[tid];
-  };
-  auto lstore = [&](int buf) {
-    uint4* dst = reinterpret_cast<uint4*>(lds[buf]);
-#pragma unroll
-    for (int j = 0; j < kStageU4; ++j) dst[j * NT + tid] = st[j];
-    if (tid < kStageNorm / 16) reinterpret_cast<uint4*>(lds[buf] + kStageBytes)[tid] = stn;
-  };
-
-  if (nst > 0) {
-    gload(s_lo);
-    lstore(0);
-  }
-  __syncthreads();
-
+  int slot_r = 0;            // buffer of stage s
+  int slot_w = 2;            // buffer of stage s + 2
   for (int64_t s = 0; s < nst; ++s) {
-    const int buf = (int)(s & 1);
-    if (s + 1 < nst) gload(s_lo + (s + 1) * SPS);
-    const uint8_t* sb = lds[buf];
+    // stage s has landed for this wave once at most one younger stage is outstanding
+    if (s + 1 < nst)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // ... and for every wave; also: stage s-1 fully read
+    if (s + 2 < nst) issue_stage(dbpack, dn, s_lo + (s + 2) * SPS, lds + slot_w * kStageSlot, wave, lane);
+    const uint8_t* sb = lds + slot_r * kStageSlot;
 #pragma unroll
     for (int u = 0; u < SPS; ++u) {
       const uint8_t* base = sb + u * kSubBytes + lane * 16;
@@ -187,28 +206,37 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
       const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(base + 2048);
       const bf16x8 a3 = *reinterpret_cast<const bf16x8*>(base + 3072);
       const f32x4 cn = *reinterpret_cast<const f32x4*>(sb + kStageBytes + u * 64 + (lane >> 4) * 16);
-      const int rowb = row_offset + (int)((s_lo + s * SPS + u) * kSubRows) + (lane >> 4) * 4;
+      f32x4 acc[QT];
 #pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[t][0], cn, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bq[t][1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bq[t][2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, bq[t][3], acc, 0, 0, 0);
-        const float m = fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3]));
-        if (__any(m < v2[t])) {
+      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[t][0], cn, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bq[t][1], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bq[t][2], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, bq[t][3], acc[t], 0, 0, 0);
+      // prefilter: can any of this lane's 4 x QT candidates beat a running 2nd best?
+      bool hit = false;
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+        hit |= (acc[t][0] < v2[t]) | (acc[t][1] < v2[t]) | (acc[t][2] < v2[t]) | (acc[t][3] < v2[t]);
+      if (__any(hit)) {
+        const int rowb = row_offset + (int)((s_lo + s * SPS + u) * kSubRows) + (lane >> 4) * 4;
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float x = acc[r];
+            const float x = acc[t][r];
             const bool lt = x < v1[t];
             v2[t] = __builtin_amdgcn_fmed3f(v1[t], v2[t], x);
             id[t] = lt ? rowb + r : id[t];
-            v1[t] = fminf(v1[t], x);
+            v1[t] = lt ? x : v1[t];
           }
         }
       }
     }
-    if (s + 1 < nst) lstore(buf ^ 1);
-    __syncthreads();
+    slot_r = slot_r == kRing - 1 ? 0 : slot_r + 1;
+    slot_w = slot_w == kRing - 1 ? 0 : slot_w + 1;
   }
 
   // merge the 4 row groups of each query (lanes l, l^16, l^32, l^48)
@@ -248,14 +276,43 @@ __global__ void merge_kernel(const float* __restrict__ d1, const int* __restrict
   od2[q] = v2;
 }
 
+// Correctly rounded sqrt of an exact integer-valued float n >= 0 (OpenCV: std::sqrt on
+// the float sum).  The hardware estimate is within an ulp; it is then corrected with the
+// exact midpoint test: a midpoint m of two adjacent floats has <= 25 significant bits, so
+// m*m is exact in f64 and compares exactly with n (ties -> even).
+__device__ __forceinline__ float sqrt_rn_exact(float n) {
+#pragma clang fp contract(off)
+  float s = sqrtf(n);
+  const double dn = (double)n;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const float up = __uint_as_float(__float_as_uint(s) + 1u);   // s >= 0, finite
+    const double mh = 0.5 * ((double)s + (double)up);
+    const double h2 = mh * mh;
+    if (h2 < dn || (h2 == dn && (__float_as_uint(up) & 1u) == 0u)) {
+      s = up;
+      continue;
+    }
+    const float lo = s > 0.0f ? __uint_as_float(__float_as_uint(s) - 1u) : s;
+    const double ml = 0.5 * ((double)s + (double)lo);
+    const double l2 = ml * ml;
+    if (lo != s && (l2 > dn || (l2 == dn && (__float_as_uint(lo) & 1u) == 0u))) {
+      s = lo;
+      continue;
+    }
+    break;
+  }
+  return s;
+}
+
 __global__ void ratio_kernel(const float* __restrict__ cd1, const int* __restrict__ cidx,
                              const float* __restrict__ cd2, int64_t nq, double ratio,
                              float* __restrict__ d1, float* __restrict__ d2,
                              int* __restrict__ idx1, uint8_t* __restrict__ good) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
-  const float a = __fsqrt_rn(cd1[q]);   // OpenCV: std::sqrt(float) of the exact sum
-  const float b = __fsqrt_rn(cd2[q]);
+  const float a = sqrt_rn_exact(cd1[q]);   // OpenCV: std::sqrt(float) of the exact sum
+  const float b = sqrt_rn_exact(cd2[q]);
   d1[q] = a;
   d2[q] = b;
   idx1[q] = cidx[q];

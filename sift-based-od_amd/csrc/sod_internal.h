@@ -88,6 +88,7 @@ struct sod_ctx {
   DevBuf<int64_t> voff;         // [vmax+1]
   DevBuf<int32_t> members;      // [mmax] query index
   DevBuf<double> means;         // [vmax*6]
+  DevBuf<double> mq;            // [6][mmax] per-member mean inputs
   DevBuf<uint32_t> allbin;      // [bmax] all occupied bins, first-touch order
   int64_t vmax = 0, mmax = 0;
   int32_t vote_thr = 0;

@@ -1,0 +1,66 @@
+"""The C ABI: libsod.so loads without a GPU and exports exactly what include/sod.h
+declares; the ctypes signature table mirrors the header.  No compute calls (CPU only)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+from sift_based_od_amd import _lib
+
+HEADER = os.path.join(REPO, "include", "sod.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sod_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_parses():
+    names = declared()
+    assert "sod_create" in names and "sod_pipeline_enqueue" in names
+    assert len(names) >= 25
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()                      # loads libamdhip64 / librccl, no device needed
+    for n in declared():
+        assert hasattr(L, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = sorted(set(re.findall(r" T (sod_[a-z0-9_]+)", out)))
+    assert exported == declared()
+
+
+def test_ctypes_table_mirrors_header():
+    assert sorted(_lib.SIGNATURES) == declared()
+
+
+def test_abi_version_without_gpu():
+    assert _lib.lib().sod_abi_version() == 1
+
+
+def test_pipeline_args_layout():
+    # sod_pipeline_args in sod.h: double, 2 x i32, i32[4], 2 x i32, 2 x double, i32
+    a = _lib.PipelineArgs
+    assert a.ratio.offset == 0
+    assert a.query_h.offset == 8 and a.bins.offset == 16
+    assert a.vote_threshold.offset == 32 and a.x_factor.offset == 40
+    assert a.run_affine.offset == 56 and ctypes.sizeof(a) == 64
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libsod.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.lib()
+
+
+def test_bins4():
+    assert _lib.bins4(15) == (15, 15, 15, 15)
+    assert _lib.bins4((32, 32, 8, 12)) == (32, 32, 8, 12)
+    with pytest.raises(ValueError):
+        _lib.bins4((1, 2, 3))
