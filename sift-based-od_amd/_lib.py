@@ -11,7 +11,9 @@ import threading
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsod.so")
+# SOD_LIB_PATH: load an alternative build (A/B experiments of kernel variants only)
+LIB_PATH = os.environ.get("SOD_LIB_PATH") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libsod.so")
 
 SOD_OK, SOD_EINVAL, SOD_EHIP, SOD_ENOMEM, SOD_ESTATE, SOD_ECOMM = range(6)
 DTYPE_U8, DTYPE_F32 = 0, 1

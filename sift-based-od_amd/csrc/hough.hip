@@ -323,12 +323,15 @@ __global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __
   }
 }
 
-// one wave per valid bin: members = matches voting for it, in query order
+// one wave per valid bin: members = matches voting for it, in query order.  Each pass
+// covers 256 queries (4 loads per lane in flight) from the bin's first touch until all
+// of its votes are found.
 __global__ __launch_bounds__(256) void members_kernel(
     int64_t nq, const uint32_t* __restrict__ scal, const uint32_t* __restrict__ vbin,
     const int64_t* __restrict__ voff, const uint32_t* __restrict__ gcount,
     const uint32_t* __restrict__ gfirst, const uint32_t* __restrict__ basekey,
     const uint32_t* __restrict__ vmask, Bins b, int32_t* __restrict__ members) {
+  constexpr int U = 4;
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t V = scal[0];
@@ -339,25 +342,30 @@ __global__ __launch_bounds__(256) void members_kernel(
     const uint32_t need = gcount[lb];
     const int64_t off = voff[v];
     uint32_t got = 0;
-    for (int64_t q0 = gfirst[lb] >> 4; got < need && q0 < nq; q0 += 64) {
-      const int64_t q = q0 + lane;
-      bool mem = false;
-      if (q < nq) {
-        const uint32_t m = vmask[q] & 0xFFFFu;
-        if (m) {
-          const uint32_t key = basekey[q];
-          const int dx = bx_ - (int)(key & 0xFF), dy = by_ - (int)((key >> 8) & 0xFF),
-                    dt = bt_ - (int)((key >> 16) & 0xFF), ds = bs_ - (int)(key >> 24);
+    for (int64_t q0 = gfirst[lb] >> 4; got < need && q0 < nq; q0 += 64 * U) {
+      uint32_t m[U], key[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = q0 + u * 64 + lane;
+        m[u] = q < nq ? (vmask[q] & 0xFFFFu) : 0u;
+        key[u] = q < nq ? basekey[q] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        bool mem = false;
+        if (m[u]) {
+          const int dx = bx_ - (int)(key[u] & 0xFF), dy = by_ - (int)((key[u] >> 8) & 0xFF),
+                    dt = bt_ - (int)((key[u] >> 16) & 0xFF), ds = bs_ - (int)(key[u] >> 24);
           if ((unsigned)dx <= 1u && (unsigned)dy <= 1u && (unsigned)dt <= 1u && (unsigned)ds <= 1u)
-            mem = (m >> (dx * 8 + dy * 4 + dt * 2 + ds)) & 1u;
+            mem = (m[u] >> (dx * 8 + dy * 4 + dt * 2 + ds)) & 1u;
         }
+        const uint64_t bal = __ballot(mem);
+        if (mem) {
+          const uint32_t pos = __popcll(bal & ((1ull << lane) - 1ull));
+          members[off + got + pos] = (int32_t)(q0 + u * 64 + lane);
+        }
+        got += __popcll(bal);
       }
-      const uint64_t bal = __ballot(mem);
-      if (mem) {
-        const uint32_t pos = __popcll(bal & ((1ull << lane) - 1ull));
-        members[off + got + pos] = (int32_t)q;
-      }
-      got += __popcll(bal);
     }
   }
 }
@@ -399,9 +407,21 @@ __global__ void means_kernel(const uint32_t* __restrict__ scal, const int64_t* _
     const int64_t a = voff[v], e = voff[v + 1];
     const double* x = mq + k * mstride;
     double m = x[a];                       // first vote: mean = pose / model size
-    for (int64_t j = a + 1; j < e; ++j) {
+    int64_t j = a + 1;
+    // loads of a batch are independent of the recurrence: issue them together
+    for (; j + 8 <= e; j += 8) {
+      double b[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = x[j + i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const double n = (double)(j + i - a);
+        m = (m * n + b[i]) / (n + 1.0);    // n + 1 is an exact small integer
+      }
+    }
+    for (; j < e; ++j) {
       const double n = (double)(j - a);
-      m = (m * n + x[j]) / (n + 1.0);      // n + 1 is an exact small integer
+      m = (m * n + x[j]) / (n + 1.0);
     }
     means[6 * v + k] = m;
   }

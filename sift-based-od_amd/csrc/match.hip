@@ -21,9 +21,9 @@
 // lane can improve does the exact top-2 update run (rare after the first few thousand rows).
 //
 // Decomposition.  A workgroup = NW waves x QT query tiles (512 queries) kept in VGPRs for
-// the whole launch; it streams one DB split through a 3-slot LDS ring filled by LDS-DMA
-// (global_load_lds, two stages in flight, counted vmcnt + raw s_barrier, one barrier per
-// 64-row stage).  Per 16-row subtile a wave issues 32 MFMAs into 8 independent
+// the whole launch; it streams one DB split through a 2-slot LDS ring filled by LDS-DMA
+// (global_load_lds, the next stage in flight, vmcnt + raw s_barrier, one barrier per
+// 128-row stage).  Per 16-row subtile a wave issues 32 MFMAs into 8 independent
 // accumulators, then one compare pass and ONE wave-uniform branch.  Grid = query blocks x DB splits, sized to fill every CU twice;
 // per-split partial top-2 are merged by merge_kernel (also used for the multi-GPU merge).
 #include "sod_internal.h"
@@ -31,11 +31,15 @@
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
+#ifndef SOD_MATCH_PREFETCH
+#define SOD_MATCH_PREFETCH 1   // read the next subtile's fragments during this one's MFMAs
+#endif
+
 namespace {
 
 constexpr int QT = 8;    // 16-query tiles per wave
 constexpr int NW = 4;    // waves per workgroup
-constexpr int SPS = 4;   // 16-row subtiles per LDS stage (64 rows = 16 KiB)
+constexpr int SPS = 8;   // 16-row subtiles per LDS stage (128 rows = 32 KiB)
 constexpr int NT = NW * 64;
 constexpr int kStageBytes = SPS * kSubBytes;
 constexpr int kStageNorm = SPS * kSubRows * 4;
@@ -119,27 +123,43 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* lds_base) {
   __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_base, 16, 0, 0);
 }
 
-// LDS-DMA ring: stage s lives in buffer s % kRing.  Every wave issues kGldsPerStage
-// wave-instructions per stage (4 x 1 KiB of fragments + 1 x 64 B of row norms), so a
-// counted vmcnt says exactly which stage has landed (MI355X: vmcnt counts LDS-DMA in order).
-constexpr int kRing = 3;
-constexpr int kStageSlot = kStageBytes + kStageNorm;   // 16640 B, a multiple of 16
-constexpr int kGldsPerStage = kStageBytes / 1024 / NW + 1;
+// LDS-DMA ring: stage s lives in buffer s % 2.  The loads of stage s+1 are issued right
+// after the barrier that opens stage s (which guarantees every wave finished reading stage
+// s-1 from that buffer) and have the whole stage's MFMA work to land.
+constexpr int kRing = 2;
+constexpr int kStageSlot = kStageBytes + kStageNorm;   // 33280 B, a multiple of 16
+constexpr int kPiecesPerWave = kStageBytes / 1024 / NW;
+constexpr int kNormLanes = kStageNorm / 16 / NW;        // 16-B norm pieces per wave
 static_assert(kStageBytes / 1024 % NW == 0, "fragment pieces split evenly over waves");
-static_assert(kGldsPerStage == 5, "vmcnt immediates below assume 5 LDS-DMA per stage");
+static_assert(kStageNorm % (16 * NW) == 0 && kNormLanes <= 64, "norm pieces split over waves");
 
 __device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
                                             const float* __restrict__ dn, int64_t sub0,
                                             uint8_t* slot, int wave, int lane) {
   const uint8_t* src = dbpack + sub0 * kSubBytes;
 #pragma unroll
-  for (int j = 0; j < kStageBytes / 1024 / NW; ++j) {
-    const int piece = wave * (kStageBytes / 1024 / NW) + j;
+  for (int j = 0; j < kPiecesPerWave; ++j) {
+    const int piece = wave * kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  // row norms: 64 rows x 4 B = 256 B, 64 B (4 lanes) per wave
-  const float* nsrc = dn + sub0 * kSubRows + wave * 16 + lane * 4;
-  if (lane < 4) glds16(nsrc, slot + kStageBytes + wave * 64);
+  const float* nsrc = dn + sub0 * kSubRows + wave * (kNormLanes * 4) + lane * 4;
+  if (lane < kNormLanes) glds16(nsrc, slot + kStageBytes + wave * (kNormLanes * 16));
+}
+
+struct Frag {
+  bf16x8 a0, a1, a2, a3;
+  f32x4 cn;
+};
+
+__device__ __forceinline__ Frag read_frag(const uint8_t* sb, int u, int lane) {
+  const uint8_t* base = sb + u * kSubBytes + lane * 16;
+  Frag f;
+  f.a0 = *reinterpret_cast<const bf16x8*>(base);
+  f.a1 = *reinterpret_cast<const bf16x8*>(base + 1024);
+  f.a2 = *reinterpret_cast<const bf16x8*>(base + 2048);
+  f.a3 = *reinterpret_cast<const bf16x8*>(base + 3072);
+  f.cn = *reinterpret_cast<const f32x4*>(sb + kStageBytes + u * 64 + (lane >> 4) * 16);
+  return f;
 }
 
 __global__ __launch_bounds__(NT, 2) void match_kernel(
@@ -161,9 +181,7 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / SPS;  // nsub and sub_per_split are multiples of SPS
 
-  // prologue: two stages in flight before the queries are even loaded
   if (nst > 0) issue_stage(dbpack, dn, s_lo, lds, wave, lane);
-  if (nst > 1) issue_stage(dbpack, dn, s_lo + SPS, lds + kStageSlot, wave, lane);
 
   // queries: B fragments stay in registers for the whole launch
   bf16x8 bq[QT][4];
@@ -187,56 +205,61 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
     id[t] = 0x7fffffff;
   }
 
-  int slot_r = 0;            // buffer of stage s
-  int slot_w = 2;            // buffer of stage s + 2
   for (int64_t s = 0; s < nst; ++s) {
-    // stage s has landed for this wave once at most one younger stage is outstanding
-    if (s + 1 < nst)
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // ... and for every wave; also: stage s-1 fully read
-    if (s + 2 < nst) issue_stage(dbpack, dn, s_lo + (s + 2) * SPS, lds + slot_w * kStageSlot, wave, lane);
-    const uint8_t* sb = lds + slot_r * kStageSlot;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's part of stage s landed
+    __builtin_amdgcn_s_barrier();                       // every wave's; stage s-1 fully read
+    uint8_t* nxt = lds + ((s + 1) & 1) * kStageSlot;
+    if (s + 1 < nst) issue_stage(dbpack, dn, s_lo + (s + 1) * SPS, nxt, wave, lane);
+    const uint8_t* sb = lds + (s & 1) * kStageSlot;
+#if SOD_MATCH_PREFETCH
+    Frag f = read_frag(sb, 0, lane);
+#endif
 #pragma unroll
     for (int u = 0; u < SPS; ++u) {
-      const uint8_t* base = sb + u * kSubBytes + lane * 16;
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(base);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(base + 1024);
-      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(base + 2048);
-      const bf16x8 a3 = *reinterpret_cast<const bf16x8*>(base + 3072);
-      const f32x4 cn = *reinterpret_cast<const f32x4*>(sb + kStageBytes + u * 64 + (lane >> 4) * 16);
+#if SOD_MATCH_PREFETCH
+      const Frag c = f;
+#else
+      const Frag c = read_frag(sb, u, lane);
+#endif
       f32x4 acc[QT];
 #pragma unroll
-      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[t][0], cn, 0, 0, 0);
+      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.a0, bq[t][0], c.cn, 0, 0, 0);
 #pragma unroll
-      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bq[t][1], acc[t], 0, 0, 0);
+      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.a1, bq[t][1], acc[t], 0, 0, 0);
+      // next subtile's fragments in flight once a0/a1/cn are dead (keeps VGPRs < 256)
+#if SOD_MATCH_PREFETCH
+      if (u + 1 < SPS) f = read_frag(sb, u + 1, lane);
+#endif
 #pragma unroll
-      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bq[t][2], acc[t], 0, 0, 0);
+      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.a2, bq[t][2], acc[t], 0, 0, 0);
 #pragma unroll
-      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, bq[t][3], acc[t], 0, 0, 0);
-      // prefilter: can any of this lane's 4 x QT candidates beat a running 2nd best?
-      bool hit = false;
+      for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.a3, bq[t][3], acc[t], 0, 0, 0);
+      // prefilter: can any of this lane's 4 x QT candidates beat its running 2nd best?
+      bool hit[QT];
+      bool any = false;
 #pragma unroll
-      for (int t = 0; t < QT; ++t)
-        hit |= (acc[t][0] < v2[t]) | (acc[t][1] < v2[t]) | (acc[t][2] < v2[t]) | (acc[t][3] < v2[t]);
-      if (__any(hit)) {
+      for (int t = 0; t < QT; ++t) {
+        const float m = fminf(fminf(acc[t][0], acc[t][1]), acc[t][2]);
+        hit[t] = (m < v2[t]) | (acc[t][3] < v2[t]);
+        any |= hit[t];
+      }
+      if (__any(any)) {
         const int rowb = row_offset + (int)((s_lo + s * SPS + u) * kSubRows) + (lane >> 4) * 4;
 #pragma unroll
         for (int t = 0; t < QT; ++t) {
+          if (__any(hit[t])) {       // exact top-2 update, only for tiles that can change
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float x = acc[t][r];
-            const bool lt = x < v1[t];
-            v2[t] = __builtin_amdgcn_fmed3f(v1[t], v2[t], x);
-            id[t] = lt ? rowb + r : id[t];
-            v1[t] = lt ? x : v1[t];
+            for (int r = 0; r < 4; ++r) {
+              const float x = acc[t][r];
+              const bool lt = x < v1[t];
+              v2[t] = __builtin_amdgcn_fmed3f(v1[t], v2[t], x);
+              id[t] = lt ? rowb + r : id[t];
+              v1[t] = lt ? x : v1[t];
+            }
           }
         }
       }
     }
-    slot_r = slot_r == kRing - 1 ? 0 : slot_r + 1;
-    slot_w = slot_w == kRing - 1 ? 0 : slot_w + 1;
   }
 
   // merge the 4 row groups of each query (lanes l, l^16, l^32, l^48)
