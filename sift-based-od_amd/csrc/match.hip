@@ -75,7 +75,9 @@ __global__ void pack_rows_kernel(const TIn* __restrict__ src, int64_t n, int64_t
       v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const bool ok = (v[j] >= 0.f) && (v[j] <= 255.f) && (v[j] == truncf(v[j]));
+        // this file is compiled with -fno-honor-nans: reject NaN/Inf on the bit pattern
+        const bool finite = (__float_as_uint(v[j]) & 0x7f800000u) != 0x7f800000u;
+        const bool ok = finite && (v[j] >= 0.f) && (v[j] <= 255.f) && (v[j] == truncf(v[j]));
         bad |= ok ? 0u : 1u;
         if (!ok) v[j] = 0.f;
       }
