@@ -139,15 +139,31 @@ int sod_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
                    const float* qy, const float* qangle, const int32_t* qoctave,
                    const double* cx, const double* cy, int32_t query_h, int32_t query_w,
                    const int32_t bins[4], double* pose, int32_t* idx);
+/* calculate_bin_index for n given poses (x, y, alpha, scale_factor): idx[n*4]. */
+int sod_bin_index_batch(sod_ctx* ctx, int64_t n, const double* pose, int32_t query_h,
+                        int32_t query_w, const int32_t bins[4], int32_t* idx);
 /* AffineParameters + remove_outliers fixed point for host-provided bins (CSR):
  * model/query points per member (f32, as cv2.KeyPoint.pt), i_sigma = pose[3] per bin.
- * max_iter = 1 runs exactly one {AffineParameters; remove_outliers} round. */
+ * max_iter = 0: AffineParameters only (params, nothing removed);
+ * max_iter = 1: one {AffineParameters; remove_outliers} round;
+ * params_in != NULL (with max_iter = 1): remove_outliers with the given params
+ * (posebin.affine_parameters) instead of solving. */
 int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets,
                      const float* mx, const float* my, const float* qx, const float* qy,
                      const int32_t* i_sigma, int32_t query_w, int32_t query_h,
                      double x_factor, double y_factor, int32_t threshold, int32_t max_iter,
-                     uint8_t* survived, int32_t* votes, double* params,
-                     uint8_t* member_alive);
+                     const double* params_in, uint8_t* survived, int32_t* votes,
+                     double* params, uint8_t* member_alive);
+
+/* ---- host-side exchange (multi-rank over a host communicator, e.g. gloo) ------------
+ * The same two exchange steps as the RCCL path, with the data staged through the host:
+ * candidates_get -> all-gather -> candidates_merge; partial_get -> all-reduce ->
+ * partial_set.  Used when no RCCL communicator is available (and by the tests). */
+int sod_match_candidates_get(sod_ctx* ctx, float* d1sq, int32_t* idx, float* d2sq);
+int sod_match_candidates_merge(sod_ctx* ctx, int32_t nparts, const float* d1sq,
+                               const int32_t* idx, const float* d2sq);
+int sod_hough_partial_get(sod_ctx* ctx, uint32_t* counts, uint32_t* first);
+int sod_hough_partial_set(sod_ctx* ctx, const uint32_t* counts, const uint32_t* first);
 
 /* ---- multi-GPU (RCCL over xGMI) --------------------------------------------------- */
 int sod_comm_unique_id(uint8_t out[SOD_UNIQUE_ID_BYTES]);

@@ -21,5 +21,21 @@ The native library is loaded lazily on first use and its absence is an error
 (there is no CPU fallback anywhere in this package).
 """
 from .database import Keypoints, SiftDatabase, centroid_of  # noqa: F401
+from .sift_helpers import (KeyPoint, get_centroid, make_kp, make_temp_kp,  # noqa: F401
+                           unpack_sift_octave)
+from .posebin import PoseBin  # noqa: F401
+from .matcher import BFMatcher, DMatch, knn2, ratio_match  # noqa: F401
+from .hough import (calculate_bin_index, calculate_bin_index_batch,  # noqa: F401
+                    estimate_object_pose, estimate_object_pose_batch, perform_hough_transform)
+from .affine import (AffineParameters, Calc_x, Ext_Params, Gen_A, Gen_b,  # noqa: F401
+                     remove_outliers, verify_bins)
+from .pipeline import Main  # noqa: F401
+from .sharded import HostComm, RcclComm, TorchHostComm, run_sharded, shard_range  # noqa: F401
 
-__all__ = ["Keypoints", "SiftDatabase", "centroid_of"]
+__all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid", "make_kp",
+           "make_temp_kp", "unpack_sift_octave", "PoseBin", "BFMatcher", "DMatch", "knn2",
+           "ratio_match", "calculate_bin_index", "calculate_bin_index_batch",
+           "estimate_object_pose", "estimate_object_pose_batch", "perform_hough_transform",
+           "AffineParameters", "Calc_x", "Ext_Params", "Gen_A", "Gen_b", "remove_outliers",
+           "verify_bins", "Main", "HostComm", "RcclComm", "TorchHostComm", "run_sharded",
+           "shard_range"]

@@ -72,9 +72,15 @@ SIGNATURES = {
     "sod_pose_batch": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_f32p, c_f32p,
                                  c_f32p, c_i32p, c_f64p, c_f64p, C.c_int32, C.c_int32, c_i32p,
                                  c_f64p, c_i32p]),
+    "sod_bin_index_batch": (C.c_int, [c_ctx, C.c_int64, c_f64p, C.c_int32, C.c_int32, c_i32p,
+                                      c_i32p]),
     "sod_affine_batch": (C.c_int, [c_ctx, C.c_int64, c_i64p, c_f32p, c_f32p, c_f32p, c_f32p,
                                    c_i32p, C.c_int32, C.c_int32, C.c_double, C.c_double,
-                                   C.c_int32, C.c_int32, c_u8p, c_i32p, c_f64p, c_u8p]),
+                                   C.c_int32, C.c_int32, c_f64p, c_u8p, c_i32p, c_f64p, c_u8p]),
+    "sod_match_candidates_get": (C.c_int, [c_ctx, c_f32p, c_i32p, c_f32p]),
+    "sod_match_candidates_merge": (C.c_int, [c_ctx, C.c_int32, c_f32p, c_i32p, c_f32p]),
+    "sod_hough_partial_get": (C.c_int, [c_ctx, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "sod_hough_partial_set": (C.c_int, [c_ctx, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "sod_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
     "sod_comm_init": (C.c_int, [c_ctx, C.c_int32, C.c_int32, C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
 }
@@ -340,8 +346,47 @@ class Context:
                                          ptr(idx, C.c_int32)))
         return pose, idx
 
+    def bin_index_batch(self, pose, query_shape, bins):
+        p = _c(pose, np.float64).reshape(-1, 4)
+        b = np.ascontiguousarray(bins4(bins), np.int32)
+        idx = np.empty((len(p), 4), np.int32)
+        self._chk(self._L.sod_bin_index_batch(self._h, len(p), ptr(p, C.c_double),
+                                              int(query_shape[0]), int(query_shape[1]),
+                                              ptr(b, C.c_int32), ptr(idx, C.c_int32)))
+        return idx
+
+    # -- host-side exchange (multi-rank without RCCL) --
+    def candidates(self):
+        n = self.nq
+        d1 = np.empty(n, np.float32)
+        idx = np.empty(n, np.int32)
+        d2 = np.empty(n, np.float32)
+        self._chk(self._L.sod_match_candidates_get(self._h, ptr(d1, C.c_float),
+                                                   ptr(idx, C.c_int32), ptr(d2, C.c_float)))
+        return d1, idx, d2
+
+    def merge_candidates(self, d1, idx, d2):
+        d1 = _c(d1, np.float32)
+        idx = _c(idx, np.int32)
+        d2 = _c(d2, np.float32)
+        nparts = d1.size // self.nq
+        self._chk(self._L.sod_match_candidates_merge(self._h, nparts, ptr(d1, C.c_float),
+                                                     ptr(idx, C.c_int32), ptr(d2, C.c_float)))
+
+    def hough_partial(self):
+        n = int(np.prod(self.bins))
+        cnt = np.empty(n, np.uint32)
+        fst = np.empty(n, np.uint32)
+        self._chk(self._L.sod_hough_partial_get(self._h, ptr(cnt, C.c_uint32), ptr(fst, C.c_uint32)))
+        return cnt, fst
+
+    def set_hough_partial(self, counts, first):
+        cnt = _c(counts, np.uint32)
+        fst = _c(first, np.uint32)
+        self._chk(self._L.sod_hough_partial_set(self._h, ptr(cnt, C.c_uint32), ptr(fst, C.c_uint32)))
+
     def affine_batch(self, offsets, mx, my, qx, qy, i_sigma, query_size, x_factor=128.0,
-                     y_factor=128.0, threshold=4, max_iter=1 << 30):
+                     y_factor=128.0, threshold=4, max_iter=1 << 30, params_in=None):
         off = _c(offsets, np.int64)
         nb = len(off) - 1
         pts = [_c(v, np.float32) for v in (mx, my, qx, qy)]
@@ -351,10 +396,12 @@ class Context:
         votes = np.empty(nb, np.int32)
         params = np.empty((nb, 6), np.float64)
         alive = np.empty(M, np.uint8)
+        pin = None if params_in is None else _c(params_in, np.float64).reshape(-1)
         self._chk(self._L.sod_affine_batch(
             self._h, nb, ptr(off, C.c_int64), *[ptr(p, C.c_float) for p in pts],
             ptr(isg, C.c_int32), int(query_size[0]), int(query_size[1]), float(x_factor),
-            float(y_factor), int(threshold), int(max_iter), ptr(surv, C.c_uint8),
+            float(y_factor), int(threshold), int(max_iter), ptr(pin, C.c_double),
+            ptr(surv, C.c_uint8),
             ptr(votes, C.c_int32), ptr(params, C.c_double), ptr(alive, C.c_uint8)))
         return {"survived": surv.astype(bool), "votes": votes, "params": params,
                 "alive": alive.astype(bool)}

@@ -237,8 +237,6 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq, const
 int sod_match_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
-  if (ctx->nranks == 1 && ctx->n_shard < 2)
-    return sod_fail(ctx, SOD_EINVAL, "knnMatch(k=2) needs at least 2 train descriptors");
   SOD_TRY(launch_match(ctx));
   ctx->matched = true;
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
@@ -445,7 +443,8 @@ int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_
   SOD_TRY(sod_reserve(ctx, ctx->alive, (size_t)ctx->mmax));
   SOD_TRY(launch_affine(ctx, 0, true, ctx->voff.p, ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p,
                         ctx->aisig.p, query_w, query_h, x_factor, y_factor, threshold, 1 << 30,
-                        ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p, ctx->scal.p));
+                        nullptr, ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p,
+                        ctx->scal.p));
   SOD_HIP(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
   ctx->affined = true;
   return SOD_OK;
@@ -525,11 +524,13 @@ int sod_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my, co
 int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets, const float* mx,
                      const float* my, const float* qx, const float* qy, const int32_t* i_sigma,
                      int32_t query_w, int32_t query_h, double x_factor, double y_factor,
-                     int32_t threshold, int32_t max_iter, uint8_t* survived, int32_t* votes,
-                     double* params, uint8_t* member_alive) {
+                     int32_t threshold, int32_t max_iter, const double* params_in,
+                     uint8_t* survived, int32_t* votes, double* params, uint8_t* member_alive) {
   SOD_TRY(set_dev(ctx));
-  if (n_bins < 0 || !offsets || max_iter < 1 || !(x_factor != 0.0) || !(y_factor != 0.0))
+  if (n_bins < 0 || !offsets || max_iter < 0 || !(x_factor != 0.0) || !(y_factor != 0.0))
     return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  if (params_in && max_iter != 1)
+    return sod_fail(ctx, SOD_EINVAL, "params_in requires max_iter = 1");
   if (n_bins == 0) return SOD_OK;
   const int64_t M = offsets[n_bins];
   for (int64_t i = 0; i < n_bins; ++i)
@@ -538,8 +539,9 @@ int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets, const
   DevBuf<float> p[4];
   DevBuf<int32_t> is, vo;
   DevBuf<uint8_t> sv, al;
-  DevBuf<double> pr;
+  DevBuf<double> pr, pin;
   int rc = upload(ctx, off, offsets, (size_t)n_bins + 1);
+  if (rc == SOD_OK && params_in) rc = upload(ctx, pin, params_in, (size_t)n_bins * 6);
   const float* ps[4] = {mx, my, qx, qy};
   for (int i = 0; i < 4 && rc == SOD_OK; ++i) rc = upload(ctx, p[i], ps[i], (size_t)M);
   if (rc == SOD_OK) rc = upload(ctx, is, i_sigma, (size_t)n_bins);
@@ -549,8 +551,8 @@ int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets, const
   if (rc == SOD_OK) rc = sod_reserve(ctx, pr, (size_t)n_bins * 6);
   if (rc == SOD_OK)
     rc = launch_affine(ctx, n_bins, false, off.p, p[0].p, p[1].p, p[2].p, p[3].p, is.p, query_w,
-                       query_h, x_factor, y_factor, threshold, max_iter, sv.p, vo.p, pr.p, al.p,
-                       nullptr);
+                       query_h, x_factor, y_factor, threshold, max_iter,
+                       params_in ? pin.p : nullptr, sv.p, vo.p, pr.p, al.p, nullptr);
   if (rc == SOD_OK) rc = download(ctx, survived, sv.p, (size_t)n_bins);
   if (rc == SOD_OK) rc = download(ctx, votes, vo.p, (size_t)n_bins);
   if (rc == SOD_OK) rc = download(ctx, params, pr.p, (size_t)n_bins * 6);
@@ -561,7 +563,78 @@ int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets, const
   sod_release(off);
   for (auto& b : p) sod_release(b);
   sod_release(is); sod_release(vo); sod_release(sv); sod_release(al); sod_release(pr);
+  sod_release(pin);
   return rc;
+}
+
+int sod_bin_index_batch(sod_ctx* ctx, int64_t n, const double* pose, int32_t query_h,
+                        int32_t query_w, const int32_t bins[4], int32_t* idx) {
+  SOD_TRY(set_dev(ctx));
+  if (n < 0 || query_h < 1 || query_w < 1 || (n && (!pose || !idx)))
+    return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  if (n == 0) return SOD_OK;
+  SOD_TRY(check_bins(ctx, bins));
+  ctx->qh = query_h;
+  ctx->qw = query_w;
+  DevBuf<double> dp;
+  DevBuf<int32_t> di;
+  int rc = upload(ctx, dp, pose, (size_t)n * 4);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, di, (size_t)n * 4);
+  if (rc == SOD_OK) rc = launch_bin_index_batch(ctx, n, dp.p, di.p);
+  if (rc == SOD_OK) rc = download(ctx, idx, di.p, (size_t)n * 4);
+  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "bin index batch failed");
+  (void)hipStreamSynchronize(ctx->stream);
+  sod_release(dp);
+  sod_release(di);
+  return rc;
+}
+
+// ---- host-side exchange ---------------------------------------------------------------
+int sod_match_candidates_get(sod_ctx* ctx, float* d1sq, int32_t* idx, float* d2sq) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
+  const size_t n = (size_t)ctx->nq;
+  SOD_TRY(download(ctx, d1sq, ctx->cd1.p, n));
+  SOD_TRY(download(ctx, idx, ctx->cidx.p, n));
+  SOD_TRY(download(ctx, d2sq, ctx->cd2.p, n));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return SOD_OK;
+}
+
+int sod_match_candidates_merge(sod_ctx* ctx, int32_t nparts, const float* d1sq,
+                               const int32_t* idx, const float* d2sq) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
+  if (nparts < 1 || !d1sq || !idx || !d2sq) return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  const size_t n = (size_t)ctx->nq, tot = n * (size_t)nparts;
+  SOD_TRY(upload(ctx, ctx->gd1, d1sq, tot));
+  SOD_TRY(upload(ctx, ctx->gidx, idx, tot));
+  SOD_TRY(upload(ctx, ctx->gd2, d2sq, tot));
+  SOD_TRY(launch_merge(ctx, ctx->gd1.p, ctx->gidx.p, ctx->gd2.p, nparts, (int64_t)n));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_hough_partial_get(sod_ctx* ctx, uint32_t* counts, uint32_t* first) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  SOD_TRY(download(ctx, counts, ctx->counts.p, (size_t)ctx->nbins));
+  SOD_TRY(download(ctx, first, ctx->first.p, (size_t)ctx->nbins));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return SOD_OK;
+}
+
+int sod_hough_partial_set(sod_ctx* ctx, const uint32_t* counts, const uint32_t* first) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  if (!counts || !first) return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->counts.p, counts, ctx->nbins * 4, hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->first.p, first, ctx->nbins * 4, hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->selected = ctx->affined = false;
+  return SOD_OK;
 }
 
 // ---- RCCL -----------------------------------------------------------------------------

@@ -48,6 +48,15 @@ __device__ __forceinline__ int xy_index(double v, int b) {
   return (int)i;
 }
 
+// calculate_bin_index (HTHF:39-72) of a pose (x, y, alpha, scale_factor = 2^k)
+__device__ __forceinline__ void bin_index(double x, double y, double a, int k, int H, int W,
+                                          Bins b, const int* __restrict__ lut, int idx[4]) {
+  idx[0] = xy_index((x * b.x) / W, b.x);
+  idx[1] = xy_index((y * b.y) / H, b.y);
+  idx[2] = (int)fmod((a * b.t) / kTwoPi, (double)b.t);
+  idx[3] = lut[k + kSigmaLutHalf];
+}
+
 // estimate_object_pose (HTHF:4-37) + calculate_bin_index (HTHF:39-72)
 __device__ __forceinline__ void pose_bins(float mx, float my, float ma, int mo, float qx, float qy,
                                           float qa, int qo, double cx, double cy, int H, int W,
@@ -66,10 +75,20 @@ __device__ __forceinline__ void pose_bins(float mx, float my, float ma, int mo, 
   pose[1] = y;
   pose[2] = a;
   pose[3] = s;
-  idx[0] = xy_index((x * b.x) / W, b.x);
-  idx[1] = xy_index((y * b.y) / H, b.y);
-  idx[2] = (int)fmod((a * b.t) / kTwoPi, (double)b.t);
-  idx[3] = lut[k + kSigmaLutHalf];
+  bin_index(x, y, a, k, H, W, b, lut, idx);
+}
+
+// scale_factor -> k with s == 2^k exactly (estimate_object_pose only produces powers of 2);
+// any other scale takes the generic path of HTHF:67 (log2 via libm-equivalent ocml log).
+__device__ __forceinline__ int sigma_from_scale(double s, Bins b, const int* lut, bool* generic) {
+  int e;
+  const double m = frexp(s, &e);          // s = m * 2^e, m in [0.5, 1)
+  if (m == 0.5 && e - 1 >= -kSigmaLutHalf && e - 1 <= kSigmaLutHalf) {
+    *generic = false;
+    return e - 1;
+  }
+  *generic = true;
+  return 0;
 }
 
 __device__ __forceinline__ uint32_t lin_bin(int ix, int iy, int it, int is, Bins b) {
@@ -134,6 +153,24 @@ __global__ void pose_batch_kernel(int64_t n, const float* __restrict__ mx,
     pose[4 * i + j] = p[j];
     idx[4 * i + j] = ix[j];
   }
+}
+
+__global__ void bin_index_batch_kernel(int64_t n, const double* __restrict__ pose, int H, int W,
+                                       Bins b, const int* __restrict__ lut, int* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* p = pose + 4 * i;
+  bool generic;
+  const int k = sigma_from_scale(p[3], b, lut, &generic);
+  int ix[4];
+  bin_index(p[0], p[1], p[2], k, H, W, b, lut, ix);
+  if (generic) {  // HTHF:67 for a scale that is not a power of two
+    const double v = (log(p[3]) / log(2.0)) / 6.5 * (double)b.s;
+    long long i3 = !(v == v) ? 0 : (v > 1e9 ? 1000000000LL : (v < -1e9 ? -1000000000LL : (long long)v));
+    ix[3] = (int)(i3 < 0 ? 0 : (i3 > b.s - 1 ? b.s - 1 : i3));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) idx[4 * i + j] = ix[j];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -508,8 +545,9 @@ __global__ __launch_bounds__(256) void affine_kernel(
     int64_t nb_host, const uint32_t* __restrict__ nb_dev, const int64_t* __restrict__ off,
     const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
     const float* __restrict__ qy, const int32_t* __restrict__ isig, int qw, int qh, double xf,
-    double yf, int thr, int max_iter, uint8_t* __restrict__ surv, int32_t* __restrict__ votes,
-    double* __restrict__ params, uint8_t* __restrict__ alive) {
+    double yf, int thr, int max_iter, const double* __restrict__ params_in,
+    uint8_t* __restrict__ surv, int32_t* __restrict__ votes, double* __restrict__ params,
+    uint8_t* __restrict__ alive) {
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t NB = nb_dev ? (int64_t)nb_dev[0] : nb_host;
@@ -522,7 +560,8 @@ __global__ __launch_bounds__(256) void affine_kernel(
     int64_t n = e - a;
     double prm[6] = {0, 0, 0, 0, 0, 0};
     bool ok = false;
-    for (int it = 0; it < max_iter; ++it) {
+    const int rounds = max_iter < 1 ? 1 : max_iter;   // max_iter 0: solve once, remove nothing
+    for (int it = 0; it < rounds; ++it) {
       double s[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       for (int64_t j = a + lane; j < e; j += 64) {
         if (!alive[j]) continue;
@@ -532,7 +571,10 @@ __global__ __launch_bounds__(256) void affine_kernel(
       }
 #pragma unroll
       for (int k = 0; k < 12; ++k) s[k] = wave_sum(s[k]);
-      if (n > 0) {  // AffineParameters.py:105: no-op for an empty bin
+      if (params_in) {  // remove_outliers with the caller's posebin.affine_parameters
+#pragma unroll
+        for (int k = 0; k < 6; ++k) prm[k] = params_in[6 * v + k];
+      } else if (n > 0) {  // AffineParameters.py:105: no-op for an empty bin
         const double g[3][3] = {{s[0], s[1], s[2]}, {s[1], s[3], s[4]}, {s[2], s[4], s[5]}};
         double p[3][3];
         pinv3_sym(g, p);
@@ -543,6 +585,10 @@ __global__ __launch_bounds__(256) void affine_kernel(
         prm[2] = p[0][0] * s[9] + p[0][1] * s[10] + p[0][2] * s[11];
         prm[3] = p[1][0] * s[9] + p[1][1] * s[10] + p[1][2] * s[11];
         prm[5] = p[2][0] * s[9] + p[2][1] * s[10] + p[2][2] * s[11];
+      }
+      if (max_iter < 1) {
+        ok = true;
+        break;
       }
       // remove_outliers, AffineParameters.py:134-159
       int dropped = 0;
@@ -608,6 +654,14 @@ int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
   hipLaunchKernelGGL(pose_batch_kernel, dim3((unsigned)cdiv(n, bs)), dim3(bs), 0, ctx->stream, n,
                      mx, my, ma, mo, qx, qy, qa, qo, cx, cy, ctx->qh, ctx->qw, ctx_bins(ctx),
                      ctx->sig_lut.p, pose, idx);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_bin_index_batch(sod_ctx* ctx, int64_t n, const double* pose, int32_t* idx) {
+  const int bs = 256;
+  hipLaunchKernelGGL(bin_index_batch_kernel, dim3((unsigned)cdiv(n, bs)), dim3(bs), 0, ctx->stream,
+                     n, pose, ctx->qh, ctx->qw, ctx_bins(ctx), ctx->sig_lut.p, idx);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
@@ -707,12 +761,12 @@ int launch_affine_gather(sod_ctx* ctx) {
 int launch_affine(sod_ctx* ctx, int64_t nb_host, bool count_on_device, const int64_t* offsets,
                   const float* mx, const float* my, const float* qx, const float* qy,
                   const int32_t* isig, int32_t qw, int32_t qh, double xf, double yf, int32_t thr,
-                  int32_t max_iter, uint8_t* surv, int32_t* votes, double* params, uint8_t* alive,
-                  const uint32_t* dev_count) {
+                  int32_t max_iter, const double* params_in, uint8_t* surv, int32_t* votes,
+                  double* params, uint8_t* alive, const uint32_t* dev_count) {
   const int wg = std::max(1, ctx->num_cus * 4);
   hipLaunchKernelGGL(affine_kernel, dim3(wg), dim3(256), 0, ctx->stream, nb_host,
                      count_on_device ? dev_count : nullptr, offsets, mx, my, qx, qy, isig, qw, qh,
-                     xf, yf, thr, max_iter, surv, votes, params, alive);
+                     xf, yf, thr, max_iter, params_in, surv, votes, params, alive);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }

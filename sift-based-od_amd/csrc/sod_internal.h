@@ -163,8 +163,10 @@ int launch_affine_gather(sod_ctx* ctx);
 int launch_affine(sod_ctx* ctx, int64_t nbins_dev_scalar_or_host, bool count_on_device,
                   const int64_t* offsets, const float* mx, const float* my, const float* qx,
                   const float* qy, const int32_t* isig, int32_t qw, int32_t qh, double xf,
-                  double yf, int32_t thr, int32_t max_iter, uint8_t* surv, int32_t* votes,
-                  double* params, uint8_t* alive, const uint32_t* dev_count);
+                  double yf, int32_t thr, int32_t max_iter, const double* params_in,
+                  uint8_t* surv, int32_t* votes, double* params, uint8_t* alive,
+                  const uint32_t* dev_count);
+int launch_bin_index_batch(sod_ctx* ctx, int64_t n, const double* pose, int32_t* idx);
 int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
                       const float* ma, const int32_t* mo, const float* qx, const float* qy,
                       const float* qa, const int32_t* qo, const double* cx, const double* cy,

@@ -1,0 +1,232 @@
+"""``Main`` -- the stage driver of ``main.py:17-188`` on the device.
+
+Same stage names, order and thresholds as the reference::
+
+    m = Main()
+    m.set_database(db)                                   # main.py:48-66 (pickle -> SoA)
+    m.get_query_features(des_query, kp_query, shape)     # main.py:36-45 (SIFT output given)
+    m.run_matcher()                                      # main.py:68-87
+    m.apply_hough_transform(15)                          # main.py:89-119
+    m.get_valid_bins(5)                                  # main.py:121-132
+    m.apply_affine_parameters(4)                         # main.py:139-157
+
+Every stage runs on the device and leaves its result there; the reference's Python
+objects (``matching_keypoints`` tuples, the ``hough_transform`` dict of PoseBins,
+``valid_bins``, ``keypoint_pairs``) are materialised lazily, only when read.  ``run()``
+enqueues the whole path on one stream (the bench path).  SIFT detection
+(``main.py:43``) and the post-processing / plotting stages are outside this path
+(SURVEY.md §8(f)).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .database import Keypoints, SiftDatabase
+from .hough import hough_table_from_tuples, posebins_from_device
+from .sift_helpers import keypoints_from_arrays
+
+POS_FACTOR = 32   # main.py:141
+
+
+class _Shape:
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+
+
+class Main:
+
+    def __init__(self, ctx=None, device=0):
+        self.ctx = ctx or _lib.Context(device)
+        self.db = None
+        self.kp = _LazyKeypoints(self, "db")
+        self.des = None
+        self.kp_query = _LazyKeypoints(self, "query")
+        self.des_query = None
+        self.rgb_query = None
+        self.image_query_size = (0, 0)
+        self._matching = None          # list of tuples once materialised / assigned
+        self._match = None             # (idx1, good) device results
+        self._hough_bins = None
+        self._table = None
+        self.valid_bins = []
+        self.keypoint_pairs = []
+        self.final_pose = []
+        self._stage = None
+
+    # ---------------------------------------------------------------- inputs
+    def set_database(self, db):
+        """The flattened training database (``main.py:53-66``): a :class:`SiftDatabase`
+        or the reference's pickle payload (list of per-image records)."""
+        if not isinstance(db, SiftDatabase):
+            db = SiftDatabase.from_records(db)
+        self.db = db
+        self.des = db.des
+        self.ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        self.ctx.upload_db(db.des)
+        self.kp = _LazyKeypoints(self, "db")
+
+    def get_query_features(self, des_query, kp_query, image_shape, database=None):
+        """``main.py:36-45`` with the SIFT output given: descriptors [Nq,128] and the
+        keypoints (a :class:`Keypoints` SoA or a list of cv2.KeyPoint);
+        ``image_shape`` = ``rgb_query.shape``."""
+        if database is not None:
+            self.set_database(database)
+        if not isinstance(kp_query, Keypoints):
+            kp_query = Keypoints.from_cv(kp_query)
+        self._qkp = kp_query
+        self.des_query = np.asarray(des_query)
+        self.rgb_query = _Shape(image_shape)
+        self.image_query_size = (int(image_shape[1]), int(image_shape[0]))   # (w, h)
+        self.kp_query = _LazyKeypoints(self, "query")
+        self.ctx.upload_queries(self.des_query, kp_query)
+        self._reset_after_match()
+
+    def _reset_after_match(self):
+        self._matching = None
+        self._match = None
+        self._table = None
+        self.valid_bins = []
+        self.keypoint_pairs = []
+
+    # ---------------------------------------------------------------- stages
+    def run_matcher(self, ratio=0.75):
+        """``main.py:68-87``: knnMatch(k=2) + ratio test, on the device."""
+        self.ctx.match()
+        self.ctx.ratio(ratio)
+        idx1, d1, d2, good = self.ctx.match_result()
+        self._match = (idx1, good)
+        self._matching = None
+        self._stage = "matched"
+
+    @property
+    def matching_keypoints(self):
+        """(kpM, kpQ, model_img_size, model_centroid) per good match in query order
+        (``main.py:85-86``).  Assigning a list makes the next stage use it instead."""
+        if self._matching is None:
+            if self._match is None:
+                self._matching = []
+            else:
+                idx1, good = self._match
+                self._matching = [self._tuple(int(q), int(idx1[q])) for q in np.nonzero(good)[0]]
+        return self._matching
+
+    @matching_keypoints.setter
+    def matching_keypoints(self, value):
+        self._matching = list(value)
+        self._match = None
+        self._stage = "assigned"
+
+    def _tuple(self, q, m):
+        im = int(self.db.img[m])
+        return (self.kp[m], self.kp_query[q], (int(self.db.size[im][0]), int(self.db.size[im][1])),
+                (float(self.db.centroid[im][0]), float(self.db.centroid[im][1])))
+
+    def apply_hough_transform(self, bins=15):
+        """``main.py:89-119`` with ``bins`` an int (reference) or per-axis 4-tuple."""
+        shape = self.rgb_query.shape
+        self._hough_bins = bins
+        self._table = None
+        if self._stage == "assigned":
+            # tuples set by the caller: vote over them as given
+            self._tuple_ctx, self._tuple_bins = hough_table_from_tuples(
+                self._matching, shape, bins, 1, _lib.Context(self.ctx.device))
+            self._table = {b.pose: b for b in self._tuple_bins}
+            return
+        self.ctx.hough(shape, bins)
+
+    @property
+    def hough_transform(self):
+        """The {pose: PoseBin} dict in insertion (first-touch) order."""
+        if self._table is None:
+            if self._hough_bins is None:
+                return {}
+            self.ctx.select(1)
+            res = self.ctx.valid_result()
+            self._table = {b.pose: b for b in posebins_from_device(res, self._pair, self._size_of)}
+            self._selected_thr = 1
+        return self._table
+
+    def _pair(self, q):
+        return (self.kp[int(self._match[0][q])], self.kp_query[q])
+
+    def _size_of(self, q):
+        m = int(self._match[0][q])
+        im = int(self.db.img[m])
+        return (int(self.db.size[im][0]), int(self.db.size[im][1]))
+
+    def get_valid_bins(self, threshold=5):
+        """``main.py:121-132``: bins with votes >= threshold, insertion order."""
+        self.keypoint_pairs = []
+        if self._stage == "assigned":
+            vb = [b for b in self._table.values() if b.votes >= threshold]
+        else:
+            self.ctx.select(threshold)
+            res = self.ctx.valid_result()
+            if self._table is not None:
+                vb = [self._table[tuple(int(v) for v in k)] for k in res["keys"]]
+            else:
+                vb = posebins_from_device(res, self._pair, self._size_of)
+        for b in vb:
+            self.keypoint_pairs.extend(b.keypoint_pairs)
+            if b not in self.valid_bins:
+                self.valid_bins.append(b)
+        self._valid_thr = threshold
+
+    def update_keypoint_pairs(self):
+        """``main.py:134-137``."""
+        self.keypoint_pairs.clear()
+        for posebin in self.valid_bins:
+            self.keypoint_pairs.extend(posebin.keypoint_pairs)
+
+    def apply_affine_parameters(self, threshold=4):
+        """``main.py:139-157``: per-bin fixed point of {AffineParameters;
+        remove_outliers} with factor pos_factor*4, on the device (all bins at once)."""
+        from .affine import verify_bins
+        self.valid_bins = verify_bins(self.valid_bins, self.image_query_size, threshold,
+                                      POS_FACTOR * 4, POS_FACTOR * 4, self.ctx)
+        self.update_keypoint_pairs()
+
+    def post_process(self):
+        raise NotImplementedError(
+            "post-processing (PostProcessing.py) is outside this build's hot path "
+            "(SURVEY.md §8(f), next row 1)")
+
+    # ---------------------------------------------------------------- fused
+    def run(self, bins=15, vote_threshold=5, affine_threshold=4, ratio=0.75, run_affine=True):
+        """The whole path on one stream, results left on the device; returns a dict of
+        arrays (matches, valid bins, members, means, affine survivors/params)."""
+        self.ctx.pipeline(self.rgb_query.shape, bins, ratio, vote_threshold, affine_threshold,
+                          POS_FACTOR * 4.0, POS_FACTOR * 4.0, run_affine)
+        idx1, d1, d2, good = self.ctx.match_result()
+        out = {"idx1": idx1, "d1": d1, "d2": d2, "good": good, "valid": self.ctx.valid_result()}
+        if run_affine:
+            out["affine"] = self.ctx.affine_result()
+        self._match = (idx1, good)
+        self._hough_bins = bins
+        return out
+
+
+class _LazyKeypoints:
+    """List-like view creating one (cached) KeyPoint object per accessed row, so the
+    same keypoint is the same object everywhere, as in the reference."""
+
+    def __init__(self, owner, which):
+        self._owner = owner
+        self._which = which
+        self._cache = {}
+
+    def _src(self):
+        return self._owner.db.kp if self._which == "db" else self._owner._qkp
+
+    def __len__(self):
+        src = self._src() if (self._owner.db is not None or self._which == "query") else None
+        return len(src) if src is not None else 0
+
+    def __getitem__(self, i):
+        i = int(i)
+        k = self._cache.get(i)
+        if k is None:
+            k = keypoints_from_arrays(self._src(), i)
+            self._cache[i] = k
+        return k

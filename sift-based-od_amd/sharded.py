@@ -1,0 +1,115 @@
+"""Database sharding across ranks (one process per GPU) -- SURVEY.md §8(e).
+
+Rank r holds descriptor rows [lo_r, hi_r) of the database (the keypoint table and the
+per-image table are replicated: they are ~8 % of the descriptor bytes and every rank
+needs them to verify bins).  One query image is processed by every rank:
+
+1. match the Nq queries against the local shard -> per query (d1^2, global idx1, d2^2)
+2. ALL-GATHER those 12 B/query candidates; every rank merges them (lexicographic on
+   (d^2, trainIdx), second = min of the rest) -- the ratio test is applied only AFTER
+   this global merge (a per-shard ratio test would keep different matches)
+3. each rank votes only for good matches whose trainIdx lies in its shard -> partial
+   bin counts + first-touch ordinals; ALL-REDUCE (sum, min) gives the global histogram
+   bit-exactly in any order
+4. valid bins, members, PoseBin means and the affine verification then run identically
+   on every rank (all inputs are replicated after 2 and 3).
+
+Two communicators carry the two exchanges:
+
+* :class:`RcclComm` -- RCCL over xGMI inside libsod (device buffers, the ctx stream);
+  the production path.
+* :class:`HostComm` -- the same exchanges staged through host memory over any object
+  providing ``allgather``/``allreduce`` of numpy arrays (``TorchHostComm`` wraps a
+  torch.distributed gloo group); used where RCCL is unavailable and by the CPU tests.
+
+``run_sharded`` drives either one with the same code, so the multi-rank logic tested
+with gloo on the CPU is the logic the GPUs run.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_range(n, rank, world):
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
+class RcclComm:
+    kind = "rccl"
+
+    def __init__(self, ctx, world, rank, broadcast_bytes):
+        """``broadcast_bytes(b or None) -> bytes`` distributes rank 0's RCCL unique id
+        (any bootstrap channel: torch.distributed, MPI, a file)."""
+        from . import _lib
+        self.world, self.rank = world, rank
+        uid = _lib.unique_id() if rank == 0 else None
+        uid = broadcast_bytes(uid)
+        ctx.comm_init(world, rank, uid)
+
+    def gather_candidates(self, ctx):
+        ctx.match_allgather()
+
+    def reduce_histogram(self, ctx):
+        ctx.hough_allreduce()
+
+
+class HostComm:
+    kind = "host"
+
+    def __init__(self, world, rank, allgather, allreduce):
+        """``allgather(arr) -> [arr_rank0, arr_rank1, ...]``;
+        ``allreduce(arr, op) -> arr`` with op in {"sum", "min"}."""
+        self.world, self.rank = world, rank
+        self._allgather = allgather
+        self._allreduce = allreduce
+
+    def gather_candidates(self, ctx):
+        d1, idx, d2 = ctx.candidates()
+        g1 = np.concatenate(self._allgather(d1))
+        gi = np.concatenate(self._allgather(idx))
+        g2 = np.concatenate(self._allgather(d2))
+        ctx.merge_candidates(g1, gi, g2)
+
+    def reduce_histogram(self, ctx):
+        cnt, fst = ctx.hough_partial()
+        cnt = self._allreduce(cnt.astype(np.int64), "sum").astype(np.uint32)
+        fst = self._allreduce(fst.astype(np.int64), "min").astype(np.uint32)
+        ctx.set_hough_partial(cnt, fst)
+
+
+class TorchHostComm(HostComm):
+    """HostComm over a torch.distributed process group (gloo)."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        self._t, self._d, self._g = torch, dist, group
+
+        def allgather(a):
+            t = torch.from_numpy(np.ascontiguousarray(a))
+            out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+            dist.all_gather(out, t, group=group)
+            return [o.numpy() for o in out]
+
+        def allreduce(a, op):
+            t = torch.from_numpy(np.ascontiguousarray(a))
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MIN,
+                            group=group)
+            return t.numpy()
+
+        super().__init__(dist.get_world_size(group), dist.get_rank(group), allgather, allreduce)
+
+
+def run_sharded(ctx, comm, shard, query_shape, bins, ratio=0.75, vote_threshold=5,
+                affine_threshold=4, x_factor=128.0, y_factor=128.0, run_affine=True):
+    """One query image over the sharded database.  ``shard`` = (lo, hi) global rows held
+    by this rank's ``ctx``.  Leaves the results in ``ctx`` (match_result, valid_result,
+    affine_result are then identical on every rank)."""
+    ctx.match()
+    comm.gather_candidates(ctx)
+    ctx.ratio(ratio)
+    ctx.hough(query_shape, bins, own=shard)
+    comm.reduce_histogram(ctx)
+    ctx.select(vote_threshold)
+    if run_affine:
+        ctx.affine((query_shape[1], query_shape[0]), x_factor, y_factor, affine_threshold)

@@ -1,0 +1,181 @@
+"""GPU: the drop-in Python API (reference names) and the sharded path with real kernels.
+Sharding is exercised with N contexts on one GPU, one host thread each, exchanging
+through a thread-barrier host communicator (the RCCL path needs one GPU per rank)."""
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from helpers import kp, kp_dict
+from oracle import oracle as orc
+from sift_based_od_amd import _lib, synthetic
+import sift_based_od_amd as sod
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bfmatcher_knnmatch():
+    g = golden("c1_b15")
+    matches = sod.BFMatcher().knnMatch(g["q_des"].astype(np.float32),
+                                       g["db_des"].astype(np.float32), k=2)
+    assert len(matches) == len(g["q_des"])
+    for q, (m, n) in enumerate(matches):
+        assert m.queryIdx == q and m.trainIdx == g["idx1"][q]
+        assert np.float32(m.distance) == g["d1"][q] and np.float32(n.distance) == g["d2"][q]
+        assert (m.distance < 0.75 * n.distance) == g["good"][q]
+
+
+def test_bfmatcher_single_train_row():
+    q = np.random.default_rng(0).integers(0, 256, (5, 128)).astype(np.uint8)
+    out = sod.BFMatcher().knnMatch(q, q[:1], k=2)
+    assert all(len(m) == 1 and m[0].trainIdx == 0 for m in out)
+
+
+def test_scalar_pose_and_bin_index():
+    g = golden("pose_sweep")
+    shape = tuple(int(v) for v in g["shape"])
+    for i in range(0, 20000, 997):
+        kM = sod.KeyPoint(g["mx"][i], g["my"][i], 0, g["ma"][i], 0, int(g["mo"][i]))
+        kQ = sod.KeyPoint(g["qx"][i], g["qy"][i], 0, g["qa"][i], 0, int(g["qo"][i]))
+        p = sod.estimate_object_pose((kM, kQ, (1500, 1000), (g["cx"][i], g["cy"][i])))
+        np.testing.assert_allclose(p, g["poses"][i], rtol=1e-13, atol=1e-10)
+        for j, b in enumerate(g["bins"]):
+            assert sod.calculate_bin_index(tuple(g["poses"][i]), int(b), shape) == \
+                tuple(g["idx"][j][i])
+    # batch form with per-axis bins reduces to the scalar form
+    idx = sod.calculate_bin_index_batch(g["poses"], (15, 15, 15, 15), shape)
+    assert np.array_equal(idx, g["idx"][0])
+
+
+def _tuples(g):
+    db_kp, q_kp = kp(g, "db_"), kp(g, "q_")
+    out = []
+    for q, m in zip(g["match_q"], g["match_m"]):
+        im = int(g["db_img"][m])
+        out.append((sod.KeyPoint(db_kp.x[m], db_kp.y[m], 0, db_kp.angle[m], 0, int(db_kp.octave[m])),
+                    sod.KeyPoint(q_kp.x[q], q_kp.y[q], 0, q_kp.angle[q], 0, int(q_kp.octave[q])),
+                    (int(g["size"][im][0]), int(g["size"][im][1])),
+                    (float(g["centroid"][im][0]), float(g["centroid"][im][1]))))
+    return out
+
+
+@pytest.mark.parametrize("name", ["edge_b15", "edge_b6"])
+def test_perform_hough_transform_and_affine_dropins(name):
+    g = golden(name)
+    t = _tuples(g)
+    b = int(g["bins"])
+    shape = tuple(int(v) for v in g["shape"])
+    table = sod.perform_hough_transform(t, type("I", (), {"shape": shape})(), b, b, b, b)
+    assert [k for k in table] == [tuple(k) for k in g["table_keys"]]
+    assert [v.votes for v in table.values()] == list(g["table_votes"])
+    valid = [v for v in table.values() if v.votes >= 5]
+    assert [v.pose for v in valid] == [tuple(k) for k in g["valid_keys"]]
+    # one AffineParameters + remove_outliers round per bin == the oracle's round
+    for v in valid[:20]:
+        mp = [p[0].pt for p in v.keypoint_pairs]
+        qp = [p[1].pt for p in v.keypoint_pairs]
+        sod.AffineParameters(v)
+        ref = orc.affine_params(mp, qp)
+        np.testing.assert_allclose(v.affine_parameters, ref, rtol=1e-6, atol=1e-4)
+        keep_ref, ch_ref = orc.remove_outliers(v.affine_parameters, mp, qp, v.pose[3],
+                                               (shape[1], shape[0]))
+        n0 = v.votes
+        _, changed = sod.remove_outliers(v, (shape[1], shape[0]), 128, 128)
+        assert changed == ch_ref and v.votes == sum(keep_ref) and n0 == len(keep_ref)
+
+
+def test_main_stages_match_golden():
+    g = golden("planted_b15")
+    db = sod.SiftDatabase(g["db_des"], kp(g, "db_"), g["db_img"], g["centroid"], g["size"])
+    m = sod.Main()
+    m.set_database(db)
+    m.get_query_features(g["q_des"], kp(g, "q_"), tuple(int(v) for v in g["shape"]))
+    m.run_matcher()
+    assert len(m.matching_keypoints) == int(g["good"].sum())
+    m.apply_hough_transform(int(g["bins"]))
+    assert [k for k in m.hough_transform] == [tuple(k) for k in g["table_keys"]]
+    m.get_valid_bins(5)
+    assert [b.pose for b in m.valid_bins] == [tuple(k) for k in g["valid_keys"]]
+    assert [b.votes for b in m.valid_bins] == list(g["valid_votes"])
+    for b, mu in zip(m.valid_bins, g["valid_means"]):
+        np.testing.assert_allclose([b.centroid[0], b.centroid[1], b.angle, b.scale,
+                                    b.img_size[0], b.img_size[1]], mu, rtol=1e-12, atol=1e-9)
+    m.apply_affine_parameters(4)
+    assert [b.pose for b in m.valid_bins] == [tuple(k) for k in g["surv_keys"]]
+    assert [b.votes for b in m.valid_bins] == list(g["surv_votes"])
+    for b, prm in zip(m.valid_bins, g["surv_params"]):
+        np.testing.assert_allclose(b.affine_parameters, prm, rtol=0, atol=1e-4)
+    assert len(m.keypoint_pairs) == int(g["surv_votes"].sum())
+
+
+class ThreadComm:
+    """allgather / allreduce between threads of one process (test plumbing)."""
+
+    def __init__(self, world):
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+
+    def for_rank(self, r):
+        from sift_based_od_amd.sharded import HostComm
+
+        def allgather(a):
+            self.slots[r] = np.array(a)
+            self.bar.wait()
+            out = list(self.slots)
+            self.bar.wait()
+            return out
+
+        def allreduce(a, op):
+            parts = allgather(a)
+            return (np.sum(parts, axis=0) if op == "sum" else np.min(parts, axis=0)).astype(a.dtype)
+
+        return HostComm(self.world, r, allgather, allreduce)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_in_process_equals_single(world):
+    db = synthetic.make_database(12, 500, seed=31)
+    qs = synthetic.make_queries(3000, seed=32, db_seed=31, kp_per_image=500)
+    bins = (32, 32, 8, 12)
+    # single context
+    with _lib.Context(0) as c:
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        c.upload_queries(qs.des, qs.kp)
+        c.pipeline(qs.shape, bins)
+        ref = (c.match_result(), c.valid_result(), c.affine_result())
+    comm = ThreadComm(world)
+    results = [None] * world
+    errors = []
+
+    def rank_main(r):
+        try:
+            lo, hi = sod.shard_range(len(db), r, world)
+            with _lib.Context(0) as c:
+                c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+                c.upload_db(db.des[lo:hi], row_offset=lo)
+                c.upload_queries(qs.des, qs.kp)
+                sod.run_sharded(c, comm.for_rank(r), (lo, hi), qs.shape, bins)
+                results[r] = (c.match_result(), c.valid_result(), c.affine_result())
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+            comm.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    (i1, d1, d2, g1), v1, a1 = ref
+    assert v1["keys"].shape[0] > 0
+    for (i2, e1, e2, g2), v2, a2 in results:
+        assert np.array_equal(i1, i2) and np.array_equal(d1, e1) and np.array_equal(d2, e2)
+        assert np.array_equal(g1, g2)
+        for k in ("keys", "votes", "offsets", "members"):
+            assert np.array_equal(v1[k], v2[k]), k
+        assert np.array_equal(v1["means"], v2["means"])
+        assert np.array_equal(a1["survived"], a2["survived"])
+        assert np.array_equal(a1["params"], a2["params"])
