@@ -56,7 +56,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-queries", type=int, default=512)
+    p.add_argument("--cpu-queries", type=int, default=4096)
     return p.parse_args()
 
 
@@ -143,6 +143,35 @@ def cpu_baseline(queries, db_des, nq_sample):
                       "rows on the host, %.1f s" % (len(q), len(db_des), dt)}
 
 
+def cpu_hough_baseline(qs, kp_all, img, cent, size, idx1, good, bins):
+    """The oracle's Python restatement of main.py:89-119 (single thread, like the
+    reference) on the same good matches: votes/s."""
+    from oracle import oracle as orc
+    matches = [(int(q), int(idx1[q])) for q in np.nonzero(good)[0]]
+    dbkp = {"x": kp_all[0], "y": kp_all[1], "angle": kp_all[2], "octave": kp_all[3], "img": img}
+    qkp = {"x": qs.kp.x, "y": qs.kp.y, "angle": qs.kp.angle, "octave": qs.kp.octave}
+    t0 = time.perf_counter()
+    table = orc.hough_vote(matches, qkp, dbkp, {"centroid": cent, "size": size}, bins, qs.shape)
+    dt = time.perf_counter() - t0
+    votes = sum(b.votes for b in table.values())
+    return {"value": votes / dt, "unit": "votes/s", "cores": 1, "kind": "port",
+            "sample": "oracle Hough vote loop (Python, main.py:89-119) over %d good matches, "
+                      "%d votes, %.1f s" % (len(matches), votes, dt)}
+
+
+def pmc_traffic(config, n_shard, nq):
+    """HBM bytes per matcher launch from the committed PMC summary of the same workload
+    (profiles/*_pmc_match_<config>.json, produced by tools/gpu_pmc.sh + tools/pmc_summary.py)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_match_%s.json" % config))):
+        best = f
+    if not best:
+        return None, None
+    d = json.load(open(best))
+    return d.get("hbm_bytes"), os.path.relpath(best, REPO)
+
+
 def main():
     a = parse()
     D = Dist(a.gpus)
@@ -222,6 +251,7 @@ def main():
     aff = ctx.affine_result() if run_affine else None
     idx1, d1, d2, good = ctx.match_result()
 
+    traffic, traffic_src = pmc_traffic(a.config, n_shard, nq)
     pairs = float(world) * nq * n_shard
     value = pairs / (ms_per_step / 1000.0)
     achieved = FLOP_PER_PAIR * nq * n_shard / (match_ms / 1000.0) / 1e12
@@ -244,6 +274,7 @@ def main():
             "queries": nq, "db_rows_per_gpu": n_shard, "db_rows_total": world * n_shard,
             "bins": list(bins), "parallelism": "db-shard%d" % world},
         "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
+        "hough_stage_votes_per_s": n_votes / ((float(stage[2]) + float(stage[3])) / 1000.0),
         "hough_votes": n_votes,
         "good_matches": int(good.sum()),
         "valid_bins": V,
@@ -252,7 +283,10 @@ def main():
                      "hough_vote": float(stage[2]), "select": float(stage[3]),
                      "affine": float(stage[4])},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
+                     "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
+                     "traffic_unit": "bytes/launch (HBM, 2*FETCH_SIZE+WRITE_SIZE)",
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes": 256 * (nq + n_shard) + 12 * nq,
                      "kernel": "match_kernel",
                      "algorithmic": "256 flop/pair x %d x %d pairs per launch" % (nq, n_shard)},
         "exact_order": ctx.exact_order(),
@@ -260,6 +294,8 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(qs.des, shard, a.cpu_queries)
+        out["cpu_baseline_hough"] = cpu_hough_baseline(qs, (x, y, ang, octv), img, cent, size,
+                                                       idx1, good, bins)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

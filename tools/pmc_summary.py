@@ -1,0 +1,37 @@
+"""Summarise rocprofv3 --pmc passes of the matcher (tools/gpu_pmc.sh) into one JSON under
+profiles/: per-launch averages, HBM bytes = 2*FETCH_SIZE*1024 (gfx950 reports half of a
+wide coalesced stream, MI355X_MICROARCH.md §HBM) + WRITE_SIZE*1024, the effective clock
+GRBM_GUI_ACTIVE/8/t and the MFMA-busy fraction.
+    python tools/pmc_summary.py gpurun_out/pmc_c3 profiles/r01_pmc_match_c3.json <kernel_ms>"""
+import collections
+import csv
+import json
+import os
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+kernel_ms = float(sys.argv[3]) if len(sys.argv) > 3 else None
+vals = collections.defaultdict(list)
+for sub in sorted(os.listdir(src)):
+    f = os.path.join(src, sub, "pmc_counter_collection.csv")
+    if not os.path.exists(f):
+        continue
+    for r in csv.DictReader(open(f)):
+        if "match_kernel" in r["Kernel_Name"]:
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+avg = {k: sum(v) / len(v) for k, v in vals.items()}
+out = {"kernel": "match_kernel", "counters_per_launch": avg}
+if "FETCH_SIZE" in avg:
+    out["hbm_read_bytes"] = 2 * avg["FETCH_SIZE"] * 1024
+if "WRITE_SIZE" in avg:
+    out["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
+if "hbm_read_bytes" in out and "hbm_write_bytes" in out:
+    out["hbm_bytes"] = out["hbm_read_bytes"] + out["hbm_write_bytes"]
+if kernel_ms and "GRBM_GUI_ACTIVE" in avg:
+    cyc = avg["GRBM_GUI_ACTIVE"] / 8
+    out["kernel_ms"] = kernel_ms
+    out["clock_ghz"] = cyc / (kernel_ms * 1e-3) / 1e9
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
+        out["mfma_busy_frac"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc)
+json.dump(out, open(dst, "w"), indent=1)
+print(json.dumps(out, indent=1))
