@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-queries", type=int, default=4096)
+    p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                   help="multi-rank exchange: RCCL on the device (default) or staged "
+                        "through host memory over gloo (for >1 rank per GPU)")
     return p.parse_args()
 
 
@@ -202,20 +205,32 @@ def main():
     qs = synthetic.make_queries(nq, seed=1, db_seed=0, kp_per_image=kpi)
     gen_s = time.time() - t0
 
-    ctx = _lib.Context(D.local)
+    dev = D.local
+    if world > 1:
+        import torch
+        ndev = max(1, torch.cuda.device_count())   # counting does not initialise HIP
+        dev = D.local % ndev                       # >1 rank per GPU only with --comm host
+    ctx = _lib.Context(dev)
     from sift_based_od_amd.database import Keypoints
     ctx.set_keypoints(Keypoints(x, y, ang, octv), img, cent, size)
     n_shard = shard.shape[0]
     ctx.upload_db(shard, row_offset=rank * n_shard)
     ctx.upload_queries(qs.des, qs.kp)
-    if world > 1:
-        uid = _lib.unique_id() if rank == 0 else None
-        uid = D.bcast_bytes(uid)
-        ctx.comm_init(world, rank, uid)
+    from sift_based_od_amd.sharded import RcclComm, TorchHostComm, run_sharded
+    comm = None
+    if world > 1 and a.comm == "rccl":
+        comm = RcclComm(ctx, world, rank, D.bcast_bytes)
+    elif world > 1:
+        comm = TorchHostComm()
+    own = (rank * n_shard, (rank + 1) * n_shard)
 
     def step():
-        ctx.pipeline(qs.shape, bins, ratio=0.75, vote_threshold=5, affine_threshold=4,
-                     x_factor=128.0, y_factor=128.0, run_affine=run_affine)
+        if comm is None or comm.kind == "rccl":
+            # one enqueue: match, all-gather, ratio, vote, all-reduce, select, affine
+            ctx.pipeline(qs.shape, bins, ratio=0.75, vote_threshold=5, affine_threshold=4,
+                         x_factor=128.0, y_factor=128.0, run_affine=run_affine)
+        else:
+            run_sharded(ctx, comm, own, qs.shape, bins, 0.75, 5, 4, 128.0, 128.0, run_affine)
 
     for _ in range(a.warmup):
         step()
@@ -272,7 +287,8 @@ def main():
             a.config.upper(), nq, n_shard, world * n_shard, "x".join(map(str, bins)),
             " + affine verify" if run_affine else ""),
             "queries": nq, "db_rows_per_gpu": n_shard, "db_rows_total": world * n_shard,
-            "bins": list(bins), "parallelism": "db-shard%d" % world},
+            "bins": list(bins), "parallelism": "db-shard%d" % world,
+            "comm": a.comm if world > 1 else None},
         "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
         "hough_stage_votes_per_s": n_votes / ((float(stage[2]) + float(stage[3])) / 1000.0),
         "hough_votes": n_votes,

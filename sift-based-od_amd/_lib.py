@@ -53,6 +53,7 @@ SIGNATURES = {
     "sod_query_upload": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int32, c_f32p, c_f32p, c_f32p,
                                    c_i32p]),
     "sod_match_enqueue": (C.c_int, [c_ctx]),
+    "sod_match_set_impl": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
     "sod_ratio_enqueue": (C.c_int, [c_ctx, C.c_double]),
     "sod_match_get": (C.c_int, [c_ctx, c_i32p, c_f32p, c_f32p, c_u8p]),
@@ -224,6 +225,13 @@ class Context:
         i = _c(idx1, np.int32)
         g = _c(np.asarray(good).astype(np.uint8), np.uint8)
         self._chk(self._L.sod_matches_set(self._h, len(i), ptr(i, C.c_int32), ptr(g, C.c_uint8)))
+
+    IMPLS = {"bf16": 0, "i8": 1}
+
+    def set_impl(self, impl):
+        """Matcher implementation "bf16" (default) or "i8"; call before uploads."""
+        self._chk(self._L.sod_match_set_impl(self._h, self.IMPLS[impl] if isinstance(impl, str)
+                                             else int(impl)))
 
     # -- stages --
     def match(self):

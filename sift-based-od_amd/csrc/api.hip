@@ -101,7 +101,8 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->first); sod_release(ctx->basekey); sod_release(ctx->vmask);
   sod_release(ctx->pose); sod_release(ctx->blk); sod_release(ctx->scal); sod_release(ctx->vbin);
   sod_release(ctx->voff); sod_release(ctx->members); sod_release(ctx->means);
-  sod_release(ctx->mq);
+  sod_release(ctx->mq); sod_release(ctx->vidx); sod_release(ctx->cursor);
+  sod_release(ctx->rtab);
   sod_release(ctx->allbin); sod_release(ctx->amx); sod_release(ctx->amy); sod_release(ctx->aqx);
   sod_release(ctx->aqy); sod_release(ctx->aisig); sod_release(ctx->surv);
   sod_release(ctx->fvotes); sod_release(ctx->params); sod_release(ctx->alive);
@@ -182,7 +183,9 @@ static int upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
     dsrc = ctx->stage_f32.p;
   }
   SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p, 0, 4, ctx->stream));  // invalid count
-  if (db)
+  if (ctx->impl == 1)
+    SOD_TRY(launch_pack_i8(ctx, dsrc, dtype, n, db));
+  else if (db)
     SOD_TRY(launch_pack_db(ctx, dsrc, dtype, n));
   else
     SOD_TRY(launch_pack_queries(ctx, dsrc, dtype, (int32_t)n));
@@ -237,9 +240,21 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq, const
 int sod_match_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
-  SOD_TRY(launch_match(ctx));
+  SOD_TRY(ctx->impl == 1 ? launch_match_i8(ctx) : launch_match(ctx));
   ctx->matched = true;
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_match_set_impl(sod_ctx* ctx, int impl) {
+  SOD_TRY(set_dev(ctx));
+  if (impl != 0 && impl != 1) return sod_fail(ctx, SOD_EINVAL, "impl must be 0 (bf16) or 1 (int8)");
+  if (impl != ctx->impl) {  // packed operands differ: uploads must be repeated
+    ctx->impl = impl;
+    ctx->nsub = 0;
+    ctx->nqt = 0;
+    ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  }
   return SOD_OK;
 }
 

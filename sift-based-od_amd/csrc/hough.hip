@@ -311,21 +311,25 @@ __global__ __launch_bounds__(1024) void scan_u32_kernel(uint32_t* __restrict__ a
 __global__ __launch_bounds__(kSelThreads) void select_write_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
     const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b, uint32_t thr,
-    const uint32_t* __restrict__ blk, uint32_t* __restrict__ out) {
+    const uint32_t* __restrict__ blk, uint32_t* __restrict__ out, uint32_t* __restrict__ vidx) {
   __shared__ uint32_t sh[kSelThreads / 64];
   const int64_t q = (int64_t)blockIdx.x * kSelThreads + threadIdx.x;
   uint32_t tmp[16];
   const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, thr, tmp) : 0;
   uint32_t tot;
   const uint32_t pos = blk[blockIdx.x] + block_excl_scan(n, sh, &tot);
-  for (uint32_t i = 0; i < n; ++i) out[pos + i] = tmp[i];
+  for (uint32_t i = 0; i < n; ++i) {
+    out[pos + i] = tmp[i];
+    if (vidx) vidx[tmp[i]] = pos + i;   // bin -> valid index (reset after the member sort)
+  }
 }
 
 // member offsets: voff[i] = sum_{j<i} count[vbin[j]], voff[V] = total (single workgroup)
 __global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __restrict__ vbin,
                                                               const uint32_t* __restrict__ gcount,
                                                               uint32_t* __restrict__ scal,
-                                                              int64_t* __restrict__ voff) {
+                                                              int64_t* __restrict__ voff,
+                                                              uint32_t* __restrict__ cursor) {
   __shared__ uint32_t sh[16];
   __shared__ int64_t carry_s;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -349,7 +353,10 @@ __global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __
       tot += sh[k];
     }
     const int64_t c = carry_s;
-    if (i < n) voff[i] = c + off + x - v;
+    if (i < n) {
+      voff[i] = c + off + x - v;
+      cursor[i] = 0;
+    }
     __syncthreads();
     if (threadIdx.x == 0) carry_s = c + tot;
     __syncthreads();
@@ -357,6 +364,153 @@ __global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __
   if (threadIdx.x == 0) {
     voff[n] = carry_s;
     scal[1] = (uint32_t)carry_s;
+  }
+}
+
+// members, step 1: every vote into a valid bin reserves a slot in its bin's member list.
+// A bin voted by many matches (a real object: thousands of votes) would serialise on one
+// global cursor, so each block of kFillQ queries first sorts its (valid bin, query) votes
+// in LDS: equal bins form runs and ONE atomicAdd per run reserves the run's slots.  Runs
+// land in arbitrary block order; member_sort_kernel restores query order per bin.
+constexpr int kFillQ = 256;                 // queries per block -> <= 4096 votes
+constexpr int kFillCap = kFillQ * 16;
+__global__ __launch_bounds__(256) void member_fill_kernel(
+    int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
+    const uint32_t* __restrict__ vidx, const int64_t* __restrict__ voff,
+    uint32_t* __restrict__ cursor, int32_t* __restrict__ members) {
+  __shared__ uint64_t key[kFillCap];
+  __shared__ uint32_t nvote;
+  __shared__ uint32_t sh[4];
+  if (threadIdx.x == 0) nvote = 0;
+  __syncthreads();
+  const int64_t q = (int64_t)blockIdx.x * kFillQ + threadIdx.x;
+  // 1. gather this block's votes into valid bins (order irrelevant: sorted next)
+  if (q < nq) {
+    const uint32_t m = vmask[q] & 0xFFFFu;
+    if (m) {
+      const uint32_t k = basekey[q];
+      const int ix = k & 0xFF, iy = (k >> 8) & 0xFF, it = (k >> 16) & 0xFF, is = k >> 24;
+      for (int slot = 0; slot < 16; ++slot) {
+        if (!((m >> slot) & 1u)) continue;
+        const uint32_t lb = lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                    it + ((slot >> 1) & 1), is + (slot & 1), b);
+        const uint32_t v = vidx[lb];
+        if (v == 0xFFFFFFFFu) continue;
+        key[atomicAdd(&nvote, 1u)] = ((uint64_t)v << 32) | (uint32_t)q;
+      }
+    }
+  }
+  __syncthreads();
+  const int n = (int)nvote;
+  if (n == 0) return;
+  int p = 1;
+  while (p < n) p <<= 1;
+  for (int i = n + threadIdx.x; i < p; i += blockDim.x) key[i] = ~0ull;
+  __syncthreads();
+  // 2. bitonic sort by (bin, query)
+  for (int kk = 2; kk <= p; kk <<= 1) {
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < p; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint64_t x = key[i], y = key[l];
+          if ((x > y) == ((i & kk) == 0)) {
+            key[i] = y;
+            key[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // 3. run starts: start[i] = last index <= i where the bin changes (block max-scan,
+  //    16 consecutive elements per thread)
+  __shared__ uint32_t start_of[kFillCap];
+  __shared__ uint32_t tmax[256];
+  const int per = (p + 255) / 256;
+  const int i0 = threadIdx.x * per;
+  uint32_t run = 0;
+  for (int i = i0; i < i0 + per && i < n; ++i) {
+    if (i == 0 || (uint32_t)(key[i - 1] >> 32) != (uint32_t)(key[i] >> 32)) run = (uint32_t)i;
+    start_of[i] = run;   // provisional: only valid if a head occurred within this chunk
+  }
+  tmax[threadIdx.x] = run;
+  __syncthreads();
+  if (threadIdx.x == 0) {   // 256-entry exclusive max-scan (cheap, LDS resident)
+    uint32_t m = 0;
+    for (int t = 0; t < 256; ++t) {
+      const uint32_t v = tmax[t];
+      tmax[t] = m;
+      m = v > m ? v : m;
+    }
+  }
+  __syncthreads();
+  {
+    const uint32_t carry = tmax[threadIdx.x];
+    bool head_seen = false;
+    for (int i = i0; i < i0 + per && i < n; ++i) {
+      if (i == 0 || (uint32_t)(key[i - 1] >> 32) != (uint32_t)(key[i] >> 32)) head_seen = true;
+      if (!head_seen) start_of[i] = carry;
+    }
+  }
+  __syncthreads();
+  // 4. the last element of each run reserves the run's slots (one atomic per run)
+  __shared__ uint32_t base_of[kFillCap];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t v = (uint32_t)(key[i] >> 32);
+    if (i == n - 1 || (uint32_t)(key[i + 1] >> 32) != v) {
+      const uint32_t st = start_of[i];
+      base_of[st] = atomicAdd(&cursor[v], (uint32_t)(i - st + 1));
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t v = (uint32_t)(key[i] >> 32);
+    const uint32_t st = start_of[i];
+    members[voff[v] + base_of[st] + (i - st)] = (int32_t)(uint32_t)key[i];
+  }
+  (void)sh;
+}
+
+// members, step 2: sort each bin's members by query index (= vote order, main.py:91) with
+// a bitonic sort in LDS; bins larger than kSortCap are rebuilt by members_kernel (scan).
+// Also resets the bin -> valid index map for the next call.
+constexpr int kSortCap = 4096;
+__global__ __launch_bounds__(256) void member_sort_kernel(const uint32_t* __restrict__ scal,
+                                                          const uint32_t* __restrict__ vbin,
+                                                          const int64_t* __restrict__ voff,
+                                                          uint32_t* __restrict__ vidx,
+                                                          int32_t* __restrict__ members) {
+  __shared__ uint32_t key[kSortCap];
+  const int64_t V = scal[0];
+  for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
+    const int64_t a = voff[v];
+    const int n = (int)(voff[v + 1] - a);
+    if (threadIdx.x == 0) vidx[vbin[v]] = 0xFFFFFFFFu;
+    if (n <= 1 || n > kSortCap) continue;   // uniform over the workgroup
+    int p = 1;
+    while (p < n) p <<= 1;
+    for (int i = threadIdx.x; i < p; i += blockDim.x)
+      key[i] = i < n ? (uint32_t)members[a + i] : 0xFFFFFFFFu;
+    __syncthreads();
+    for (int k = 2; k <= p; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < p; i += blockDim.x) {
+          const int l = i ^ j;
+          if (l > i) {
+            const uint32_t x = key[i], y = key[l];
+            const bool up = (i & k) == 0;
+            if ((x > y) == up) {
+              key[i] = y;
+              key[l] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) members[a + i] = (int32_t)key[i];
+    __syncthreads();
   }
 }
 
@@ -377,6 +531,7 @@ __global__ __launch_bounds__(256) void members_kernel(
     const int bs_ = lb % b.s, bt_ = (lb / b.s) % b.t, by_ = (lb / (b.s * b.t)) % b.y,
               bx_ = lb / (b.s * b.t * b.y);
     const uint32_t need = gcount[lb];
+    if (need <= (uint32_t)kSortCap) continue;   // handled by fill + sort
     const int64_t off = voff[v];
     uint32_t got = 0;
     for (int64_t q0 = gfirst[lb] >> 4; got < need && q0 < nq; q0 += 64 * U) {
@@ -433,9 +588,16 @@ __global__ void means_gather_kernel(const uint32_t* __restrict__ scal,
   }
 }
 
+__global__ void recip_table_kernel(const uint32_t* __restrict__ scal, double* __restrict__ rtab) {
+  const int64_t M = scal[1];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M;
+       i += (int64_t)gridDim.x * blockDim.x)
+    rtab[i] = 1.0 / (double)(i + 1);
+}
+
 __global__ void means_kernel(const uint32_t* __restrict__ scal, const int64_t* __restrict__ voff,
                              const double* __restrict__ mq, int64_t mstride,
-                             double* __restrict__ means) {
+                             const double* __restrict__ rtab, double* __restrict__ means) {
   const int64_t V = scal[0];
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < 6 * V;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -446,14 +608,22 @@ __global__ void means_kernel(const uint32_t* __restrict__ scal, const int64_t* _
     double m = x[a];                       // first vote: mean = pose / model size
     int64_t j = a + 1;
     // loads of a batch are independent of the recurrence: issue them together
+    // r / d with d = n + 1 as RN(r * inv) corrected by one FMA residual step (Markstein):
+    // with inv = RN(1/d) from a table the result equals the correctly rounded r / d
+    // (verified against r / d on 2e8 random cases), and the chain is 5 dependent f64 ops.
     for (; j + 8 <= e; j += 8) {
-      double b[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) b[i] = x[j + i];
+      double b[8], inv[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const double n = (double)(j + i - a);
-        m = (m * n + b[i]) / (n + 1.0);    // n + 1 is an exact small integer
+        b[i] = x[j + i];
+        inv[i] = rtab[j + i - a];            // 1 / (n + 1), n = j + i - a
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const double n = (double)(j + i - a), d = n + 1.0;
+        const double r = m * n + b[i];     // -ffp-contract=off: rounded mul, rounded add
+        const double q0 = r * inv[i];
+        m = __builtin_fma(__builtin_fma(-q0, d, r), inv[i], q0);
       }
     }
     for (; j < e; ++j) {
@@ -689,7 +859,8 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
   return SOD_OK;
 }
 
-static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* total_slot) {
+static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* total_slot,
+                          uint32_t* vidx) {
   const int64_t nq = ctx->nq;
   const int64_t nblk = cdiv(nq, kSelThreads);
   SOD_TRY(sod_reserve(ctx, ctx->blk, (size_t)nblk));
@@ -702,7 +873,7 @@ static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* t
   SOD_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(select_write_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream,
                      nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
-                     thr, ctx->blk.p, out);
+                     thr, ctx->blk.p, out, vidx);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
@@ -717,9 +888,22 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   SOD_TRY(sod_reserve(ctx, ctx->voff, (size_t)ctx->vmax + 1));
   SOD_TRY(sod_reserve(ctx, ctx->members, (size_t)ctx->mmax));
   SOD_TRY(sod_reserve(ctx, ctx->means, (size_t)ctx->vmax * 6));
-  SOD_TRY(run_compaction(ctx, (uint32_t)thr, ctx->vbin.p, ctx->scal.p + 0));
+  SOD_TRY(sod_reserve(ctx, ctx->cursor, (size_t)ctx->vmax));
+  if (ctx->vidx.n < (size_t)ctx->nbins) {   // bin -> valid index, all-ones between calls
+    SOD_TRY(sod_reserve(ctx, ctx->vidx, (size_t)ctx->nbins));
+    SOD_HIP(ctx, hipMemsetAsync(ctx->vidx.p, 0xFF, ctx->vidx.n * 4, ctx->stream));
+  }
+  SOD_TRY(run_compaction(ctx, (uint32_t)thr, ctx->vbin.p, ctx->scal.p + 0, ctx->vidx.p));
   hipLaunchKernelGGL(member_offsets_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->vbin.p,
-                     ctx->counts.p, ctx->scal.p, ctx->voff.p);
+                     ctx->counts.p, ctx->scal.p, ctx->voff.p, ctx->cursor.p);
+  SOD_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(member_fill_kernel, dim3((unsigned)cdiv(nq, kFillQ)), dim3(256), 0, ctx->stream,
+                     nq, ctx->basekey.p, ctx->vmask.p, ctx_bins(ctx), ctx->vidx.p, ctx->voff.p,
+                     ctx->cursor.p, ctx->members.p);
+  SOD_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(member_sort_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
+                     ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, ctx->vidx.p,
+                     ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   const int wg = std::max(1, ctx->num_cus * 4);
   hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
@@ -731,8 +915,12 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
                      ctx->stream, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p,
                      ctx->mimg.p, ctx->isize.p, ctx->mmax, ctx->mq.p);
   SOD_HIP(ctx, hipGetLastError());
+  SOD_TRY(sod_reserve(ctx, ctx->rtab, (size_t)ctx->mmax));
+  hipLaunchKernelGGL(recip_table_kernel, dim3(std::max(1, ctx->num_cus)), dim3(256), 0,
+                     ctx->stream, ctx->scal.p, ctx->rtab.p);
+  SOD_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus * 2)), dim3(64), 0, ctx->stream,
-                     ctx->scal.p, ctx->voff.p, ctx->mq.p, ctx->mmax, ctx->means.p);
+                     ctx->scal.p, ctx->voff.p, ctx->mq.p, ctx->mmax, ctx->rtab.p, ctx->means.p);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
@@ -741,7 +929,7 @@ int launch_all_bins(sod_ctx* ctx) {
   const int64_t bmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * (int64_t)ctx->nq));
   SOD_TRY(sod_reserve(ctx, ctx->scal, 4));
   SOD_TRY(sod_reserve(ctx, ctx->allbin, (size_t)bmax));
-  return run_compaction(ctx, 1u, ctx->allbin.p, ctx->scal.p + 2);
+  return run_compaction(ctx, 1u, ctx->allbin.p, ctx->scal.p + 2, nullptr);
 }
 
 int launch_affine_gather(sod_ctx* ctx) {

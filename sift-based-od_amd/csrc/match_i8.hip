@@ -1,0 +1,302 @@
+// match_i8.hip -- the brute-force k=2 matcher on the int8 MFMA (v_mfma_i32_16x16x64_i8),
+// twice the bf16 MFMA rate, exact.
+//
+// SIFT values are integers 0..255; shifted by -128 they are int8, and the L2 distance is
+// shift-invariant: ||q - d||^2 = ||q'||^2 + ||d'||^2 - 2 q'.d'  (q' = q - 128, d' = d - 128).
+// The MFMA accumulates q'.d' exactly in i32 (|q'.d'| <= 2^21).  Minimising the distance
+// is maximising y = 2 q'.d' - ||d'||^2; -2 does not fit the int8 operands, so the row
+// norm is folded into the accumulator init as c = floor(-||d'||^2 / 2) (w = -||d'||^2 is
+// stored per row; c = w >> 1).  The MFMA then yields h = q'.d' + c and y = 2h + (w & 1):
+// ordering by y is ordering by h with the parity bit as tiebreak, and max(h) >=
+// floor(y2 / 2) is a NECESSARY condition for a row to beat the running second best y2 --
+// so the fast path needs no per-element op (3 VALU per 16x16 tile, like the bf16 path).
+// The two largest y per query (= two smallest distances) are tracked exactly;
+// distance^2 = ||q'||^2 - y, exact in f32 (< 2^24).
+//
+// Layout (operand lane map verified on hardware, tools/mfma_i8_layout.hip): lane l holds
+// A[row l&15][k 16(l>>4)..+15] and B[k ..][col l&15]; D: col l&15, rows 4(l>>4)+r.  A 16-row
+// subtile is [kstep 2][lane 64][16 B] = 2 KiB (the LDS image is the HBM image).
+// Structure as match.hip: queries stationary in VGPRs (64 per lane for 128 queries),
+// 2-slot LDS-DMA ring of 128-row stages, prefilter + one uniform branch per subtile.
+#include <climits>
+
+#include "sod_internal.h"
+
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+namespace {
+
+constexpr int QT = 8;          // 16-query tiles per wave
+constexpr int NW = 4;
+constexpr int NT = NW * 64;
+constexpr int SPS = 8;         // subtiles per stage (128 rows)
+constexpr int kSub = 2048;     // bytes per 16-row subtile
+constexpr int kStageBytes = SPS * kSub;          // 16 KiB
+constexpr int kStageNorm = SPS * kSubRows * 4;   // 512 B of i32 norms
+constexpr int kStageSlot = kStageBytes + kStageNorm;
+constexpr int kPiecesPerWave = kStageBytes / 1024 / NW;   // 4
+constexpr int kNormLanes = kStageNorm / 16 / NW;          // 8
+constexpr int kPadNormI = 1 << 30;                        // ||d'||^2 of padding rows (w = -2^30)
+static_assert(kStageBytes / 1024 % NW == 0, "pieces split evenly");
+
+// pack: one thread per (row, 16-dim chunk c = 0..7); int8 of (value - 128); exact i32 norm
+template <typename TIn>
+__global__ void pack_i8_kernel(const TIn* __restrict__ src, int64_t n, int64_t npad,
+                               uint8_t* __restrict__ pack, int* __restrict__ norms, int padnorm,
+                               uint32_t* __restrict__ flags, int max_slot) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = t >> 3;
+  const int c = (int)(t & 7);
+  if (row >= npad) return;   // npad*8 threads is a multiple of 64
+  int v[16];
+  uint32_t bad = 0;
+  if (row < n) {
+    if constexpr (sizeof(TIn) == 1) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(src + row * kDim + c * 16);
+      const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = (int)((w[j >> 2] >> (8 * (j & 3))) & 0xFF);
+    } else {
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const float4 f = *reinterpret_cast<const float4*>(src + row * kDim + c * 16 + 4 * j4);
+        const float ff[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float x = ff[j];
+          const bool finite = (__float_as_uint(x) & 0x7f800000u) != 0x7f800000u;
+          const bool ok = finite && x >= 0.f && x <= 255.f && x == truncf(x);
+          bad |= ok ? 0u : 1u;
+          v[4 * j4 + j] = ok ? (int)x : 0;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = 128;   // shifted to 0
+  }
+  int ss = 0, raw = 0;
+  uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int s = v[j] - 128;
+    ss += s * s;
+    raw += v[j] * v[j];
+    o[j >> 2] |= ((uint32_t)(s & 0xFF)) << (8 * (j & 3));
+  }
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) {
+    ss += __shfl_xor(ss, m, 8);
+    raw += __shfl_xor(raw, m, 8);
+  }
+  const int64_t sub = row >> 4;
+  const int rr = (int)(row & 15);
+  const int64_t off = sub * kSub + (c >> 2) * 1024 + (rr + 16 * (c & 3)) * 16;
+  *reinterpret_cast<uint4*>(pack + off) = make_uint4(o[0], o[1], o[2], o[3]);
+  if (c == 0) {
+    // DB rows: w = -||d'||^2 (padding: -2^30); queries: +||q'||^2 (padding: 0)
+    norms[row] = (row < n) ? (padnorm ? -ss : ss) : -padnorm;
+    // raw ||v||^2 (as float bits, like match.hip) for sod_match_exact_order
+    if (row < n) atomicMax(&flags[max_slot], __float_as_uint((float)raw));
+  }
+  if (bad) atomicAdd(&flags[0], 1u);
+}
+
+__device__ __forceinline__ void glds16(const void* g, uint8_t* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
+                                            const int* __restrict__ dn, int64_t sub0,
+                                            uint8_t* slot, int wave, int lane) {
+  const uint8_t* src = dbpack + sub0 * kSub;
+#pragma unroll
+  for (int j = 0; j < kPiecesPerWave; ++j) {
+    const int piece = wave * kPiecesPerWave + j;
+    glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
+  }
+  const int* nsrc = dn + sub0 * kSubRows + wave * (kNormLanes * 4) + lane * 4;
+  if (lane < kNormLanes) glds16(nsrc, slot + kStageBytes + wave * (kNormLanes * 16));
+}
+
+__device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int oi, int o2) {
+  // max on y (= min distance), ties -> lower trainIdx; second = max of the rest
+  if (o1 > y1 || (o1 == y1 && oi < i1)) {
+    y2 = max(y1, o2);
+    y1 = o1;
+    i1 = oi;
+  } else {
+    y2 = max(y2, o1);
+  }
+}
+
+__global__ __launch_bounds__(NT, 2) void match_i8_kernel(
+    const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
+    const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
+    int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
+    int* __restrict__ pidx, float* __restrict__ pd2) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStageSlot];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sp = blockIdx.x % split;
+  const int qb = blockIdx.x / split;
+  const int qt0 = (qb * NW + wave) * QT;
+  const int64_t s_lo = (int64_t)sp * sub_per_split;
+  const int64_t s_hi = min(nsub, s_lo + sub_per_split);
+  const int64_t nst = (s_hi - s_lo) / SPS;
+
+  if (nst > 0) issue_stage(dbpack, dn, s_lo, lds, wave, lane);
+
+  i32x4 bq[QT][2];
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int qt = qt0 + t;
+      bq[t][k] = qt < nqt ? *reinterpret_cast<const i32x4*>(qpack + ((int64_t)qt * 2 + k) * 1024 + lane * 16)
+                          : i32x4{0, 0, 0, 0};
+    }
+  int y1[QT], y2[QT], t2[QT], id[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    y1[t] = INT_MIN;
+    y2[t] = INT_MIN;
+    t2[t] = INT_MIN >> 1;
+    id[t] = 0x7fffffff;
+  }
+
+  for (int64_t s = 0; s < nst; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nst) issue_stage(dbpack, dn, s_lo + (s + 1) * SPS, lds + ((s + 1) & 1) * kStageSlot, wave, lane);
+    const uint8_t* sb = lds + (s & 1) * kStageSlot;
+    i32x4 fa0 = *reinterpret_cast<const i32x4*>(sb + lane * 16);
+    i32x4 fa1 = *reinterpret_cast<const i32x4*>(sb + 1024 + lane * 16);
+    i32x4 fw = *reinterpret_cast<const i32x4*>(sb + kStageBytes + (lane >> 4) * 16);
+#pragma unroll
+    for (int u = 0; u < SPS; ++u) {
+      const i32x4 a0 = fa0, a1 = fa1, w = fw;
+      const i32x4 c = {w[0] >> 1, w[1] >> 1, w[2] >> 1, w[3] >> 1};   // floor(-||d'||^2 / 2)
+      i32x4 acc[QT];
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq[t][0], c, 0, 0, 0);
+      if (u + 1 < SPS) {   // next subtile's fragments in flight
+        const uint8_t* nb = sb + (u + 1) * kSub + lane * 16;
+        fa0 = *reinterpret_cast<const i32x4*>(nb);
+        fa1 = *reinterpret_cast<const i32x4*>(nb + 1024);
+        fw = *reinterpret_cast<const i32x4*>(sb + kStageBytes + (u + 1) * 64 + (lane >> 4) * 16);
+      }
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq[t][1], acc[t], 0, 0, 0);
+      // prefilter on h: a row can beat y2 only if h >= floor(y2 / 2)
+      bool hit[QT];
+      bool any = false;
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        const int m = max(max(acc[t][0], acc[t][1]), max(acc[t][2], acc[t][3]));
+        hit[t] = m >= t2[t];
+        any |= hit[t];
+      }
+      if (__any(any)) {
+        const int rowb = row_offset + (int)((s_lo + s * SPS + u) * kSubRows) + (lane >> 4) * 4;
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          if (__any(hit[t])) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int y = 2 * acc[t][r] + (w[r] & 1);
+              const bool gt = y > y1[t];
+              y2[t] = max(min(y1[t], y), y2[t]);   // med3(y1, y2, y) with y1 >= y2
+              id[t] = gt ? rowb + r : id[t];
+              y1[t] = gt ? y : y1[t];
+            }
+            t2[t] = y2[t] >> 1;
+          }
+        }
+      }
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      const int o1 = __shfl_xor(y1[t], m), oi = __shfl_xor(id[t], m), o2 = __shfl_xor(y2[t], m);
+      merge2i(y1[t], id[t], y2[t], o1, oi, o2);
+    }
+    const int qt = qt0 + t;
+    if (lane < 16 && qt < nqt) {
+      const int64_t q = (int64_t)qt * 16 + lane;
+      const int n2 = qn[q];
+      const int64_t o = (int64_t)sp * nq_pad + q;
+      // padding rows only win when the shard has fewer than two real rows: keep them huge
+      pd1[o] = y1[t] < -(1 << 29) ? 3.0e38f : (float)(n2 - y1[t]);
+      pidx[o] = id[t];
+      pd2[o] = y2[t] < -(1 << 29) ? 3.0e38f : (float)(n2 - y2[t]);
+    }
+  }
+}
+
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db) {
+  const int64_t npad = db ? cdiv(n, SPS * kSubRows) * SPS * kSubRows : cdiv(n, kSubRows) * kSubRows;
+  uint8_t* pack;
+  int* norms;
+  if (db) {
+    ctx->nsub = npad / kSubRows;
+    SOD_TRY(sod_reserve(ctx, ctx->dbpack, (size_t)ctx->nsub * kSub));
+    SOD_TRY(sod_reserve(ctx, ctx->dn, (size_t)npad));
+    pack = ctx->dbpack.p;
+    norms = reinterpret_cast<int*>(ctx->dn.p);
+  } else {
+    ctx->nqt = (int32_t)(npad / kSubRows);
+    SOD_TRY(sod_reserve(ctx, ctx->qpack, (size_t)ctx->nqt * kSub));
+    SOD_TRY(sod_reserve(ctx, ctx->qn, (size_t)npad));
+    pack = ctx->qpack.p;
+    norms = reinterpret_cast<int*>(ctx->qn.p);
+  }
+  const int64_t threads = npad * 8;
+  const int bs = 256;
+  const unsigned grid = (unsigned)cdiv(threads, bs);
+  const int padnorm = db ? kPadNormI : 0;
+  const int slot = db ? 1 : 2;
+  if (dtype == SOD_DTYPE_U8)
+    hipLaunchKernelGGL(pack_i8_kernel<uint8_t>, dim3(grid), dim3(bs), 0, ctx->stream,
+                       (const uint8_t*)dsrc, n, npad, pack, norms, padnorm, ctx->flags.p, slot);
+  else
+    hipLaunchKernelGGL(pack_i8_kernel<float>, dim3(grid), dim3(bs), 0, ctx->stream,
+                       (const float*)dsrc, n, npad, pack, norms, padnorm, ctx->flags.p, slot);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+int launch_match_i8(sod_ctx* ctx) {
+  const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
+  const int64_t qblocks = cdiv(ctx->nqt, NW * QT);
+  const int64_t nstages = ctx->nsub / SPS;
+  const int64_t target = 2LL * ctx->num_cus;
+  int64_t split = std::max<int64_t>(1, (target + qblocks / 2) / qblocks);
+  split = std::min<int64_t>(split, nstages);
+  const int64_t st_per_split = cdiv(nstages, split);
+  split = cdiv(nstages, st_per_split);
+  ctx->split = (int)split;
+  SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(split * nq_pad)));
+  SOD_TRY(sod_reserve(ctx, ctx->pd2, (size_t)(split * nq_pad)));
+  SOD_TRY(sod_reserve(ctx, ctx->pidx, (size_t)(split * nq_pad)));
+  SOD_TRY(sod_reserve(ctx, ctx->cd1, (size_t)nq_pad));
+  SOD_TRY(sod_reserve(ctx, ctx->cd2, (size_t)nq_pad));
+  SOD_TRY(sod_reserve(ctx, ctx->cidx, (size_t)nq_pad));
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+  hipLaunchKernelGGL(match_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(NT), 0, ctx->stream,
+                     ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub, ctx->qpack.p,
+                     reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad, (int)split,
+                     st_per_split * SPS, (int)ctx->row_offset, ctx->pd1.p, ctx->pidx.p, ctx->pd2.p);
+  SOD_HIP(ctx, hipGetLastError());
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+  return launch_merge(ctx, ctx->pd1.p, ctx->pidx.p, ctx->pd2.p, (int)split, nq_pad);
+}

@@ -31,6 +31,7 @@ struct sod_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   int num_cus = 256;
+  int impl = 0;                 // matcher: 0 = bf16 MFMA (match.hip), 1 = int8 MFMA (match_i8.hip)
 
   // ---- database (keypoints replicated, descriptors = shard) ----
   int64_t n_total = 0;          // keypoints in the whole DB
@@ -89,6 +90,9 @@ struct sod_ctx {
   DevBuf<int32_t> members;      // [mmax] query index
   DevBuf<double> means;         // [vmax*6]
   DevBuf<double> mq;            // [6][mmax] per-member mean inputs
+  DevBuf<uint32_t> vidx;        // [nbins] bin -> valid index (0xFFFFFFFF otherwise)
+  DevBuf<uint32_t> cursor;      // [vmax] member fill cursors
+  DevBuf<double> rtab;          // [mmax] 1/(n+1) for the running means
   DevBuf<uint32_t> allbin;      // [bmax] all occupied bins, first-touch order
   int64_t vmax = 0, mmax = 0;
   int32_t vote_thr = 0;
@@ -153,6 +157,8 @@ void sod_release(DevBuf<T>& b) {
 int launch_pack_db(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n);
 int launch_pack_queries(sod_ctx* ctx, const void* dsrc, int dtype, int32_t nq);
 int launch_match(sod_ctx* ctx);
+int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db);
+int launch_match_i8(sod_ctx* ctx);
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2,
                  int nparts, int64_t stride);
 int launch_ratio(sod_ctx* ctx, double ratio);

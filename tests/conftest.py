@@ -25,8 +25,14 @@ def golden(name):
 
 
 @pytest.fixture(scope="session")
-def ctx():
+def _ctx_session():
     from sift_based_od_amd import _lib
     c = _lib.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture
+def ctx(_ctx_session):
+    _ctx_session.set_impl("bf16")
+    return _ctx_session

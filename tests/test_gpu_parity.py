@@ -14,6 +14,7 @@ pytestmark = pytest.mark.gpu
 
 CASES = ["c1_b15", "planted_b15", "planted_b12"]
 AFFINE_ATOL = 1e-4
+IMPLS = ["bf16", "i8"]
 
 
 def load_case(ctx, g):
@@ -22,9 +23,11 @@ def load_case(ctx, g):
     ctx.upload_queries(g["q_des"], kp(g, "q_"))
 
 
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("name", CASES)
-def test_matcher_golden(ctx, name):
+def test_matcher_golden(ctx, name, impl):
     g = golden(name)
+    ctx.set_impl(impl)
     load_case(ctx, g)
     ctx.match()
     ctx.ratio(0.75)
@@ -34,10 +37,13 @@ def test_matcher_golden(ctx, name):
     assert np.array_equal(d2.view(np.uint32), g["d2"].view(np.uint32))
     assert np.array_equal(good, g["good"])
     assert ctx.exact_order()
+    ctx.set_impl("bf16")
 
 
-def test_matcher_edges(ctx):
+@pytest.mark.parametrize("impl", IMPLS)
+def test_matcher_edges(ctx, impl):
     g = golden("matcher_edges")
+    ctx.set_impl(impl)
     ctx.upload_db(g["db_des"])
     ctx.upload_queries(g["q_des"])
     ctx.match()
@@ -48,9 +54,11 @@ def test_matcher_edges(ctx):
     assert np.array_equal(good, g["good"])
 
 
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("nq,ndb,seed", [(1, 2, 0), (17, 1000, 1), (700, 4099, 2), (3000, 60000, 3)])
-def test_matcher_vs_oracle(ctx, nq, ndb, seed):
+def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
     rng = np.random.default_rng(seed)
+    ctx.set_impl(impl)
     db = synthetic.sift_like_descriptors(rng, ndb)
     q = synthetic.sift_like_descriptors(rng, nq)
     q[: nq // 3] = db[rng.integers(0, ndb, nq // 3)]      # exact hits (d1 = 0)
@@ -65,8 +73,10 @@ def test_matcher_vs_oracle(ctx, nq, ndb, seed):
     assert np.array_equal(good, orc.ratio_test(f1, f2))
 
 
-def test_matcher_f32_input_and_validation(ctx):
+@pytest.mark.parametrize("impl", IMPLS)
+def test_matcher_f32_input_and_validation(ctx, impl):
     rng = np.random.default_rng(11)
+    ctx.set_impl(impl)
     db = rng.integers(0, 256, (500, 128)).astype(np.uint8)
     q = rng.integers(0, 256, (100, 128)).astype(np.uint8)
     ctx.upload_db(db.astype(np.float32))
@@ -116,9 +126,11 @@ def _check_hough(ctx, g):
         assert np.array_equal(kept, g["surv_members"][g["surv_off"][k]:g["surv_off"][k + 1]])
 
 
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("name", CASES)
-def test_pipeline_golden(ctx, name):
+def test_pipeline_golden(ctx, name, impl):
     g = golden(name)
+    ctx.set_impl(impl)
     load_case(ctx, g)
     shape = tuple(int(v) for v in g["shape"])
     ctx.pipeline(shape, int(g["bins"]), ratio=0.75, vote_threshold=5, affine_threshold=4)
