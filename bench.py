@@ -5,7 +5,7 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One step = one pass of the whole hot path over one synthetic query image:
-BF k=2 matching of Nq queries against this rank's DB shard (bf16 MFMA) -> RCCL all-gather
+BF k=2 matching of Nq queries against this rank's DB shard (int8 MFMA, exact) -> RCCL all-gather
 + global top-2 merge -> ratio test -> Hough pose + LDS-privatised vote histogram (own
 shard) -> RCCL all-reduce of bin counts / first touch -> valid-bin selection, members,
 PoseBin means -> per-bin affine LSQ + outlier rejection to a fixed point.
@@ -16,7 +16,7 @@ the query image has 50k keypoints (1000x800), bins 32x32x8x12, thresholds 5/4.
 
 value = descriptor pairs / s over the whole job = N * Nq * Nshard / step time (max over
 ranks).  Hough votes/s and per-stage times are reported beside it, the matcher kernel's
-achieved bf16 MFMA rate against the 2.5 PF/s dense peak in "roofline", and the CPU
+achieved MFMA rate against the dense peak of its type in "roofline", and the CPU
 restatement (oracle, numpy/OpenBLAS on the host cores) on a bounded slice in
 "cpu_baseline".
 """
@@ -37,8 +37,14 @@ sod_pkg.load()
 from sift_based_od_amd import _lib, synthetic  # noqa: E402
 
 METRIC = "descriptor-pair distances/sec + Hough votes/sec per query; 1/2/4/8 GPU"
-PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
-FLOP_PER_PAIR = 2 * 128
+OPS_PER_PAIR = 2 * 128          # one multiply + one add per dimension
+# matcher implementations: kernel name, arithmetic type, dense MFMA peak of that type on
+# MI355X (MI355X_MICROARCH.md "Matrix cores": bf16 ~2.5 PF, int8 2x bf16 per clock)
+IMPLS = {
+    "i8": ("match_i8_kernel", "i8", 5000.0, "TOP/s"),
+    "i8w": ("match_i8w_kernel", "i8", 5000.0, "TOP/s"),
+    "bf16": ("match_kernel", "bf16", 2500.0, "TFLOP/s"),
+}
 
 CONFIGS = {
     # name: (queries, images per rank, keypoints per image, bins, run_affine)
@@ -57,6 +63,9 @@ def parse():
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-queries", type=int, default=4096)
+    p.add_argument("--impl", default="i8", choices=sorted(IMPLS),
+                   help="matcher kernel: int8 MFMA 16x16x64 (default, fastest), int8 32x32x32 "
+                        "or bf16 MFMA; all bit-exact")
     p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                    help="multi-rank exchange: RCCL on the device (default) or staged "
                         "through host memory over gloo (for >1 rank per GPU)")
@@ -162,12 +171,13 @@ def cpu_hough_baseline(qs, kp_all, img, cent, size, idx1, good, bins):
                       "%d votes, %.1f s" % (len(matches), votes, dt)}
 
 
-def pmc_traffic(config, n_shard, nq):
-    """HBM bytes per matcher launch from the committed PMC summary of the same workload
-    (profiles/*_pmc_match_<config>.json, produced by tools/gpu_pmc.sh + tools/pmc_summary.py)."""
+def pmc_traffic(kernel, config):
+    """HBM bytes per matcher launch from the committed PMC summary of the same kernel and
+    workload (profiles/*_pmc_<kernel>_<config>.json, from tools/gpu_pmc.sh +
+    tools/pmc_summary.py)."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_match_%s.json" % config))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s_%s.json" % (kernel, config)))):
         best = f
     if not best:
         return None, None
@@ -211,6 +221,8 @@ def main():
         ndev = max(1, torch.cuda.device_count())   # counting does not initialise HIP
         dev = D.local % ndev                       # >1 rank per GPU only with --comm host
     ctx = _lib.Context(dev)
+    ctx.set_impl(a.impl)
+    kernel, dtype, peak, peak_unit = IMPLS[a.impl]
     from sift_based_od_amd.database import Keypoints
     ctx.set_keypoints(Keypoints(x, y, ang, octv), img, cent, size)
     n_shard = shard.shape[0]
@@ -266,10 +278,10 @@ def main():
     aff = ctx.affine_result() if run_affine else None
     idx1, d1, d2, good = ctx.match_result()
 
-    traffic, traffic_src = pmc_traffic(a.config, n_shard, nq)
+    traffic, traffic_src = pmc_traffic(kernel, a.config)
     pairs = float(world) * nq * n_shard
     value = pairs / (ms_per_step / 1000.0)
-    achieved = FLOP_PER_PAIR * nq * n_shard / (match_ms / 1000.0) / 1e12
+    achieved = OPS_PER_PAIR * nq * n_shard / (match_ms / 1000.0) / 1e12
     out = {
         "metric": METRIC,
         "value": value,
@@ -281,7 +293,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": dtype,
         "data": "synthetic (seeded SIFT-like uint8 descriptors, SURVEY.md §8(d))",
         "config": {"workload": "%s: %d query x %d DB/GPU (total %d) + Hough %s%s" % (
             a.config.upper(), nq, n_shard, world * n_shard, "x".join(map(str, bins)),
@@ -298,13 +310,14 @@ def main():
         "stage_ms": {"match_kernel": match_ms, "merge_gather_ratio": float(stage[1]),
                      "hough_vote": float(stage[2]), "select": float(stage[3]),
                      "affine": float(stage[4])},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
+                     "unit": peak_unit, "frac": achieved / peak, "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, 2*FETCH_SIZE+WRITE_SIZE)",
                      "traffic_source": traffic_src,
                      "algorithmic_bytes": 256 * (nq + n_shard) + 12 * nq,
-                     "kernel": "match_kernel",
-                     "algorithmic": "256 flop/pair x %d x %d pairs per launch" % (nq, n_shard)},
+                     "kernel": kernel,
+                     "algorithmic": "256 op/pair x %d x %d pairs per launch" % (nq, n_shard)},
+        "matcher_impl": a.impl,
         "exact_order": ctx.exact_order(),
         "datagen_s": gen_s,
     }

@@ -226,10 +226,11 @@ class Context:
         g = _c(np.asarray(good).astype(np.uint8), np.uint8)
         self._chk(self._L.sod_matches_set(self._h, len(i), ptr(i, C.c_int32), ptr(g, C.c_uint8)))
 
-    IMPLS = {"bf16": 0, "i8": 1}
+    IMPLS = {"bf16": 0, "i8": 1, "i8w": 2}
 
     def set_impl(self, impl):
-        """Matcher implementation "bf16" (default) or "i8"; call before uploads."""
+        """Matcher implementation "bf16" (default), "i8" (int8 16x16x64) or "i8w" (int8
+        32x32x32); call before uploads."""
         self._chk(self._L.sod_match_set_impl(self._h, self.IMPLS[impl] if isinstance(impl, str)
                                              else int(impl)))
 

@@ -183,7 +183,7 @@ static int upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
     dsrc = ctx->stage_f32.p;
   }
   SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p, 0, 4, ctx->stream));  // invalid count
-  if (ctx->impl == 1)
+  if (ctx->impl != 0)
     SOD_TRY(launch_pack_i8(ctx, dsrc, dtype, n, db));
   else if (db)
     SOD_TRY(launch_pack_db(ctx, dsrc, dtype, n));
@@ -240,7 +240,7 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq, const
 int sod_match_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
-  SOD_TRY(ctx->impl == 1 ? launch_match_i8(ctx) : launch_match(ctx));
+  SOD_TRY(ctx->impl != 0 ? launch_match_i8(ctx) : launch_match(ctx));
   ctx->matched = true;
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
@@ -248,7 +248,8 @@ int sod_match_enqueue(sod_ctx* ctx) {
 
 int sod_match_set_impl(sod_ctx* ctx, int impl) {
   SOD_TRY(set_dev(ctx));
-  if (impl != 0 && impl != 1) return sod_fail(ctx, SOD_EINVAL, "impl must be 0 (bf16) or 1 (int8)");
+  if (impl < 0 || impl > 2)
+    return sod_fail(ctx, SOD_EINVAL, "impl must be 0 (bf16), 1 (int8 16x16x64) or 2 (int8 32x32x32)");
   if (impl != ctx->impl) {  // packed operands differ: uploads must be repeated
     ctx->impl = impl;
     ctx->nsub = 0;
@@ -263,7 +264,7 @@ int sod_match_allgather_enqueue(sod_ctx* ctx) {
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
   if (ctx->nranks <= 1) return SOD_OK;
   if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
-  const size_t nq_pad = (size_t)ctx->nqt * kSubRows;
+  const size_t nq_pad = (size_t)sod_nq_pad(ctx);
   const size_t tot = nq_pad * ctx->nranks;
   SOD_TRY(sod_reserve(ctx, ctx->gd1, tot));
   SOD_TRY(sod_reserve(ctx, ctx->gd2, tot));

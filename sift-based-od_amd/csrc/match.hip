@@ -420,7 +420,7 @@ int launch_match(sod_ctx* ctx) {
 
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2, int nparts,
                  int64_t stride) {
-  const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
+  const int64_t nq_pad = sod_nq_pad(ctx);
   const int bs = 256;
   hipLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, bs)), dim3(bs), 0, ctx->stream,
                      d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p, ctx->cd2.p);

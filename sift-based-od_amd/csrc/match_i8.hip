@@ -41,7 +41,7 @@ constexpr int kPadNormI = 1 << 30;                        // ||d'||^2 of padding
 static_assert(kStageBytes / 1024 % NW == 0, "pieces split evenly");
 
 // pack: one thread per (row, 16-dim chunk c = 0..7); int8 of (value - 128); exact i32 norm
-template <typename TIn>
+template <typename TIn, bool kWide>
 __global__ void pack_i8_kernel(const TIn* __restrict__ src, int64_t n, int64_t npad,
                                uint8_t* __restrict__ pack, int* __restrict__ norms, int padnorm,
                                uint32_t* __restrict__ flags, int max_slot) {
@@ -90,9 +90,12 @@ __global__ void pack_i8_kernel(const TIn* __restrict__ src, int64_t n, int64_t n
     ss += __shfl_xor(ss, m, 8);
     raw += __shfl_xor(raw, m, 8);
   }
-  const int64_t sub = row >> 4;
-  const int rr = (int)(row & 15);
-  const int64_t off = sub * kSub + (c >> 2) * 1024 + (rr + 16 * (c & 3)) * 16;
+  int64_t off;
+  if constexpr (kWide) {   // 32-row subtiles for 32x32x32: [kstep 4][lane 64][16 B]
+    off = (row >> 5) * 4096 + (c >> 1) * 1024 + ((row & 31) + 32 * (c & 1)) * 16;
+  } else {                 // 16-row subtiles for 16x16x64: [kstep 2][lane 64][16 B]
+    off = (row >> 4) * kSub + (c >> 2) * 1024 + ((row & 15) + 16 * (c & 3)) * 16;
+  }
   *reinterpret_cast<uint4*>(pack + off) = make_uint4(o[0], o[1], o[2], o[3]);
   if (c == 0) {
     // DB rows: w = -||d'||^2 (padding: -2^30); queries: +||q'||^2 (padding: 0)
@@ -131,12 +134,82 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
   }
 }
 
+#ifndef SOD_I8_RING
+#define SOD_I8_RING 3      // LDS stage slots (prefetch distance = RING - 1 stages)
+#endif
+#ifndef SOD_I8_PIPE
+#define SOD_I8_PIPE 1      // prefilter subtile u while the MFMAs of subtile u+1 run
+#endif
+#ifndef SOD_SHARED_T
+#define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
+#endif
+constexpr int kRing = SOD_I8_RING;
+constexpr int kLoadsPerStage = kPiecesPerWave + 1;   // vm instructions per wave per stage
+
+// Top-2 VALUES of {a, partner lane's a} for the lane pairs (l, l^32) / (l, l^16):
+// v_permlane32_swap / v_permlane16_swap of a register with itself leaves {x_l, x_partner}
+// in the two results (in some order), so max / min of the pair need no lane select.
+__device__ __forceinline__ void top2_xor32(int& y1, int& y2) {
+  const auto p = __builtin_amdgcn_permlane32_swap((unsigned)y1, (unsigned)y1, false, false);
+  const auto q = __builtin_amdgcn_permlane32_swap((unsigned)y2, (unsigned)y2, false, false);
+  const int a = (int)p[0], b = (int)p[1];
+  y1 = max(a, b);
+  y2 = max(max(min(a, b), (int)q[0]), (int)q[1]);
+}
+__device__ __forceinline__ void top2_xor16(int& y1, int& y2) {
+  const auto p = __builtin_amdgcn_permlane16_swap((unsigned)y1, (unsigned)y1, false, false);
+  const auto q = __builtin_amdgcn_permlane16_swap((unsigned)y2, (unsigned)y2, false, false);
+  const int a = (int)p[0], b = (int)p[1];
+  y1 = max(a, b);
+  y2 = max(max(min(a, b), (int)q[0]), (int)q[1]);
+}
+
+// prefilter + exact top-2 update of one 16x16 tile set (see the file comment).  Each lane
+// keeps the exact top-2 (with index) of ITS rows; the prefilter threshold is the query's
+// second-best value over all four lane groups (lanes l, l^16, l^32, l^48), which every
+// row of the final top-2 reaches (>=, so ties keep their lowest-index winner).
+__device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 w, int rowb,
+                                            int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
+                                            int (&id)[QT]) {
+  uint64_t hit[QT];
+  uint64_t any = 0;
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int m = max(max(acc[t][0], acc[t][1]), max(acc[t][2], acc[t][3]));
+    hit[t] = __builtin_amdgcn_ballot_w64(m >= t2[t]);
+    any |= hit[t];
+  }
+  if (any) {
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      if (hit[t]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int y = 2 * acc[t][r] + (w[r] & 1);
+          const bool gt = y > y1[t];
+          y2[t] = max(min(y1[t], y), y2[t]);   // med3(y1, y2, y) with y1 >= y2
+          id[t] = gt ? rowb + r : id[t];
+          y1[t] = gt ? y : y1[t];
+        }
+#if SOD_SHARED_T
+        int g1 = y1[t], g2 = y2[t];
+        top2_xor32(g1, g2);
+        top2_xor16(g1, g2);
+        t2[t] = g2 >> 1;
+#else
+        t2[t] = y2[t] >> 1;
+#endif
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStageSlot];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageSlot];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int sp = blockIdx.x % split;
   const int qb = blockIdx.x / split;
@@ -145,7 +218,9 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / SPS;
 
-  if (nst > 0) issue_stage(dbpack, dn, s_lo, lds, wave, lane);
+#pragma unroll
+  for (int j = 0; j < kRing - 1; ++j)
+    if (j < nst) issue_stage(dbpack, dn, s_lo + j * SPS, lds + j * kStageSlot, wave, lane);
 
   i32x4 bq[QT][2];
 #pragma unroll
@@ -164,12 +239,33 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
     t2[t] = INT_MIN >> 1;
     id[t] = 0x7fffffff;
   }
+  const int rowl = row_offset + (int)(s_lo * kSubRows) + (lane >> 4) * 4;
+#if SOD_I8_PIPE
+  // accumulators, norms and first row of the subtile whose prefilter is pending; the
+  // initial "previous subtile" is empty (h = INT_MIN can never pass t2)
+  i32x4 accp[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) accp[t] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
+  i32x4 wp = {0, 0, 0, 0};
+  int rowp = 0;
+#endif
 
+  int slot = 0;
   for (int64_t s = 0; s < nst; ++s) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the wave's loads of stage s are complete when at most the later prefetched stages'
+    // loads remain in flight (vector memory returns in order)
+    if (kRing == 3 && s + 1 < nst)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLoadsPerStage) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (s + 1 < nst) issue_stage(dbpack, dn, s_lo + (s + 1) * SPS, lds + ((s + 1) & 1) * kStageSlot, wave, lane);
-    const uint8_t* sb = lds + (s & 1) * kStageSlot;
+    // every wave has finished stage s-1, so its slot takes stage s+kRing-1
+    if (s + kRing - 1 < nst) {
+      const int ns = slot == 0 ? kRing - 1 : slot - 1;
+      issue_stage(dbpack, dn, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageSlot, wave, lane);
+    }
+    const uint8_t* sb = lds + slot * kStageSlot;
+    slot = slot + 1 == kRing ? 0 : slot + 1;
     i32x4 fa0 = *reinterpret_cast<const i32x4*>(sb + lane * 16);
     i32x4 fa1 = *reinterpret_cast<const i32x4*>(sb + 1024 + lane * 16);
     i32x4 fw = *reinterpret_cast<const i32x4*>(sb + kStageBytes + (lane >> 4) * 16);
@@ -190,34 +286,21 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
 #pragma unroll
       for (int t = 0; t < QT; ++t)
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq[t][1], acc[t], 0, 0, 0);
-      // prefilter on h: a row can beat y2 only if h >= floor(y2 / 2)
-      bool hit[QT];
-      bool any = false;
+      const int rowb = rowl + (int)((s * SPS + u) * kSubRows);
+#if SOD_I8_PIPE
+      tile_update(accp, wp, rowp, y1, y2, t2, id);
 #pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        const int m = max(max(acc[t][0], acc[t][1]), max(acc[t][2], acc[t][3]));
-        hit[t] = m >= t2[t];
-        any |= hit[t];
-      }
-      if (__any(any)) {
-        const int rowb = row_offset + (int)((s_lo + s * SPS + u) * kSubRows) + (lane >> 4) * 4;
-#pragma unroll
-        for (int t = 0; t < QT; ++t) {
-          if (__any(hit[t])) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int y = 2 * acc[t][r] + (w[r] & 1);
-              const bool gt = y > y1[t];
-              y2[t] = max(min(y1[t], y), y2[t]);   // med3(y1, y2, y) with y1 >= y2
-              id[t] = gt ? rowb + r : id[t];
-              y1[t] = gt ? y : y1[t];
-            }
-            t2[t] = y2[t] >> 1;
-          }
-        }
-      }
+      for (int t = 0; t < QT; ++t) accp[t] = acc[t];
+      wp = w;
+      rowp = rowb;
+#else
+      tile_update(acc, w, rowb, y1, y2, t2, id);
+#endif
     }
   }
+#if SOD_I8_PIPE
+  tile_update(accp, wp, rowp, y1, y2, t2, id);
+#endif
 
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
@@ -239,23 +322,185 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 32x32x32 variant: lane l owns query l&31 and 16 rows (reg r -> row (r&3) + 8(r>>2) +
+// 4(l>>5)) of each 32-row subtile.  An MFMA of this shape holds the SIMD's issue port for
+// 8 of its 32 cycles (vs 8 of 16 for 16x16x64), and the prefilter reduces 16 values per
+// lane per tile, so the instruction stream leaves room beside the matrix pipe.
+namespace w {
+constexpr int QT = 4;            // 32-query tiles per wave (128 queries)
+constexpr int SPS = 4;           // 32-row subtiles per stage (128 rows)
+constexpr int kSub = 4096;
+constexpr int kStageBytes = SPS * kSub;          // 16 KiB
+constexpr int kStageNorm = SPS * 32 * 4;         // 512 B
+constexpr int kStageSlot = kStageBytes + kStageNorm;
+constexpr int kPiecesPerWave = kStageBytes / 1024 / NW;
+constexpr int kNormLanes = kStageNorm / 16 / NW;
+}  // namespace w
+
+typedef __attribute__((ext_vector_type(16))) int i32x16;
+
+__device__ __forceinline__ void issue_stage_w(const uint8_t* __restrict__ dbpack,
+                                              const int* __restrict__ dn, int64_t sub0,
+                                              uint8_t* slot, int wave, int lane) {
+  const uint8_t* src = dbpack + sub0 * w::kSub;
+#pragma unroll
+  for (int j = 0; j < w::kPiecesPerWave; ++j) {
+    const int piece = wave * w::kPiecesPerWave + j;
+    glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
+  }
+  const int* nsrc = dn + sub0 * 32 + wave * (w::kNormLanes * 4) + lane * 4;
+  if (lane < w::kNormLanes) glds16(nsrc, slot + w::kStageBytes + wave * (w::kNormLanes * 16));
+}
+
+__global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
+    const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
+    const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
+    int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
+    int* __restrict__ pidx, float* __restrict__ pd2) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * w::kStageSlot];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sp = blockIdx.x % split;
+  const int qb = blockIdx.x / split;
+  const int qt0 = (qb * NW + wave) * w::QT;
+  const int64_t s_lo = (int64_t)sp * sub_per_split;
+  const int64_t s_hi = min(nsub, s_lo + sub_per_split);
+  const int64_t nst = (s_hi - s_lo) / w::SPS;
+  const int h = lane >> 5;
+
+  if (nst > 0) issue_stage_w(dbpack, dn, s_lo, lds, wave, lane);
+
+  i32x4 bq[w::QT][4];
+#pragma unroll
+  for (int t = 0; t < w::QT; ++t)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int qt = qt0 + t;
+      bq[t][k] = qt < nqt ? *reinterpret_cast<const i32x4*>(qpack + ((int64_t)qt * 4 + k) * 1024 + lane * 16)
+                          : i32x4{0, 0, 0, 0};
+    }
+  int y1[w::QT], y2[w::QT], t2[w::QT], id[w::QT];
+#pragma unroll
+  for (int t = 0; t < w::QT; ++t) {
+    y1[t] = INT_MIN;
+    y2[t] = INT_MIN;
+    t2[t] = INT_MIN >> 1;
+    id[t] = 0x7fffffff;
+  }
+
+  for (int64_t s = 0; s < nst; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nst)
+      issue_stage_w(dbpack, dn, s_lo + (s + 1) * w::SPS, lds + ((s + 1) & 1) * w::kStageSlot, wave, lane);
+    const uint8_t* sb = lds + (s & 1) * w::kStageSlot;
+    i32x4 fa[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) fa[k] = *reinterpret_cast<const i32x4*>(sb + k * 1024 + lane * 16);
+#pragma unroll
+    for (int u = 0; u < w::SPS; ++u) {
+      i32x4 a[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = fa[k];
+      // w = -||d'||^2 of the lane's 16 rows: rows 8g + 4h + i -> 4 x 16 B
+      const int* wp = reinterpret_cast<const int*>(sb + w::kStageBytes + u * 128);
+      i32x16 c;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const i32x4 wv = *reinterpret_cast<const i32x4*>(wp + 8 * g + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[4 * g + i] = wv[i] >> 1;   // floor(-||d'||^2 / 2)
+      }
+      i32x16 acc[w::QT];
+#pragma unroll
+      for (int t = 0; t < w::QT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], bq[t][0], c, 0, 0, 0);
+      if (u + 1 < w::SPS) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          fa[k] = *reinterpret_cast<const i32x4*>(sb + (u + 1) * w::kSub + k * 1024 + lane * 16);
+      }
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+#pragma unroll
+        for (int t = 0; t < w::QT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], bq[t][k], acc[t], 0, 0, 0);
+      bool hit[w::QT];
+      bool any = false;
+#pragma unroll
+      for (int t = 0; t < w::QT; ++t) {
+        int m = acc[t][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = max(m, acc[t][r]);
+        hit[t] = m >= t2[t];
+        any |= hit[t];
+      }
+      if (__any(any)) {
+        const int rowb = row_offset + (int)((s_lo + s * w::SPS + u) * 32) + 4 * h;
+#pragma unroll
+        for (int t = 0; t < w::QT; ++t) {
+          if (__any(hit[t])) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const i32x4 wv = *reinterpret_cast<const i32x4*>(wp + 8 * g + 4 * h);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int y = 2 * acc[t][4 * g + i] + (wv[i] & 1);
+                const bool gt = y > y1[t];
+                y2[t] = max(min(y1[t], y), y2[t]);
+                id[t] = gt ? rowb + 8 * g + i : id[t];
+                y1[t] = gt ? y : y1[t];
+              }
+            }
+#if SOD_SHARED_T
+            int g1 = y1[t], g2 = y2[t];
+            top2_xor32(g1, g2);
+            t2[t] = g2 >> 1;
+#else
+            t2[t] = y2[t] >> 1;
+#endif
+          }
+        }
+      }
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < w::QT; ++t) {
+    const int o1 = __shfl_xor(y1[t], 32), oi = __shfl_xor(id[t], 32), o2 = __shfl_xor(y2[t], 32);
+    merge2i(y1[t], id[t], y2[t], o1, oi, o2);
+    const int qt = qt0 + t;
+    if (lane < 32 && qt < nqt) {
+      const int64_t q = (int64_t)qt * 32 + lane;
+      const int n2 = qn[q];
+      const int64_t o = (int64_t)sp * nq_pad + q;
+      pd1[o] = y1[t] < -(1 << 29) ? 3.0e38f : (float)(n2 - y1[t]);
+      pidx[o] = id[t];
+      pd2[o] = y2[t] < -(1 << 29) ? 3.0e38f : (float)(n2 - y2[t]);
+    }
+  }
+}
+
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace
 
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db) {
-  const int64_t npad = db ? cdiv(n, SPS * kSubRows) * SPS * kSubRows : cdiv(n, kSubRows) * kSubRows;
+  const bool wide = ctx->impl == 2;
+  const int rows = wide ? 32 : kSubRows;            // rows per subtile / queries per tile
+  const int sub_bytes = wide ? w::kSub : kSub;
+  const int64_t npad = db ? cdiv(n, 128) * 128 : cdiv(n, rows) * rows;
   uint8_t* pack;
   int* norms;
   if (db) {
-    ctx->nsub = npad / kSubRows;
-    SOD_TRY(sod_reserve(ctx, ctx->dbpack, (size_t)ctx->nsub * kSub));
+    ctx->nsub = npad / rows;
+    SOD_TRY(sod_reserve(ctx, ctx->dbpack, (size_t)ctx->nsub * sub_bytes));
     SOD_TRY(sod_reserve(ctx, ctx->dn, (size_t)npad));
     pack = ctx->dbpack.p;
     norms = reinterpret_cast<int*>(ctx->dn.p);
   } else {
-    ctx->nqt = (int32_t)(npad / kSubRows);
-    SOD_TRY(sod_reserve(ctx, ctx->qpack, (size_t)ctx->nqt * kSub));
+    ctx->nqt = (int32_t)(npad / rows);
+    SOD_TRY(sod_reserve(ctx, ctx->qpack, (size_t)ctx->nqt * sub_bytes));
     SOD_TRY(sod_reserve(ctx, ctx->qn, (size_t)npad));
     pack = ctx->qpack.p;
     norms = reinterpret_cast<int*>(ctx->qn.p);
@@ -265,20 +510,27 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   const unsigned grid = (unsigned)cdiv(threads, bs);
   const int padnorm = db ? kPadNormI : 0;
   const int slot = db ? 1 : 2;
-  if (dtype == SOD_DTYPE_U8)
-    hipLaunchKernelGGL(pack_i8_kernel<uint8_t>, dim3(grid), dim3(bs), 0, ctx->stream,
-                       (const uint8_t*)dsrc, n, npad, pack, norms, padnorm, ctx->flags.p, slot);
-  else
-    hipLaunchKernelGGL(pack_i8_kernel<float>, dim3(grid), dim3(bs), 0, ctx->stream,
-                       (const float*)dsrc, n, npad, pack, norms, padnorm, ctx->flags.p, slot);
+#define SOD_PACK(T, W)                                                                     \
+  hipLaunchKernelGGL((pack_i8_kernel<T, W>), dim3(grid), dim3(bs), 0, ctx->stream,         \
+                     (const T*)dsrc, n, npad, pack, norms, padnorm, ctx->flags.p, slot)
+  if (dtype == SOD_DTYPE_U8) {
+    if (wide) SOD_PACK(uint8_t, true); else SOD_PACK(uint8_t, false);
+  } else {
+    if (wide) SOD_PACK(float, true); else SOD_PACK(float, false);
+  }
+#undef SOD_PACK
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
 
 int launch_match_i8(sod_ctx* ctx) {
-  const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
-  const int64_t qblocks = cdiv(ctx->nqt, NW * QT);
-  const int64_t nstages = ctx->nsub / SPS;
+  const bool wide = ctx->impl == 2;
+  const int rows = wide ? 32 : kSubRows;
+  const int sps = wide ? w::SPS : SPS;
+  const int qt_per_wg = NW * (wide ? w::QT : QT);
+  const int64_t nq_pad = (int64_t)ctx->nqt * rows;
+  const int64_t qblocks = cdiv(ctx->nqt, qt_per_wg);
+  const int64_t nstages = ctx->nsub / sps;
   const int64_t target = 2LL * ctx->num_cus;
   int64_t split = std::max<int64_t>(1, (target + qblocks / 2) / qblocks);
   split = std::min<int64_t>(split, nstages);
@@ -292,10 +544,18 @@ int launch_match_i8(sod_ctx* ctx) {
   SOD_TRY(sod_reserve(ctx, ctx->cd2, (size_t)nq_pad));
   SOD_TRY(sod_reserve(ctx, ctx->cidx, (size_t)nq_pad));
   SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
-  hipLaunchKernelGGL(match_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(NT), 0, ctx->stream,
-                     ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub, ctx->qpack.p,
-                     reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad, (int)split,
-                     st_per_split * SPS, (int)ctx->row_offset, ctx->pd1.p, ctx->pidx.p, ctx->pd2.p);
+  if (wide)
+    hipLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(NT), 0, ctx->stream,
+                       ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,
+                       ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,
+                       (int)split, st_per_split * sps, (int)ctx->row_offset, ctx->pd1.p,
+                       ctx->pidx.p, ctx->pd2.p);
+  else
+    hipLaunchKernelGGL(match_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(NT), 0, ctx->stream,
+                       ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,
+                       ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,
+                       (int)split, st_per_split * sps, (int)ctx->row_offset, ctx->pd1.p,
+                       ctx->pidx.p, ctx->pd2.p);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
   return launch_merge(ctx, ctx->pd1.p, ctx->pidx.p, ctx->pd2.p, (int)split, nq_pad);

@@ -31,7 +31,7 @@ struct sod_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   int num_cus = 256;
-  int impl = 0;                 // matcher: 0 = bf16 MFMA (match.hip), 1 = int8 MFMA (match_i8.hip)
+  int impl = 0;                 // matcher: 0 = bf16 MFMA (match.hip), 1/2 = int8 MFMA 16x16x64 / 32x32x32 (match_i8.hip)
 
   // ---- database (keypoints replicated, descriptors = shard) ----
   int64_t n_total = 0;          // keypoints in the whole DB
@@ -48,7 +48,7 @@ struct sod_ctx {
 
   // ---- query ----
   int32_t nq = 0;
-  int32_t nqt = 0;              // 16-query tiles
+  int32_t nqt = 0;              // query tiles (16 queries; 32 for impl 2)
   DevBuf<uint8_t> qpack;        // nqt * 4096
   DevBuf<float> qn;             // nqt * 16
   DevBuf<float> qx, qy, qang;
@@ -154,6 +154,8 @@ void sod_release(DevBuf<T>& b) {
 }
 
 // kernel launchers implemented in the .hip files ----------------------------------------
+// queries covered by the packed query tiles (tile height depends on the matcher)
+inline int64_t sod_nq_pad(const sod_ctx* ctx) { return (int64_t)ctx->nqt * (ctx->impl == 2 ? 32 : kSubRows); }
 int launch_pack_db(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n);
 int launch_pack_queries(sod_ctx* ctx, const void* dsrc, int dtype, int32_t nq);
 int launch_match(sod_ctx* ctx);

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 CASES = ["c1_b15", "planted_b15", "planted_b12"]
 AFFINE_ATOL = 1e-4
-IMPLS = ["bf16", "i8"]
+IMPLS = ["bf16", "i8", "i8w"]
 
 
 def load_case(ctx, g):

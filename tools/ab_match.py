@@ -34,7 +34,7 @@ for i in range(12):
         ts.append(ctx.last_match_ms())
 ts = np.array(ts)
 tf = 256.0 * nq * len(db) / (ts.mean() / 1e3) / 1e12
-peak = 2500.0 if impl == "bf16" else 5000.0
+peak = 2500.0 if impl == "bf16" else 5000.0   # dense bf16 / int8 MFMA peaks
 print("%s [%s]: match %.3f ms (min %.3f)  %.0f T(FL)OP/s  frac %.3f  %.3g pairs/s" % (
     os.path.basename(_lib.LIB_PATH), impl, ts.mean(), ts.min(), tf, tf / peak,
     nq * len(db) / (ts.mean() / 1e3)), flush=True)

@@ -73,6 +73,35 @@ static int test32() {
   return bad ? 1 : 0;
 }
 
+// v_permlane32_swap / v_permlane16_swap of a register with itself: the two results hold
+// {x_l, x_(l^32)} / {x_l, x_(l^16)} (the shared-threshold reduction in match_i8.hip)
+__global__ void kswap(int* o) {
+  const unsigned x = threadIdx.x * 7u + 3u;
+  const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  const auto q = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  const unsigned l = threadIdx.x;
+  const unsigned e32 = (l ^ 32) * 7u + 3u, e16 = (l ^ 16) * 7u + 3u;
+  const bool ok32 = (p[0] == x && p[1] == e32) || (p[0] == e32 && p[1] == x);
+  const bool ok16 = (q[0] == x && q[1] == e16) || (q[0] == e16 && q[1] == x);
+  o[l] = (ok32 ? 0 : 1) | (ok16 ? 0 : 2);
+}
+
+static int test_swap() {
+  int* d;
+  int h[64];
+  if (hipMalloc(&d, sizeof h)) return 2;
+  hipLaunchKernelGGL(kswap, dim3(1), dim3(64), 0, 0, d);
+  if (hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost)) return 2;
+  int b32 = 0, b16 = 0;
+  for (int i = 0; i < 64; ++i) {
+    b32 += h[i] & 1;
+    b16 += (h[i] >> 1) & 1;
+  }
+  printf("permlane32_swap pair hypothesis: %s (%d/64)\n", b32 ? "WRONG" : "OK", b32);
+  printf("permlane16_swap pair hypothesis: %s (%d/64)\n", b16 ? "WRONG" : "OK", b16);
+  return (b32 || b16) ? 1 : 0;
+}
+
 int main() {
   signed char hA[16 * 64], hB[64 * 16];
   int ref[16 * 16], got[16 * 16];
@@ -95,5 +124,5 @@ int main() {
   int bad = 0;
   for (int i = 0; i < 256; ++i) bad += got[i] != ref[i];
   printf("i8 16x16x64 layout hypothesis H: %s (%d/256 mismatches)\n", bad ? "WRONG" : "OK", bad);
-  return (bad ? 1 : 0) | test32();
+  return (bad ? 1 : 0) | test32() | test_swap();
 }

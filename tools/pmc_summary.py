@@ -2,25 +2,28 @@
 profiles/: per-launch averages, HBM bytes = 2*FETCH_SIZE*1024 (gfx950 reports half of a
 wide coalesced stream, MI355X_MICROARCH.md §HBM) + WRITE_SIZE*1024, the effective clock
 GRBM_GUI_ACTIVE/8/t and the MFMA-busy fraction.
-    python tools/pmc_summary.py gpurun_out/pmc_c3 profiles/r01_pmc_match_c3.json <kernel_ms>"""
+    python tools/pmc_summary.py gpurun_out/pmc_<kernel>_c3 profiles/r01_pmc_<kernel>_c3.json \
+        <kernel_ms> <kernel>"""
 import collections
 import csv
 import json
 import os
+import re
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
-kernel_ms = float(sys.argv[3]) if len(sys.argv) > 3 else None
+kernel_ms = float(sys.argv[3]) if len(sys.argv) > 3 and sys.argv[3] != "-" else None
+kernel = sys.argv[4] if len(sys.argv) > 4 else "match_i8_kernel"
 vals = collections.defaultdict(list)
 for sub in sorted(os.listdir(src)):
     f = os.path.join(src, sub, "pmc_counter_collection.csv")
     if not os.path.exists(f):
         continue
     for r in csv.DictReader(open(f)):
-        if "match_kernel" in r["Kernel_Name"]:
+        if re.search(r"(^|::|\s)%s\b" % kernel, r["Kernel_Name"]):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 avg = {k: sum(v) / len(v) for k, v in vals.items()}
-out = {"kernel": "match_kernel", "counters_per_launch": avg}
+out = {"kernel": kernel, "counters_per_launch": avg}
 if "FETCH_SIZE" in avg:
     out["hbm_read_bytes"] = 2 * avg["FETCH_SIZE"] * 1024
 if "WRITE_SIZE" in avg:
