@@ -6,7 +6,8 @@
 // The MFMA accumulates q'.d' exactly in i32 (|q'.d'| <= 2^21).  Minimising the distance
 // is maximising y = 2 q'.d' - ||d'||^2; -2 does not fit the int8 operands, so the row
 // norm is folded into the accumulator init as c = floor(-||d'||^2 / 2) (w = -||d'||^2 is
-// stored per row; c = w >> 1).  The MFMA then yields h = q'.d' + c and y = 2h + (w & 1):
+// stored per row as c = w >> 1 and its parity p = w & 1).  The MFMA then yields
+// h = q'.d' + c and y = 2h + p:
 // ordering by y is ordering by h with the parity bit as tiebreak, and max(h) >=
 // floor(y2 / 2) is a NECESSARY condition for a row to beat the running second best y2 --
 // so the fast path needs no per-element op (3 VALU per 16x16 tile, like the bf16 path).
@@ -33,10 +34,10 @@ constexpr int NT = NW * 64;
 constexpr int SPS = 8;         // subtiles per stage (128 rows)
 constexpr int kSub = 2048;     // bytes per 16-row subtile
 constexpr int kStageBytes = SPS * kSub;          // 16 KiB
-constexpr int kStageNorm = SPS * kSubRows * 4;   // 512 B of i32 norms
+// per stage (128 rows) and wave w (rows 32w..32w+31): [c: 32 x i32 | p: 32 x i32]
+constexpr int kStageNorm = 2 * SPS * kSubRows * 4;   // 1 KiB
 constexpr int kStageSlot = kStageBytes + kStageNorm;
 constexpr int kPiecesPerWave = kStageBytes / 1024 / NW;   // 4
-constexpr int kNormLanes = kStageNorm / 16 / NW;          // 8
 constexpr int kPadNormI = 1 << 30;                        // ||d'||^2 of padding rows (w = -2^30)
 static_assert(kStageBytes / 1024 % NW == 0, "pieces split evenly");
 
@@ -98,8 +99,14 @@ __global__ void pack_i8_kernel(const TIn* __restrict__ src, int64_t n, int64_t n
   }
   *reinterpret_cast<uint4*>(pack + off) = make_uint4(o[0], o[1], o[2], o[3]);
   if (c == 0) {
-    // DB rows: w = -||d'||^2 (padding: -2^30); queries: +||q'||^2 (padding: 0)
-    norms[row] = (row < n) ? (padnorm ? -ss : ss) : -padnorm;
+    if (padnorm) {
+      // DB rows: w = -||d'||^2 (padding: -2^30) as c = w >> 1 and p = w & 1 (npad apart)
+      const int w = (row < n) ? -ss : -padnorm;
+      norms[row] = w >> 1;
+      norms[npad + row] = w & 1;
+    } else {
+      norms[row] = ss;   // queries: +||q'||^2 (padding: 0)
+    }
     // raw ||v||^2 (as float bits, like match.hip) for sod_match_exact_order
     if (row < n) atomicMax(&flags[max_slot], __float_as_uint((float)raw));
   }
@@ -110,8 +117,16 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* lds_base) {
   __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_base, 16, 0, 0);
 }
 
+// norms of the stage's 128 rows: wave w's lanes 0-7 fetch c, lanes 8-15 parity, of rows
+// 32w..32w+31 (one 256-B run per wave: global_load_lds writes lane i at M0 + 16 i)
+__device__ __forceinline__ void issue_norms(const int* __restrict__ dn, int64_t npad, int64_t row0,
+                                            uint8_t* slot_norm, int wave, int lane) {
+  const int* src = dn + (lane < 8 ? 0 : npad) + row0 + wave * 32 + (lane & 7) * 4;
+  if (lane < 16) glds16(src, slot_norm + wave * 256);
+}
+
 __device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
-                                            const int* __restrict__ dn, int64_t sub0,
+                                            const int* __restrict__ dn, int64_t npad, int64_t sub0,
                                             uint8_t* slot, int wave, int lane) {
   const uint8_t* src = dbpack + sub0 * kSub;
 #pragma unroll
@@ -119,8 +134,19 @@ __device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
     const int piece = wave * kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  const int* nsrc = dn + sub0 * kSubRows + wave * (kNormLanes * 4) + lane * 4;
-  if (lane < kNormLanes) glds16(nsrc, slot + kStageBytes + wave * (kNormLanes * 16));
+  issue_norms(dn, npad, sub0 * kSubRows, slot + kStageBytes, wave, lane);
+}
+
+// LDS offset of a 16-row subtile's c (p at +128) for lane group g = lane >> 4
+__device__ __forceinline__ int norm_off(int u, int g) {
+  return kStageBytes + (u >> 1) * 256 + (u & 1) * 64 + g * 16;
+}
+
+// median of three (v_med3_i32): with y1 >= y2, med3(y1, y, y2) is the new second best
+__device__ __forceinline__ int imed3(int a, int b, int c) {
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
 }
 
 __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int oi, int o2) {
@@ -168,7 +194,7 @@ __device__ __forceinline__ void top2_xor16(int& y1, int& y2) {
 // keeps the exact top-2 (with index) of ITS rows; the prefilter threshold is the query's
 // second-best value over all four lane groups (lanes l, l^16, l^32, l^48), which every
 // row of the final top-2 reaches (>=, so ties keep their lowest-index winner).
-__device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 w, int rowb,
+__device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 p, int rowb,
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
                                             int (&id)[QT]) {
   uint64_t hit[QT];
@@ -185,9 +211,9 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 
       if (hit[t]) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int y = 2 * acc[t][r] + (w[r] & 1);
+          const int y = 2 * acc[t][r] | p[r];
           const bool gt = y > y1[t];
-          y2[t] = max(min(y1[t], y), y2[t]);   // med3(y1, y2, y) with y1 >= y2
+          y2[t] = imed3(y1[t], y, y2[t]);
           id[t] = gt ? rowb + r : id[t];
           y1[t] = gt ? y : y1[t];
         }
@@ -217,10 +243,11 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / SPS;
+  const int64_t npad = nsub * kSubRows;
 
 #pragma unroll
   for (int j = 0; j < kRing - 1; ++j)
-    if (j < nst) issue_stage(dbpack, dn, s_lo + j * SPS, lds + j * kStageSlot, wave, lane);
+    if (j < nst) issue_stage(dbpack, dn, npad, s_lo + j * SPS, lds + j * kStageSlot, wave, lane);
 
   i32x4 bq[QT][2];
 #pragma unroll
@@ -246,7 +273,7 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
   i32x4 accp[QT];
 #pragma unroll
   for (int t = 0; t < QT; ++t) accp[t] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
-  i32x4 wp = {0, 0, 0, 0};
+  i32x4 pp = {0, 0, 0, 0};
   int rowp = 0;
 #endif
 
@@ -262,17 +289,17 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
     // every wave has finished stage s-1, so its slot takes stage s+kRing-1
     if (s + kRing - 1 < nst) {
       const int ns = slot == 0 ? kRing - 1 : slot - 1;
-      issue_stage(dbpack, dn, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageSlot, wave, lane);
+      issue_stage(dbpack, dn, npad, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageSlot, wave, lane);
     }
     const uint8_t* sb = lds + slot * kStageSlot;
     slot = slot + 1 == kRing ? 0 : slot + 1;
     i32x4 fa0 = *reinterpret_cast<const i32x4*>(sb + lane * 16);
     i32x4 fa1 = *reinterpret_cast<const i32x4*>(sb + 1024 + lane * 16);
-    i32x4 fw = *reinterpret_cast<const i32x4*>(sb + kStageBytes + (lane >> 4) * 16);
+    i32x4 fc = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4));
+    i32x4 fp = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4) + 128);
 #pragma unroll
     for (int u = 0; u < SPS; ++u) {
-      const i32x4 a0 = fa0, a1 = fa1, w = fw;
-      const i32x4 c = {w[0] >> 1, w[1] >> 1, w[2] >> 1, w[3] >> 1};   // floor(-||d'||^2 / 2)
+      const i32x4 a0 = fa0, a1 = fa1, c = fc, p = fp;   // c = floor(-||d'||^2 / 2)
       i32x4 acc[QT];
 #pragma unroll
       for (int t = 0; t < QT; ++t)
@@ -281,25 +308,26 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
         const uint8_t* nb = sb + (u + 1) * kSub + lane * 16;
         fa0 = *reinterpret_cast<const i32x4*>(nb);
         fa1 = *reinterpret_cast<const i32x4*>(nb + 1024);
-        fw = *reinterpret_cast<const i32x4*>(sb + kStageBytes + (u + 1) * 64 + (lane >> 4) * 16);
+        fc = *reinterpret_cast<const i32x4*>(sb + norm_off(u + 1, lane >> 4));
+        fp = *reinterpret_cast<const i32x4*>(sb + norm_off(u + 1, lane >> 4) + 128);
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t)
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq[t][1], acc[t], 0, 0, 0);
       const int rowb = rowl + (int)((s * SPS + u) * kSubRows);
 #if SOD_I8_PIPE
-      tile_update(accp, wp, rowp, y1, y2, t2, id);
+      tile_update(accp, pp, rowp, y1, y2, t2, id);
 #pragma unroll
       for (int t = 0; t < QT; ++t) accp[t] = acc[t];
-      wp = w;
+      pp = p;
       rowp = rowb;
 #else
-      tile_update(acc, w, rowb, y1, y2, t2, id);
+      tile_update(acc, p, rowb, y1, y2, t2, id);
 #endif
     }
   }
 #if SOD_I8_PIPE
-  tile_update(accp, wp, rowp, y1, y2, t2, id);
+  tile_update(accp, pp, rowp, y1, y2, t2, id);
 #endif
 
 #pragma unroll
@@ -332,16 +360,15 @@ constexpr int QT = 4;            // 32-query tiles per wave (128 queries)
 constexpr int SPS = 4;           // 32-row subtiles per stage (128 rows)
 constexpr int kSub = 4096;
 constexpr int kStageBytes = SPS * kSub;          // 16 KiB
-constexpr int kStageNorm = SPS * 32 * 4;         // 512 B
+constexpr int kStageNorm = 2 * SPS * 32 * 4;     // c and p of 128 rows: 1 KiB
 constexpr int kStageSlot = kStageBytes + kStageNorm;
 constexpr int kPiecesPerWave = kStageBytes / 1024 / NW;
-constexpr int kNormLanes = kStageNorm / 16 / NW;
 }  // namespace w
 
 typedef __attribute__((ext_vector_type(16))) int i32x16;
 
 __device__ __forceinline__ void issue_stage_w(const uint8_t* __restrict__ dbpack,
-                                              const int* __restrict__ dn, int64_t sub0,
+                                              const int* __restrict__ dn, int64_t npad, int64_t sub0,
                                               uint8_t* slot, int wave, int lane) {
   const uint8_t* src = dbpack + sub0 * w::kSub;
 #pragma unroll
@@ -349,8 +376,7 @@ __device__ __forceinline__ void issue_stage_w(const uint8_t* __restrict__ dbpack
     const int piece = wave * w::kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  const int* nsrc = dn + sub0 * 32 + wave * (w::kNormLanes * 4) + lane * 4;
-  if (lane < w::kNormLanes) glds16(nsrc, slot + w::kStageBytes + wave * (w::kNormLanes * 16));
+  issue_norms(dn, npad, sub0 * 32, slot + w::kStageBytes, wave, lane);   // wave u: subtile u
 }
 
 __global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
@@ -367,8 +393,9 @@ __global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / w::SPS;
   const int h = lane >> 5;
+  const int64_t npad = nsub * 32;
 
-  if (nst > 0) issue_stage_w(dbpack, dn, s_lo, lds, wave, lane);
+  if (nst > 0) issue_stage_w(dbpack, dn, npad, s_lo, lds, wave, lane);
 
   i32x4 bq[w::QT][4];
 #pragma unroll
@@ -392,7 +419,7 @@ __global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (s + 1 < nst)
-      issue_stage_w(dbpack, dn, s_lo + (s + 1) * w::SPS, lds + ((s + 1) & 1) * w::kStageSlot, wave, lane);
+      issue_stage_w(dbpack, dn, npad, s_lo + (s + 1) * w::SPS, lds + ((s + 1) & 1) * w::kStageSlot, wave, lane);
     const uint8_t* sb = lds + (s & 1) * w::kStageSlot;
     i32x4 fa[4];
 #pragma unroll
@@ -402,14 +429,14 @@ __global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
       i32x4 a[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) a[k] = fa[k];
-      // w = -||d'||^2 of the lane's 16 rows: rows 8g + 4h + i -> 4 x 16 B
-      const int* wp = reinterpret_cast<const int*>(sb + w::kStageBytes + u * 128);
+      // c = floor(-||d'||^2 / 2) of the lane's 16 rows 8g + 4h + i (4 x 16 B); p at +128 B
+      const int* wp = reinterpret_cast<const int*>(sb + w::kStageBytes + u * 256);
       i32x16 c;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const i32x4 wv = *reinterpret_cast<const i32x4*>(wp + 8 * g + 4 * h);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) c[4 * g + i] = wv[i] >> 1;   // floor(-||d'||^2 / 2)
+        for (int i = 0; i < 4; ++i) c[4 * g + i] = wv[i];
       }
       i32x16 acc[w::QT];
 #pragma unroll
@@ -442,12 +469,12 @@ __global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
           if (__any(hit[t])) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              const i32x4 wv = *reinterpret_cast<const i32x4*>(wp + 8 * g + 4 * h);
+              const i32x4 pv = *reinterpret_cast<const i32x4*>(wp + 32 + 8 * g + 4 * h);
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
-                const int y = 2 * acc[t][4 * g + i] + (wv[i] & 1);
+                const int y = 2 * acc[t][4 * g + i] | pv[i];
                 const bool gt = y > y1[t];
-                y2[t] = max(min(y1[t], y), y2[t]);
+                y2[t] = imed3(y1[t], y, y2[t]);
                 id[t] = gt ? rowb + 8 * g + i : id[t];
                 y1[t] = gt ? y : y1[t];
               }
@@ -495,7 +522,7 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   if (db) {
     ctx->nsub = npad / rows;
     SOD_TRY(sod_reserve(ctx, ctx->dbpack, (size_t)ctx->nsub * sub_bytes));
-    SOD_TRY(sod_reserve(ctx, ctx->dn, (size_t)npad));
+    SOD_TRY(sod_reserve(ctx, ctx->dn, (size_t)(2 * npad)));   // c and parity
     pack = ctx->dbpack.p;
     norms = reinterpret_cast<int*>(ctx->dn.p);
   } else {
