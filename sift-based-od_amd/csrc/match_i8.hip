@@ -17,8 +17,18 @@
 // Layout (operand lane map verified on hardware, tools/mfma_i8_layout.hip): lane l holds
 // A[row l&15][k 16(l>>4)..+15] and B[k ..][col l&15]; D: col l&15, rows 4(l>>4)+r.  A 16-row
 // subtile is [kstep 2][lane 64][16 B] = 2 KiB (the LDS image is the HBM image).
-// Structure as match.hip: queries stationary in VGPRs (64 per lane for 128 queries),
-// 2-slot LDS-DMA ring of 128-row stages, prefilter + one uniform branch per subtile.
+// Structure (cf. match.hip): queries stationary in VGPRs (64 per lane for 128 queries per
+// wave), DB streamed through a 3-slot LDS-DMA ring of 128-row stages (prefetch distance 2,
+// one barrier per stage), c/p read per subtile.  The prefilter of subtile u runs while
+// the MFMAs of subtile u+1 are in flight (software pipeline: no MFMA->VALU stall), with
+// one ballot + scalar branch per subtile and per 16x16 tile.  Each lane keeps the exact
+// top-2 of its own rows; the threshold is the query's second best over its four lane
+// groups (permlane swaps), so a query's slow path fires about as often as its top-2 changes.
+// Work-groups are ordered XCD-aware: each XCD's L2 serves one or two DB chunks.
+// Measured and rejected (C3, same device): a persistent work-queue kernel (more chunks =
+// more top-2 restarts), a seeded threshold pre-pass (gain eaten by the pass), other
+// shifts than -128 (slower), the 32x32x32 shape (impl 2: lower clock held, kept as an
+// option).
 #include <climits>
 
 #include "sod_internal.h"
@@ -166,6 +176,9 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_PIPE
 #define SOD_I8_PIPE 1      // prefilter subtile u while the MFMAs of subtile u+1 run
 #endif
+#ifndef SOD_I8_XCD
+#define SOD_I8_XCD 1       // XCD-aware work-group -> (chunk, query block) order
+#endif
 #ifndef SOD_SHARED_T
 #define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
 #endif
@@ -230,15 +243,14 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 
   }
 }
 
-__global__ __launch_bounds__(NT, 2) void match_i8_kernel(
-    const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
-    const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
-    int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
+// One work unit: query block qb (NW*QT tiles) against DB chunk sp (sub_per_split subtiles),
+// writing the chunk's partial top-2 of every query to slot sp of pd1/pidx/pd2.
+__device__ __forceinline__ void match_unit(
+    uint8_t* lds, int sp, int qb, const uint8_t* __restrict__ dbpack, const int* __restrict__ dn,
+    int64_t nsub, const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt,
+    int64_t nq_pad, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageSlot];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int sp = blockIdx.x % split;
-  const int qb = blockIdx.x / split;
   const int qt0 = (qb * NW + wave) * QT;
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
@@ -348,6 +360,26 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
       pd2[o] = y2[t] < -(1 << 29) ? 3.0e38f : (float)(n2 - y2[t]);
     }
   }
+}
+
+__global__ __launch_bounds__(NT, 2) void match_i8_kernel(
+    const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
+    const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
+    int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
+    int* __restrict__ pidx, float* __restrict__ pd2, int nqb) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageSlot];
+#if SOD_I8_XCD
+  // XCD-aware order: blocks b, b+8, ... share an XCD (and its L2); give each such group a
+  // contiguous run of chunk-major units, so an XCD streams one or two DB chunks, in step,
+  // instead of all of them (bijective for any grid size; cdna_hip_programming.md T1)
+  const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = blockIdx.x % 8;
+  const unsigned u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blockIdx.x / 8;
+  match_unit(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
+             sub_per_split, row_offset, pd1, pidx, pd2);
+#else
+  match_unit(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
+             nq_pad, sub_per_split, row_offset, pd1, pidx, pd2);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -558,8 +590,10 @@ int launch_match_i8(sod_ctx* ctx) {
   const int64_t nq_pad = (int64_t)ctx->nqt * rows;
   const int64_t qblocks = cdiv(ctx->nqt, qt_per_wg);
   const int64_t nstages = ctx->nsub / sps;
-  const int64_t target = 2LL * ctx->num_cus;
-  int64_t split = std::max<int64_t>(1, (target + qblocks / 2) / qblocks);
+  // one round of 2 work-groups per CU: as few DB chunks as fill the chip (every chunk
+  // restarts each query's running top-2, so more chunks mean more slow-path updates)
+  const int64_t slots = 2LL * ctx->num_cus;
+  int64_t split = std::max<int64_t>(1, (slots + qblocks / 2) / qblocks);
   split = std::min<int64_t>(split, nstages);
   const int64_t st_per_split = cdiv(nstages, split);
   split = cdiv(nstages, st_per_split);
@@ -582,7 +616,7 @@ int launch_match_i8(sod_ctx* ctx) {
                        ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,
                        ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,
                        (int)split, st_per_split * sps, (int)ctx->row_offset, ctx->pd1.p,
-                       ctx->pidx.p, ctx->pd2.p);
+                       ctx->pidx.p, ctx->pd2.p, (int)qblocks);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
   return launch_merge(ctx, ctx->pd1.p, ctx->pidx.p, ctx->pd2.p, (int)split, nq_pad);

@@ -57,7 +57,7 @@ struct sod_ctx {
   DevBuf<float> stage_f32;
 
   // ---- matcher outputs ----
-  int split = 1;                // DB splits of the current launch
+  int split = 1;                // DB splits (chunks) of the current launch
   DevBuf<float> pd1, pd2;       // [split * nq_pad]
   DevBuf<int32_t> pidx;
   DevBuf<float> cd1, cd2;       // merged (this shard / after allgather: global)  [nq_pad]
