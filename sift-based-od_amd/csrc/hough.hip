@@ -14,7 +14,10 @@
 //                    atomics (deterministic)
 //   select_*         votes that are the first touch of a bin with >= thr votes, compacted
 //                    in ordinal order = dict insertion order of main.py:126
-//   members_kernel   one wave per valid bin collects its member queries in query order
+//   member_fill      per 256-query block: LDS sort of its (valid bin, query) votes, one
+//                    atomic per run reserves the run's slots in the bin's member list
+//   member_order     per bin: runs reordered by fill block = query order
+//   members_kernel   fallback for bins beyond the LDS cap: one wave scans the queries
 //   means_kernel     PoseBin running means, sequential per bin (PoseBin.py:19-43)
 //   affine_kernel    one wave per bin: decoupled 3x3 normal equations, pinv by Jacobi,
 //                    outlier rejection, fixed point (AffineParameters.py:89-160)
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __
 // A bin voted by many matches (a real object: thousands of votes) would serialise on one
 // global cursor, so each block of kFillQ queries first sorts its (valid bin, query) votes
 // in LDS: equal bins form runs and ONE atomicAdd per run reserves the run's slots.  Runs
-// land in arbitrary block order; member_sort_kernel restores query order per bin.
+// land in arbitrary block order; member_order_kernel restores query order per bin.
 constexpr int kFillQ = 256;                 // queries per block -> <= 4096 votes
 constexpr int kFillCap = kFillQ * 16;
 __global__ __launch_bounds__(256) void member_fill_kernel(
@@ -472,44 +475,78 @@ __global__ __launch_bounds__(256) void member_fill_kernel(
   (void)sh;
 }
 
-// members, step 2: sort each bin's members by query index (= vote order, main.py:91) with
-// a bitonic sort in LDS; bins larger than kSortCap are rebuilt by members_kernel (scan).
-// Also resets the bin -> valid index map for the next call.
-constexpr int kSortCap = 4096;
-__global__ __launch_bounds__(256) void member_sort_kernel(const uint32_t* __restrict__ scal,
-                                                          const uint32_t* __restrict__ vbin,
-                                                          const int64_t* __restrict__ voff,
-                                                          uint32_t* __restrict__ vidx,
-                                                          int32_t* __restrict__ members) {
-  __shared__ uint32_t key[kSortCap];
+// members, step 2: restore query order (= vote order, main.py:91) inside each bin.  After
+// member_fill a bin's list is a concatenation of runs, one per fill block, each sorted by
+// query, in arbitrary block order; fill blocks cover disjoint query ranges (block =
+// query / kFillQ), so ordering the RUNS by block id orders the list.  Per bin (one
+// work-group, LDS): run starts by a max-scan of head positions, run lengths tabulated by
+// block id, an exclusive scan of that table gives each run's destination, one scatter.
+// Bins with more than kOrderCap members (or more than kOrderCap fill blocks) are rebuilt
+// by members_kernel (scan).  Also resets the bin -> valid index map for the next call.
+constexpr int kOrderCap = 8192;
+constexpr int kOrderT = 256;
+constexpr int kOrderPer = kOrderCap / kOrderT;   // elements per thread in the scans
+
+// in-place exclusive (sum) / inclusive (max) scan of a[0..n), n <= kOrderCap, 256 threads
+template <bool kMax>
+__device__ void block_scan_lds(uint32_t* a, int n, uint32_t* part) {
+  const int t = threadIdx.x, i0 = t * kOrderPer;
+  uint32_t acc = 0;
+  for (int i = i0; i < i0 + kOrderPer && i < n; ++i) acc = kMax ? max(acc, a[i]) : acc + a[i];
+  part[t] = acc;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int k = 0; k < kOrderT; ++k) {
+      const uint32_t v = part[k];
+      part[k] = run;
+      run = kMax ? max(run, v) : run + v;
+    }
+  }
+  __syncthreads();
+  uint32_t run = part[t];
+  for (int i = i0; i < i0 + kOrderPer && i < n; ++i) {
+    const uint32_t v = a[i];
+    if (kMax) {
+      run = max(run, v);
+      a[i] = run;
+    } else {
+      a[i] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kOrderT) void member_order_kernel(const uint32_t* __restrict__ scal,
+                                                               const uint32_t* __restrict__ vbin,
+                                                               const int64_t* __restrict__ voff,
+                                                               int nblk,
+                                                               uint32_t* __restrict__ vidx,
+                                                               int32_t* __restrict__ members) {
+  __shared__ uint32_t key[kOrderCap];     // the bin's members as filled
+  __shared__ uint32_t start[kOrderCap];   // run start of each element
+  __shared__ uint32_t tab[kOrderCap];     // run length -> destination, by fill block
+  __shared__ uint32_t part[kOrderT];
   const int64_t V = scal[0];
   for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
     const int64_t a = voff[v];
     const int n = (int)(voff[v + 1] - a);
     if (threadIdx.x == 0) vidx[vbin[v]] = 0xFFFFFFFFu;
-    if (n <= 1 || n > kSortCap) continue;   // uniform over the workgroup
-    int p = 1;
-    while (p < n) p <<= 1;
-    for (int i = threadIdx.x; i < p; i += blockDim.x)
-      key[i] = i < n ? (uint32_t)members[a + i] : 0xFFFFFFFFu;
+    if (n <= 1 || n > kOrderCap || nblk > kOrderCap) continue;   // uniform over the group
+    for (int i = threadIdx.x; i < n; i += kOrderT) key[i] = (uint32_t)members[a + i];
+    for (int i = threadIdx.x; i < nblk; i += kOrderT) tab[i] = 0;
     __syncthreads();
-    for (int k = 2; k <= p; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = threadIdx.x; i < p; i += blockDim.x) {
-          const int l = i ^ j;
-          if (l > i) {
-            const uint32_t x = key[i], y = key[l];
-            const bool up = (i & k) == 0;
-            if ((x > y) == up) {
-              key[i] = y;
-              key[l] = x;
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    for (int i = threadIdx.x; i < n; i += blockDim.x) members[a + i] = (int32_t)key[i];
+    for (int i = threadIdx.x; i < n; i += kOrderT)
+      start[i] = (i == 0 || key[i] / kFillQ != key[i - 1] / kFillQ) ? (uint32_t)i : 0u;
+    __syncthreads();
+    block_scan_lds<true>(start, n, part);
+    for (int i = threadIdx.x; i < n; i += kOrderT)   // the run's last element records it
+      if (i == n - 1 || start[i + 1] != start[i]) tab[key[i] / kFillQ] = (uint32_t)i - start[i] + 1;
+    __syncthreads();
+    block_scan_lds<false>(tab, nblk, part);
+    for (int i = threadIdx.x; i < n; i += kOrderT)
+      members[a + tab[key[i] / kFillQ] + ((uint32_t)i - start[i])] = (int32_t)key[i];
     __syncthreads();
   }
 }
@@ -521,7 +558,7 @@ __global__ __launch_bounds__(256) void members_kernel(
     int64_t nq, const uint32_t* __restrict__ scal, const uint32_t* __restrict__ vbin,
     const int64_t* __restrict__ voff, const uint32_t* __restrict__ gcount,
     const uint32_t* __restrict__ gfirst, const uint32_t* __restrict__ basekey,
-    const uint32_t* __restrict__ vmask, Bins b, int32_t* __restrict__ members) {
+    const uint32_t* __restrict__ vmask, Bins b, int nblk, int32_t* __restrict__ members) {
   constexpr int U = 4;
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -531,7 +568,7 @@ __global__ __launch_bounds__(256) void members_kernel(
     const int bs_ = lb % b.s, bt_ = (lb / b.s) % b.t, by_ = (lb / (b.s * b.t)) % b.y,
               bx_ = lb / (b.s * b.t * b.y);
     const uint32_t need = gcount[lb];
-    if (need <= (uint32_t)kSortCap) continue;   // handled by fill + sort
+    if (need <= (uint32_t)kOrderCap && nblk <= kOrderCap) continue;   // fill + order
     const int64_t off = voff[v];
     uint32_t got = 0;
     for (int64_t q0 = gfirst[lb] >> 4; got < need && q0 < nq; q0 += 64 * U) {
@@ -901,14 +938,15 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
                      nq, ctx->basekey.p, ctx->vmask.p, ctx_bins(ctx), ctx->vidx.p, ctx->voff.p,
                      ctx->cursor.p, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(member_sort_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
-                     ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, ctx->vidx.p,
+  const int nblk = (int)cdiv(nq, kFillQ);
+  hipLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->num_cus * 2)), dim3(kOrderT), 0,
+                     ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, nblk, ctx->vidx.p,
                      ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   const int wg = std::max(1, ctx->num_cus * 4);
   hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
                      ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
-                     ctx->vmask.p, ctx_bins(ctx), ctx->members.p);
+                     ctx->vmask.p, ctx_bins(ctx), nblk, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(sod_reserve(ctx, ctx->mq, (size_t)ctx->mmax * 6));
   hipLaunchKernelGGL(means_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,

@@ -154,3 +154,26 @@ def test_hough_affine_edges(ctx, name):
     ctx.select(5)
     ctx.affine((shape[1], shape[0]), 128.0, 128.0, 4)
     _check_hough(ctx, g)
+
+
+def test_member_order_at_scale(ctx):
+    """Large bins (thousands of members from many 256-query fill blocks): every valid bin's
+    member list is in query order, holds exactly its vote count, and only good matches."""
+    db = synthetic.make_database(20, 1000, seed=0)
+    qs = synthetic.make_queries(40000, seed=5, db_seed=0, kp_per_image=1000, n_objects=2)
+    ctx.set_impl("i8")
+    ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
+    ctx.upload_db(db.des)
+    ctx.upload_queries(qs.des, qs.kp)
+    ctx.pipeline(qs.shape, (32, 32, 8, 12), ratio=0.75, vote_threshold=5, affine_threshold=4)
+    _, _, _, good = ctx.match_result()
+    v = ctx.valid_result()
+    off, mem = v["offsets"], v["members"]
+    sizes = np.diff(off)
+    assert sizes.max() > 1000                      # spans many fill blocks
+    assert np.array_equal(sizes, v["votes"])
+    assert good[mem].all()
+    for i in range(len(sizes)):
+        seg = mem[off[i]:off[i + 1]]
+        assert np.all(np.diff(seg) > 0), "bin %d members not in query order" % i
+    ctx.set_impl("bf16")
