@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256) void members_kernel(
 // rounds at every step, so each bin's chain is inherently sequential; but the six
 // quantities are independent chains and their inputs can be fetched in parallel first:
 // means_gather_kernel writes per-member SoA values (x, y, alpha, s, w, h), then
-// means_kernel runs one thread per (bin, quantity) streaming contiguous memory.
+// means_kernel runs one wave per bin (six quantity chains in lockstep).
 __global__ void means_gather_kernel(const uint32_t* __restrict__ scal,
                                     const int32_t* __restrict__ members,
                                     const double* __restrict__ pose, const int* __restrict__ idx1,
@@ -632,42 +632,63 @@ __global__ void recip_table_kernel(const uint32_t* __restrict__ scal, double* __
     rtab[i] = 1.0 / (double)(i + 1);
 }
 
-__global__ void means_kernel(const uint32_t* __restrict__ scal, const int64_t* __restrict__ voff,
-                             const double* __restrict__ mq, int64_t mstride,
-                             const double* __restrict__ rtab, double* __restrict__ means) {
+// One wave per valid bin; lanes 0-5 run the six quantity chains in lockstep (same n, same
+// 1/(n+1)).  All 64 lanes stage the next 64 members' inputs (coalesced) into LDS while the
+// chains run on the current batch, so a chain step is 5 dependent f64 ops and never a
+// memory wait.  Division r / d (d = n + 1) is RN(r * inv) corrected by one FMA residual
+// step (Markstein): with inv = RN(1/d) the result equals the correctly rounded r / d
+// (verified against r / d on 2e8 random cases).
+__global__ __launch_bounds__(64) void means_kernel(const uint32_t* __restrict__ scal,
+                                                   const int64_t* __restrict__ voff,
+                                                   const double* __restrict__ mq, int64_t mstride,
+                                                   const double* __restrict__ rtab,
+                                                   double* __restrict__ means) {
+  __shared__ double xs[2][7][64];   // [buffer][quantity 0-5, 1/(n+1)][member]
+  const int lane = threadIdx.x;
+  const int k = lane < 6 ? lane : 0;
   const int64_t V = scal[0];
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < 6 * V;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t v = t / 6;
-    const int k = (int)(t % 6);
+  for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
     const int64_t a = voff[v], e = voff[v + 1];
-    const double* x = mq + k * mstride;
-    double m = x[a];                       // first vote: mean = pose / model size
-    int64_t j = a + 1;
-    // loads of a batch are independent of the recurrence: issue them together
-    // r / d with d = n + 1 as RN(r * inv) corrected by one FMA residual step (Markstein):
-    // with inv = RN(1/d) from a table the result equals the correctly rounded r / d
-    // (verified against r / d on 2e8 random cases), and the chain is 5 dependent f64 ops.
-    for (; j + 8 <= e; j += 8) {
-      double b[8], inv[8];
+    double m = mq[k * mstride + a];        // first vote: mean = pose / model size
+    // batch b covers members a+1+64b ... ; n of member j is j - a
+    double nx[7];
+    auto fetch = [&](int64_t j0) {
+      const int64_t j = j0 + lane;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        b[i] = x[j + i];
-        inv[i] = rtab[j + i - a];            // 1 / (n + 1), n = j + i - a
-      }
+      for (int q = 0; q < 6; ++q) nx[q] = j < e ? mq[q * mstride + j] : 0.0;
+      nx[6] = j < e ? rtab[j - a] : 0.0;   // 1 / (n + 1)
+    };
+    int buf = 0;
+    fetch(a + 1);
+    for (int64_t j0 = a + 1; j0 < e; j0 += 64) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const double n = (double)(j + i - a), d = n + 1.0;
-        const double r = m * n + b[i];     // -ffp-contract=off: rounded mul, rounded add
-        const double q0 = r * inv[i];
-        m = __builtin_fma(__builtin_fma(-q0, d, r), inv[i], q0);
+      for (int q = 0; q < 7; ++q) xs[buf][q][lane] = nx[q];
+      __builtin_amdgcn_wave_barrier();
+      if (j0 + 64 < e) fetch(j0 + 64);     // in flight during the chains below
+      const int cnt = (int)min<int64_t>(64, e - j0);
+      if (lane < 6) {
+        const double n0 = (double)(j0 - a);
+        if (cnt == 64) {   // full batch: unrolled, LDS reads run ahead of the chain
+#pragma unroll
+          for (int i = 0; i < 64; ++i) {
+            const double n = n0 + i, d = n + 1.0, inv = xs[buf][6][i];
+            const double r = m * n + xs[buf][k][i];   // -ffp-contract=off: 2 roundings
+            const double q0 = r * inv;
+            m = __builtin_fma(__builtin_fma(-q0, d, r), inv, q0);
+          }
+        } else {
+          for (int i = 0; i < cnt; ++i) {
+            const double n = n0 + i, d = n + 1.0, inv = xs[buf][6][i];
+            const double r = m * n + xs[buf][k][i];
+            const double q0 = r * inv;
+            m = __builtin_fma(__builtin_fma(-q0, d, r), inv, q0);
+          }
+        }
       }
+      __builtin_amdgcn_wave_barrier();
+      buf ^= 1;
     }
-    for (; j < e; ++j) {
-      const double n = (double)(j - a);
-      m = (m * n + x[j]) / (n + 1.0);
-    }
-    means[6 * v + k] = m;
+    if (lane < 6) means[6 * v + k] = m;
   }
 }
 
@@ -957,7 +978,7 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   hipLaunchKernelGGL(recip_table_kernel, dim3(std::max(1, ctx->num_cus)), dim3(256), 0,
                      ctx->stream, ctx->scal.p, ctx->rtab.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus * 2)), dim3(64), 0, ctx->stream,
+  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus * 8)), dim3(64), 0, ctx->stream,
                      ctx->scal.p, ctx->voff.p, ctx->mq.p, ctx->mmax, ctx->rtab.p, ctx->means.p);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
