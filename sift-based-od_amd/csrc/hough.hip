@@ -244,6 +244,27 @@ __device__ __forceinline__ uint32_t first_touch_slots(int64_t q, const uint32_t*
   return n;
 }
 
+// 256-thread exclusive scan (sum, or max with identity 0): wave prefix via shuffles, then
+// the preceding waves' totals; sh holds 4 entries.  Ends with a barrier (sh reusable).
+template <bool kMax>
+__device__ __forceinline__ uint32_t block_scan256(uint32_t v, uint32_t* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x = kMax ? max(x, y) : x + y;
+  }
+  const uint32_t ex = __shfl_up(x, 1);   // exclusive within the wave
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int i = 0; i < w; ++i) off = kMax ? max(off, sh[i]) : off + sh[i];
+  __syncthreads();
+  const uint32_t inw = lane ? ex : 0u;
+  return kMax ? max(off, inw) : off + inw;
+}
+
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
   // kSelThreads-wide exclusive scan (4 waves): wave prefix via shuffles, then wave offsets
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -429,7 +450,7 @@ __global__ __launch_bounds__(256) void member_fill_kernel(
   // 3. run starts: start[i] = last index <= i where the bin changes (block max-scan,
   //    16 consecutive elements per thread)
   __shared__ uint32_t start_of[kFillCap];
-  __shared__ uint32_t tmax[256];
+  __shared__ uint32_t tmax[4];
   const int per = (p + 255) / 256;
   const int i0 = threadIdx.x * per;
   uint32_t run = 0;
@@ -437,19 +458,8 @@ __global__ __launch_bounds__(256) void member_fill_kernel(
     if (i == 0 || (uint32_t)(key[i - 1] >> 32) != (uint32_t)(key[i] >> 32)) run = (uint32_t)i;
     start_of[i] = run;   // provisional: only valid if a head occurred within this chunk
   }
-  tmax[threadIdx.x] = run;
-  __syncthreads();
-  if (threadIdx.x == 0) {   // 256-entry exclusive max-scan (cheap, LDS resident)
-    uint32_t m = 0;
-    for (int t = 0; t < 256; ++t) {
-      const uint32_t v = tmax[t];
-      tmax[t] = m;
-      m = v > m ? v : m;
-    }
-  }
-  __syncthreads();
   {
-    const uint32_t carry = tmax[threadIdx.x];
+    const uint32_t carry = block_scan256<true>(run, tmax);   // exclusive max over threads
     bool head_seen = false;
     for (int i = i0; i < i0 + per && i < n; ++i) {
       if (i == 0 || (uint32_t)(key[i - 1] >> 32) != (uint32_t)(key[i] >> 32)) head_seen = true;
@@ -493,18 +503,7 @@ __device__ void block_scan_lds(uint32_t* a, int n, uint32_t* part) {
   const int t = threadIdx.x, i0 = t * kOrderPer;
   uint32_t acc = 0;
   for (int i = i0; i < i0 + kOrderPer && i < n; ++i) acc = kMax ? max(acc, a[i]) : acc + a[i];
-  part[t] = acc;
-  __syncthreads();
-  if (t == 0) {
-    uint32_t run = 0;
-    for (int k = 0; k < kOrderT; ++k) {
-      const uint32_t v = part[k];
-      part[k] = run;
-      run = kMax ? max(run, v) : run + v;
-    }
-  }
-  __syncthreads();
-  uint32_t run = part[t];
+  uint32_t run = block_scan256<kMax>(acc, part);
   for (int i = i0; i < i0 + kOrderPer && i < n; ++i) {
     const uint32_t v = a[i];
     if (kMax) {

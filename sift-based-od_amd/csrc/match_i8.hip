@@ -39,17 +39,25 @@ typedef __attribute__((address_space(3))) void lds_void;
 namespace {
 
 constexpr int QT = 8;          // 16-query tiles per wave
-constexpr int NW = 4;
-constexpr int NT = NW * 64;
+#ifndef SOD_I8_NW
+#define SOD_I8_NW 8
+#endif
+// 16x16x64 kernel: one work-group of NW16 waves per CU slot.  With 8 waves (2 per SIMD)
+// in ONE work-group the stage barrier keeps the two waves of a SIMD in step; two 4-wave
+// work-groups per CU instead let the older one take issue priority, finish ~30 % earlier
+// and leave the other running alone (one wave per SIMD) for the tail (measured with
+// in-kernel stamps).
+constexpr int NW16 = SOD_I8_NW;
+constexpr int NT16 = NW16 * 64;
 constexpr int SPS = 8;         // subtiles per stage (128 rows)
 constexpr int kSub = 2048;     // bytes per 16-row subtile
 constexpr int kStageBytes = SPS * kSub;          // 16 KiB
 // per stage (128 rows) and wave w (rows 32w..32w+31): [c: 32 x i32 | p: 32 x i32]
 constexpr int kStageNorm = 2 * SPS * kSubRows * 4;   // 1 KiB
 constexpr int kStageSlot = kStageBytes + kStageNorm;
-constexpr int kPiecesPerWave = kStageBytes / 1024 / NW;   // 4
+constexpr int kPiecesPerWave = kStageBytes / 1024 / NW16;   // 1 KiB LDS-DMA pieces
 constexpr int kPadNormI = 1 << 30;                        // ||d'||^2 of padding rows (w = -2^30)
-static_assert(kStageBytes / 1024 % NW == 0, "pieces split evenly");
+static_assert(kStageBytes / 1024 % NW16 == 0, "pieces split evenly");
 
 // pack: one thread per (row, 16-dim chunk c = 0..7); int8 of (value - 128); exact i32 norm
 template <typename TIn, bool kWide>
@@ -127,12 +135,15 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* lds_base) {
   __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_base, 16, 0, 0);
 }
 
-// norms of the stage's 128 rows: wave w's lanes 0-7 fetch c, lanes 8-15 parity, of rows
-// 32w..32w+31 (one 256-B run per wave: global_load_lds writes lane i at M0 + 16 i)
+// norms of the stage's 128 rows, wave w of NWx covering rows R*w .. R*w+R-1 (R = 128/NWx):
+// lanes 0..R/4-1 fetch c, the next R/4 lanes parity -> one run [c: R x i32 | p: R x i32]
+// per wave (global_load_lds writes lane i at M0 + 16 i)
+template <int NWx>
 __device__ __forceinline__ void issue_norms(const int* __restrict__ dn, int64_t npad, int64_t row0,
                                             uint8_t* slot_norm, int wave, int lane) {
-  const int* src = dn + (lane < 8 ? 0 : npad) + row0 + wave * 32 + (lane & 7) * 4;
-  if (lane < 16) glds16(src, slot_norm + wave * 256);
+  constexpr int R = 128 / NWx, L = R / 4;
+  const int* src = dn + (lane < L ? 0 : npad) + row0 + wave * R + (lane % L) * 4;
+  if (lane < 2 * L) glds16(src, slot_norm + wave * (8 * R));
 }
 
 __device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
@@ -144,12 +155,16 @@ __device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
     const int piece = wave * kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  issue_norms(dn, npad, sub0 * kSubRows, slot + kStageBytes, wave, lane);
+  issue_norms<NW16>(dn, npad, sub0 * kSubRows, slot + kStageBytes, wave, lane);
 }
 
-// LDS offset of a 16-row subtile's c (p at +128) for lane group g = lane >> 4
+// LDS offset of a 16-row subtile's c for lane group g = lane >> 4 (its 4 rows 16u+4g..);
+// the parity words follow at +kParOff
+constexpr int kNormRows = 128 / NW16;
+constexpr int kParOff = 4 * kNormRows;
 __device__ __forceinline__ int norm_off(int u, int g) {
-  return kStageBytes + (u >> 1) * 256 + (u & 1) * 64 + g * 16;
+  const int row = 16 * u + 4 * g;
+  return kStageBytes + (row / kNormRows) * (8 * kNormRows) + (row % kNormRows) * 4;
 }
 
 // median of three (v_med3_i32): with y1 >= y2, med3(y1, y, y2) is the new second best
@@ -175,6 +190,9 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #endif
 #ifndef SOD_I8_PIPE
 #define SOD_I8_PIPE 1      // prefilter subtile u while the MFMAs of subtile u+1 run
+#endif
+#ifndef SOD_I8_SGB
+#define SOD_I8_SGB 1       // explicit MFMA / VALU interleave of the subtile block (+3 %)
 #endif
 #ifndef SOD_I8_XCD
 #define SOD_I8_XCD 1       // XCD-aware work-group -> (chunk, query block) order
@@ -218,6 +236,16 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 
     hit[t] = __builtin_amdgcn_ballot_w64(m >= t2[t]);
     any |= hit[t];
   }
+#if SOD_I8_SGB
+  // interleave this block (the subtile's 16 MFMAs, next-subtile LDS reads, the previous
+  // subtile's prefilter) as MFMA, 2 VALU, MFMA, 2 VALU, ...
+#pragma unroll
+  for (int i = 0; i < 2 * QT; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);                            // MFMA
+    if (i < 3 * QT / 2) __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);       // VALU
+    if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+  }
+#endif
   if (any) {
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
@@ -243,7 +271,7 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 
   }
 }
 
-// One work unit: query block qb (NW*QT tiles) against DB chunk sp (sub_per_split subtiles),
+// One work unit: query block qb (NW16*QT tiles) against DB chunk sp (sub_per_split subtiles),
 // writing the chunk's partial top-2 of every query to slot sp of pd1/pidx/pd2.
 __device__ __forceinline__ void match_unit(
     uint8_t* lds, int sp, int qb, const uint8_t* __restrict__ dbpack, const int* __restrict__ dn,
@@ -251,7 +279,7 @@ __device__ __forceinline__ void match_unit(
     int64_t nq_pad, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qt0 = (qb * NW + wave) * QT;
+  const int qt0 = (qb * NW16 + wave) * QT;
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / SPS;
@@ -293,7 +321,10 @@ __device__ __forceinline__ void match_unit(
   for (int64_t s = 0; s < nst; ++s) {
     // the wave's loads of stage s are complete when at most the later prefetched stages'
     // loads remain in flight (vector memory returns in order)
-    if (kRing == 3 && s + 1 < nst)
+    const int64_t younger = min<int64_t>(kRing - 2, nst - 1 - s);   // stages issued after s
+    if (kRing >= 4 && younger >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kLoadsPerStage) : "memory");
+    else if (kRing >= 3 && younger >= 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLoadsPerStage) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -308,7 +339,7 @@ __device__ __forceinline__ void match_unit(
     i32x4 fa0 = *reinterpret_cast<const i32x4*>(sb + lane * 16);
     i32x4 fa1 = *reinterpret_cast<const i32x4*>(sb + 1024 + lane * 16);
     i32x4 fc = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4));
-    i32x4 fp = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4) + 128);
+    i32x4 fp = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4) + kParOff);
 #pragma unroll
     for (int u = 0; u < SPS; ++u) {
       const i32x4 a0 = fa0, a1 = fa1, c = fc, p = fp;   // c = floor(-||d'||^2 / 2)
@@ -321,7 +352,7 @@ __device__ __forceinline__ void match_unit(
         fa0 = *reinterpret_cast<const i32x4*>(nb);
         fa1 = *reinterpret_cast<const i32x4*>(nb + 1024);
         fc = *reinterpret_cast<const i32x4*>(sb + norm_off(u + 1, lane >> 4));
-        fp = *reinterpret_cast<const i32x4*>(sb + norm_off(u + 1, lane >> 4) + 128);
+        fp = *reinterpret_cast<const i32x4*>(sb + norm_off(u + 1, lane >> 4) + kParOff);
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t)
@@ -362,12 +393,25 @@ __device__ __forceinline__ void match_unit(
   }
 }
 
-__global__ __launch_bounds__(NT, 2) void match_i8_kernel(
+#ifdef SOD_I8_STAMP
+// diagnostic build only: per work-group (s_memtime, s_memrealtime) at start and end, for
+// the in-kernel clock = d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS)
+__device__ unsigned long long g_stamps[4096][8];
+#endif
+
+__global__ __launch_bounds__(NT16, 8 / NW16) void match_i8_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2, int nqb) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageSlot];
+#ifdef SOD_I8_STAMP
+  unsigned long long t0 = 0, r0 = 0;
+  if (threadIdx.x == 0) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 #if SOD_I8_XCD
   // XCD-aware order: blocks b, b+8, ... share an XCD (and its L2); give each such group a
   // contiguous run of chunk-major units, so an XCD streams one or two DB chunks, in step,
@@ -380,6 +424,21 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
   match_unit(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
              nq_pad, sub_per_split, row_offset, pd1, pidx, pd2);
 #endif
+#ifdef SOD_I8_STAMP
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    g_stamps[blockIdx.x][0] = t0;
+    g_stamps[blockIdx.x][1] = r0;
+    g_stamps[blockIdx.x][2] = t1;
+    g_stamps[blockIdx.x][3] = r1;
+    unsigned hwid, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_stamps[blockIdx.x][4] = hwid;
+    g_stamps[blockIdx.x][5] = xcc;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -387,7 +446,12 @@ __global__ __launch_bounds__(NT, 2) void match_i8_kernel(
 // 4(l>>5)) of each 32-row subtile.  An MFMA of this shape holds the SIMD's issue port for
 // 8 of its 32 cycles (vs 8 of 16 for 16x16x64), and the prefilter reduces 16 values per
 // lane per tile, so the instruction stream leaves room beside the matrix pipe.
+#ifndef SOD_I8W_NW
+#define SOD_I8W_NW 8
+#endif
 namespace w {
+constexpr int NW = SOD_I8W_NW;   // waves per work-group (8: one work-group per CU)
+constexpr int NT = NW * 64;
 constexpr int QT = 4;            // 32-query tiles per wave (128 queries)
 constexpr int SPS = 4;           // 32-row subtiles per stage (128 rows)
 constexpr int kSub = 4096;
@@ -395,6 +459,14 @@ constexpr int kStageBytes = SPS * kSub;          // 16 KiB
 constexpr int kStageNorm = 2 * SPS * 32 * 4;     // c and p of 128 rows: 1 KiB
 constexpr int kStageSlot = kStageBytes + kStageNorm;
 constexpr int kPiecesPerWave = kStageBytes / 1024 / NW;
+constexpr int kRing = 3;
+constexpr int kLoadsPerStage = kPiecesPerWave + 1;
+constexpr int kNormRows = 128 / NW;               // norm rows staged per wave
+// LDS offset (from the slot) of c for the 4 consecutive rows starting at stage row r;
+// parity at + 4 * kNormRows
+__device__ __forceinline__ int norm_off(int r) {
+  return kStageBytes + (r / kNormRows) * (8 * kNormRows) + (r % kNormRows) * 4;
+}
 }  // namespace w
 
 typedef __attribute__((ext_vector_type(16))) int i32x16;
@@ -408,26 +480,31 @@ __device__ __forceinline__ void issue_stage_w(const uint8_t* __restrict__ dbpack
     const int piece = wave * w::kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  issue_norms(dn, npad, sub0 * 32, slot + w::kStageBytes, wave, lane);   // wave u: subtile u
+  issue_norms<w::NW>(dn, npad, sub0 * 32, slot + w::kStageBytes, wave, lane);
 }
 
-__global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
+__global__ __launch_bounds__(w::NT) void match_i8w_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
-    int* __restrict__ pidx, float* __restrict__ pd2) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * w::kStageSlot];
+    int* __restrict__ pidx, float* __restrict__ pd2, int nqb) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[w::kRing * w::kStageSlot];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int sp = blockIdx.x % split;
-  const int qb = blockIdx.x / split;
-  const int qt0 = (qb * NW + wave) * w::QT;
+  // XCD-aware chunk-major order, as match_i8_kernel
+  const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x8 = blockIdx.x % 8;
+  const unsigned unit = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + blockIdx.x / 8;
+  const int sp = (int)(unit / nqb);
+  const int qb = (int)(unit % nqb);
+  const int qt0 = (qb * w::NW + wave) * w::QT;
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / w::SPS;
   const int h = lane >> 5;
   const int64_t npad = nsub * 32;
 
-  if (nst > 0) issue_stage_w(dbpack, dn, npad, s_lo, lds, wave, lane);
+#pragma unroll
+  for (int j = 0; j < w::kRing - 1; ++j)
+    if (j < nst) issue_stage_w(dbpack, dn, npad, s_lo + j * w::SPS, lds + j * w::kStageSlot, wave, lane);
 
   i32x4 bq[w::QT][4];
 #pragma unroll
@@ -447,12 +524,20 @@ __global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
     id[t] = 0x7fffffff;
   }
 
+  int slot = 0;
   for (int64_t s = 0; s < nst; ++s) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
     if (s + 1 < nst)
-      issue_stage_w(dbpack, dn, npad, s_lo + (s + 1) * w::SPS, lds + ((s + 1) & 1) * w::kStageSlot, wave, lane);
-    const uint8_t* sb = lds + (s & 1) * w::kStageSlot;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(w::kLoadsPerStage) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + w::kRing - 1 < nst) {
+      const int ns = slot == 0 ? w::kRing - 1 : slot - 1;
+      issue_stage_w(dbpack, dn, npad, s_lo + (s + w::kRing - 1) * w::SPS, lds + ns * w::kStageSlot,
+                    wave, lane);
+    }
+    const uint8_t* sb = lds + slot * w::kStageSlot;
+    slot = slot + 1 == w::kRing ? 0 : slot + 1;
     i32x4 fa[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) fa[k] = *reinterpret_cast<const i32x4*>(sb + k * 1024 + lane * 16);
@@ -461,12 +546,11 @@ __global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
       i32x4 a[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) a[k] = fa[k];
-      // c = floor(-||d'||^2 / 2) of the lane's 16 rows 8g + 4h + i (4 x 16 B); p at +128 B
-      const int* wp = reinterpret_cast<const int*>(sb + w::kStageBytes + u * 256);
+      // c = floor(-||d'||^2 / 2) of the lane's 16 rows 8g + 4h + i (4 x 16 B)
       i32x16 c;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const i32x4 wv = *reinterpret_cast<const i32x4*>(wp + 8 * g + 4 * h);
+        const i32x4 wv = *reinterpret_cast<const i32x4*>(sb + w::norm_off(32 * u + 8 * g + 4 * h));
 #pragma unroll
         for (int i = 0; i < 4; ++i) c[4 * g + i] = wv[i];
       }
@@ -484,24 +568,25 @@ __global__ __launch_bounds__(NT, 2) void match_i8w_kernel(
 #pragma unroll
         for (int t = 0; t < w::QT; ++t)
           acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], bq[t][k], acc[t], 0, 0, 0);
-      bool hit[w::QT];
-      bool any = false;
+      uint64_t hit[w::QT];
+      uint64_t any = 0;
 #pragma unroll
       for (int t = 0; t < w::QT; ++t) {
         int m = acc[t][0];
 #pragma unroll
         for (int r = 1; r < 16; ++r) m = max(m, acc[t][r]);
-        hit[t] = m >= t2[t];
+        hit[t] = __builtin_amdgcn_ballot_w64(m >= t2[t]);
         any |= hit[t];
       }
-      if (__any(any)) {
+      if (any) {
         const int rowb = row_offset + (int)((s_lo + s * w::SPS + u) * 32) + 4 * h;
 #pragma unroll
         for (int t = 0; t < w::QT; ++t) {
-          if (__any(hit[t])) {
+          if (hit[t]) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              const i32x4 pv = *reinterpret_cast<const i32x4*>(wp + 32 + 8 * g + 4 * h);
+              const i32x4 pv = *reinterpret_cast<const i32x4*>(
+                  sb + w::norm_off(32 * u + 8 * g + 4 * h) + 4 * w::kNormRows);
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 const int y = 2 * acc[t][4 * g + i] | pv[i];
@@ -582,17 +667,23 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   return SOD_OK;
 }
 
+#ifdef SOD_I8_STAMP
+extern "C" int sod_debug_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 64) == hipSuccess ? 0 : 1;
+}
+#endif
+
 int launch_match_i8(sod_ctx* ctx) {
   const bool wide = ctx->impl == 2;
   const int rows = wide ? 32 : kSubRows;
   const int sps = wide ? w::SPS : SPS;
-  const int qt_per_wg = NW * (wide ? w::QT : QT);
+  const int qt_per_wg = wide ? w::NW * w::QT : NW16 * QT;
   const int64_t nq_pad = (int64_t)ctx->nqt * rows;
   const int64_t qblocks = cdiv(ctx->nqt, qt_per_wg);
   const int64_t nstages = ctx->nsub / sps;
-  // one round of 2 work-groups per CU: as few DB chunks as fill the chip (every chunk
+  // one round of work-groups (8 waves per CU): as few DB chunks as fill the chip (every chunk
   // restarts each query's running top-2, so more chunks mean more slow-path updates)
-  const int64_t slots = 2LL * ctx->num_cus;
+  const int64_t slots = ((wide ? w::NW : NW16) == 4 ? 2LL : 1LL) * ctx->num_cus;   // in flight
   int64_t split = std::max<int64_t>(1, (slots + qblocks / 2) / qblocks);
   split = std::min<int64_t>(split, nstages);
   const int64_t st_per_split = cdiv(nstages, split);
@@ -606,13 +697,13 @@ int launch_match_i8(sod_ctx* ctx) {
   SOD_TRY(sod_reserve(ctx, ctx->cidx, (size_t)nq_pad));
   SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
   if (wide)
-    hipLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(NT), 0, ctx->stream,
-                       ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,
-                       ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,
-                       (int)split, st_per_split * sps, (int)ctx->row_offset, ctx->pd1.p,
-                       ctx->pidx.p, ctx->pd2.p);
+    hipLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0,
+                       ctx->stream, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
+                       ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt,
+                       nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, ctx->pd1.p,
+                       ctx->pidx.p, ctx->pd2.p, (int)qblocks);
   else
-    hipLaunchKernelGGL(match_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(NT), 0, ctx->stream,
+    hipLaunchKernelGGL(match_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(NT16), 0, ctx->stream,
                        ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,
                        ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,
                        (int)split, st_per_split * sps, (int)ctx->row_offset, ctx->pd1.p,

@@ -38,6 +38,41 @@ peak = 2500.0 if impl == "bf16" else 5000.0   # dense bf16 / int8 MFMA peaks
 print("%s [%s]: match %.3f ms (min %.3f)  %.0f T(FL)OP/s  frac %.3f  %.3g pairs/s" % (
     os.path.basename(_lib.LIB_PATH), impl, ts.mean(), ts.min(), tf, tf / peak,
     nq * len(db) / (ts.mean() / 1e3)), flush=True)
+if hasattr(ctx._L, "sod_debug_stamps"):   # diagnostic build: in-kernel clock
+    import ctypes as C
+    st = np.zeros((4096, 8), np.uint64)
+    ctx._L.sod_debug_stamps(st.ctypes.data_as(C.c_void_p), 4096)
+    nb = int((st[:, 3] > st[:, 1]).sum())
+    st = st[:nb]
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    np.save(os.path.join(REPO, "gpurun_out", "stamps_%s.npy" % impl), st)
+    ghz = (st[:, 2] - st[:, 0]) / (st[:, 3] - st[:, 1]) * 0.1
+    dur = (st[:, 3] - st[:, 1]) / 100.0   # us (100 MHz realtime)
+    print("in-kernel clock: median %.3f GHz (min %.3f max %.3f) over %d work-groups; "
+          "WG duration us: min %.0f median %.0f max %.0f; start skew %.1f us, span %.0f us" % (
+              np.median(ghz), ghz.min(), ghz.max(), len(st), dur.min(), np.median(dur),
+              dur.max(), (st[:, 1].max() - st[:, 1].min()) / 100.0,
+              (st[:, 3].max() - st[:, 1].min()) / 100.0), flush=True)
+    # per-WG placement: HW_ID (gfx9: wave[3:0] simd[5:4] pipe[7:6] cu[11:8] sh[12] se[15:13])
+    hw = st[:, 4].astype(np.int64)
+    cu = (hw >> 8) & 0xF
+    se = (hw >> 13) & 0x7
+    sh = (hw >> 12) & 1
+    xcc = st[:, 5].astype(np.int64) & 0xF
+    place = (xcc * 8 + se) * 32 + sh * 16 + cu
+    uniq, inv, cnt = np.unique(place, return_inverse=True, return_counts=True)
+    shared = cnt[inv] > 1
+    print("WGs alone on a CU: %d, duration median %.0f us; sharing: %d, median %.0f us" % (
+        (~shared).sum(), np.median(dur[~shared]) if (~shared).any() else 0,
+        shared.sum(), np.median(dur[shared])), flush=True)
+    for x in range(8):
+        m = xcc == x
+        if m.any():
+            print("  xcc %d: %d WGs, duration median %.0f max %.0f us" % (
+                x, m.sum(), np.median(dur[m]), dur[m].max()), flush=True)
+    order = np.argsort(-dur)[:8]
+    print("  slowest WGs (block, us, xcc, cu-slot):", [(int(b), int(dur[b]), int(xcc[b]),
+                                                     int(place[b])) for b in order], flush=True)
 ctx.ratio(0.75)
 idx1, d1, d2, good = ctx.match_result()
 print("checksum", int(idx1.astype(np.int64).sum()), float(d1.astype(np.float64).sum()), flush=True)
