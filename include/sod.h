@@ -73,10 +73,10 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq,
  * main.py:70-86.  enqueue: local shard top-2 (exact squared distances), merged over
  * this ctx's descriptor shard. */
 int sod_match_enqueue(sod_ctx* ctx);
-/* Matcher implementation: 0 = bf16 MFMA (default), 1 = int8 MFMA 16x16x64 and
- * 2 = int8 MFMA 32x32x32 (values shifted by -128; exact i32 dot products; 2x the MFMA
- * rate).  All are bit-exact; call before the descriptor uploads (the packed layouts
- * differ; switching drops uploaded descriptors). */
+/* Matcher implementation: 1 = int8 MFMA 16x16x64 (default, fastest), 2 = int8 MFMA
+ * 32x32x32, 0 = bf16 MFMA.  int8: values shifted by -128, exact i32 dot products, 2x the
+ * bf16 MFMA rate.  All are bit-exact; call before the descriptor uploads (the packed
+ * layouts differ; switching drops uploaded descriptors). */
 int sod_match_set_impl(sod_ctx* ctx, int impl);
 /* multi-GPU: RCCL all-gather of every rank's per-query (d1^2, idx1, d2^2) and the
  * global merge.  No-op on a single rank. */

@@ -229,7 +229,7 @@ class Context:
     IMPLS = {"bf16": 0, "i8": 1, "i8w": 2}
 
     def set_impl(self, impl):
-        """Matcher implementation "bf16" (default), "i8" (int8 16x16x64) or "i8w" (int8
+        """Matcher implementation "i8" (int8 16x16x64, default), "bf16" or "i8w" (int8
         32x32x32); call before uploads."""
         self._chk(self._L.sod_match_set_impl(self._h, self.IMPLS[impl] if isinstance(impl, str)
                                              else int(impl)))

@@ -31,7 +31,7 @@ struct sod_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   int num_cus = 256;
-  int impl = 0;                 // matcher: 0 = bf16 MFMA (match.hip), 1/2 = int8 MFMA 16x16x64 / 32x32x32 (match_i8.hip)
+  int impl = 1;                 // matcher: 1 = int8 MFMA 16x16x64 (default), 2 = int8 32x32x32 (match_i8.hip), 0 = bf16 (match.hip)
 
   // ---- database (keypoints replicated, descriptors = shard) ----
   int64_t n_total = 0;          // keypoints in the whole DB

@@ -34,5 +34,5 @@ def _ctx_session():
 
 @pytest.fixture
 def ctx(_ctx_session):
-    _ctx_session.set_impl("bf16")
+    _ctx_session.set_impl("i8")
     return _ctx_session
