@@ -14,9 +14,15 @@ int sod_fail(sod_ctx* ctx, int code, const std::string& msg) {
 namespace {
 thread_local std::string g_err;  // errors before a ctx exists
 
-int set_dev(sod_ctx* ctx) {
+// Every entry point starts here; by default it also joins the side stream (PoseBin means),
+// so whatever comes next on the main stream sees their results.
+int set_dev(sod_ctx* ctx, bool join = true) {
   if (!ctx) return SOD_EINVAL;
   SOD_HIP(ctx, hipSetDevice(ctx->device));
+  if (join && ctx->side_pending) {
+    SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+    ctx->side_pending = false;
+  }
   return SOD_OK;
 }
 
@@ -68,6 +74,9 @@ int sod_create(int device, sod_ctx** out) {
     if (e == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
   }
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
   if (e != hipSuccess) {
     g_err = std::string("sod_create: ") + hipGetErrorString(e);
     delete ctx;
@@ -86,6 +95,7 @@ int sod_create(int device, sod_ctx** out) {
 void sod_destroy(sod_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   sod_release(ctx->mx); sod_release(ctx->my); sod_release(ctx->mang);
@@ -108,6 +118,9 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->fvotes); sod_release(ctx->params); sod_release(ctx->alive);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -449,7 +462,7 @@ int sod_bins_get(sod_ctx* ctx, int32_t* keys, int32_t* votes) {
 // ---- affine ---------------------------------------------------------------------------
 int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_factor,
                        double y_factor, int32_t threshold) {
-  SOD_TRY(set_dev(ctx));
+  SOD_TRY(set_dev(ctx, false));   // runs beside the means on the side stream
   if (!ctx->selected) return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
   if (!(x_factor != 0.0) || !(y_factor != 0.0)) return sod_fail(ctx, SOD_EINVAL, "zero factor");
   SOD_TRY(launch_affine_gather(ctx));

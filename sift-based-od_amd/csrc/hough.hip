@@ -968,18 +968,24 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
                      ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
                      ctx->vmask.p, ctx_bins(ctx), nblk, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
+  // PoseBin means depend only on the member lists: they run on the side stream, beside the
+  // affine verification, and the main stream joins them at the next entry point (set_dev)
   SOD_TRY(sod_reserve(ctx, ctx->mq, (size_t)ctx->mmax * 6));
+  SOD_TRY(sod_reserve(ctx, ctx->rtab, (size_t)ctx->mmax));
+  SOD_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+  SOD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
   hipLaunchKernelGGL(means_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
-                     ctx->stream, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p,
+                     ctx->side, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p,
                      ctx->mimg.p, ctx->isize.p, ctx->mmax, ctx->mq.p);
   SOD_HIP(ctx, hipGetLastError());
-  SOD_TRY(sod_reserve(ctx, ctx->rtab, (size_t)ctx->mmax));
   hipLaunchKernelGGL(recip_table_kernel, dim3(std::max(1, ctx->num_cus)), dim3(256), 0,
-                     ctx->stream, ctx->scal.p, ctx->rtab.p);
+                     ctx->side, ctx->scal.p, ctx->rtab.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus * 8)), dim3(64), 0, ctx->stream,
+  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus * 8)), dim3(64), 0, ctx->side,
                      ctx->scal.p, ctx->voff.p, ctx->mq.p, ctx->mmax, ctx->rtab.p, ctx->means.p);
   SOD_HIP(ctx, hipGetLastError());
+  SOD_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
+  ctx->side_pending = true;
   return SOD_OK;
 }
 

@@ -111,6 +111,11 @@ struct sod_ctx {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
 
+  // ---- side stream: PoseBin means run beside the affine verification ----
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool side_pending = false;    // main stream has not yet waited for the side work
+
   // ---- timing ----
   hipEvent_t ev[8] = {};
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
