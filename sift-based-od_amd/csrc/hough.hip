@@ -397,6 +397,66 @@ __global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __
 // in LDS: equal bins form runs and ONE atomicAdd per run reserves the run's slots.  Runs
 // land in arbitrary block order; member_order_kernel restores query order per bin.
 constexpr int kFillQ = 256;                 // queries per block -> <= 4096 votes
+constexpr int kSortE = 16;                  // keys per thread in sort_block_u64
+
+// bitonic compare-exchange of registers r and r|J (J < kSortE) of thread t, stage size k
+template <int J>
+__device__ __forceinline__ void sort_reg_stage(uint64_t (&a)[kSortE], int t, int k) {
+#pragma unroll
+  for (int r = 0; r < kSortE; ++r) {
+    if (r & J) continue;
+    const bool asc = ((t * kSortE + r) & k) == 0;
+    const uint64_t x = a[r], y = a[r | J];
+    const bool sw = asc ? (x > y) : (x < y);
+    a[r] = sw ? y : x;
+    a[r | J] = sw ? x : y;
+  }
+}
+
+// Ascending bitonic sort of key[0..p) (p a power of two, kSortE <= p <= kSortE * blockDim)
+// held as kSortE consecutive keys per thread: strides below kSortE are register
+// compare-exchanges, larger ones one LDS exchange each.
+__device__ void sort_block_u64(uint64_t* key, int p) {
+  const int t = threadIdx.x;
+  const bool act = t * kSortE < p;
+  uint64_t a[kSortE];
+  if (act) {
+#pragma unroll
+    for (int r = 0; r < kSortE; ++r) a[r] = key[t * kSortE + r];
+  }
+  for (int k = 2; k <= p; k <<= 1) {
+    for (int j = k >> 1; j >= kSortE; j >>= 1) {   // partner in another thread
+      __syncthreads();
+      if (act) {
+#pragma unroll
+        for (int r = 0; r < kSortE; ++r) key[t * kSortE + r] = a[r];
+      }
+      __syncthreads();
+      if (act) {
+        const int lo = ((t * kSortE) & j) == 0;     // this thread holds the lower index
+#pragma unroll
+        for (int r = 0; r < kSortE; ++r) {
+          const int i = t * kSortE + r;
+          const uint64_t o = key[i ^ j];
+          const bool asc = (i & k) == 0;
+          a[r] = (lo == asc) ? (a[r] < o ? a[r] : o) : (a[r] > o ? a[r] : o);
+        }
+      }
+    }
+    if (act) {
+      if (k >= 16) sort_reg_stage<8>(a, t, k);
+      if (k >= 8) sort_reg_stage<4>(a, t, k);
+      if (k >= 4) sort_reg_stage<2>(a, t, k);
+      sort_reg_stage<1>(a, t, k);
+    }
+  }
+  __syncthreads();
+  if (act) {
+#pragma unroll
+    for (int r = 0; r < kSortE; ++r) key[t * kSortE + r] = a[r];
+  }
+  __syncthreads();
+}
 constexpr int kFillCap = kFillQ * 16;
 __global__ __launch_bounds__(256) void member_fill_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
@@ -427,26 +487,12 @@ __global__ __launch_bounds__(256) void member_fill_kernel(
   __syncthreads();
   const int n = (int)nvote;
   if (n == 0) return;
-  int p = 1;
+  int p = kSortE;
   while (p < n) p <<= 1;
   for (int i = n + threadIdx.x; i < p; i += blockDim.x) key[i] = ~0ull;
   __syncthreads();
-  // 2. bitonic sort by (bin, query)
-  for (int kk = 2; kk <= p; kk <<= 1) {
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < p; i += blockDim.x) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint64_t x = key[i], y = key[l];
-          if ((x > y) == ((i & kk) == 0)) {
-            key[i] = y;
-            key[l] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
+  // 2. bitonic sort by (bin, query): 16 keys per thread in registers
+  sort_block_u64(key, p);
   // 3. run starts: start[i] = last index <= i where the bin changes (block max-scan,
   //    16 consecutive elements per thread)
   __shared__ uint32_t start_of[kFillCap];
