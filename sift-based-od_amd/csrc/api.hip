@@ -275,7 +275,7 @@ int sod_match_set_impl(sod_ctx* ctx, int impl) {
 int sod_match_allgather_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
-  if (ctx->nranks <= 1) return SOD_OK;
+  if (ctx->nranks <= 1 && !ctx->comm) return SOD_OK;   // a 1-rank communicator still runs
   if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
   const size_t nq_pad = (size_t)sod_nq_pad(ctx);
   const size_t tot = nq_pad * ctx->nranks;
@@ -368,7 +368,7 @@ int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int3
 int sod_hough_allreduce_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
-  if (ctx->nranks <= 1) return SOD_OK;
+  if (ctx->nranks <= 1 && !ctx->comm) return SOD_OK;   // a 1-rank communicator still runs
   if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
   ncclResult_t r = ncclGroupStart();
   if (r == ncclSuccess)
@@ -688,7 +688,8 @@ int sod_comm_init(sod_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[S
   }
   ctx->nranks = nranks;
   ctx->rank = rank;
-  if (nranks == 1) return SOD_OK;
+  // nranks == 1 also builds a communicator: the collectives then run (as copies), which is
+  // how the RCCL path is exercised on a one-GPU machine
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);

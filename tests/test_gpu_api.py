@@ -179,3 +179,30 @@ def test_sharded_in_process_equals_single(world):
         assert np.array_equal(v1["means"], v2["means"])
         assert np.array_equal(a1["survived"], a2["survived"])
         assert np.array_equal(a1["params"], a2["params"])
+
+
+def test_rccl_single_rank_collectives():
+    """The RCCL exchange on real hardware: a 1-rank communicator runs the all-gather of
+    the match candidates and the (sum, min) all-reduce of the Hough partials (as copies);
+    the pipeline result must equal the communicator-less one bit for bit."""
+    db = synthetic.make_database(12, 500, seed=41)
+    qs = synthetic.make_queries(3000, seed=42, db_seed=41, kp_per_image=500)
+    bins = (32, 32, 8, 12)
+    out = []
+    for use_comm in (False, True):
+        with _lib.Context(0) as c:
+            if use_comm:
+                c.comm_init(1, 0, _lib.unique_id())
+            c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+            c.upload_db(db.des)
+            c.upload_queries(qs.des, qs.kp)
+            c.pipeline(qs.shape, bins)
+            out.append((c.match_result(), c.valid_result(), c.affine_result(), c.all_bins()))
+    (m0, v0, a0, b0), (m1, v1, a1, b1) = out
+    for x, y in zip(m0, m1):
+        assert np.array_equal(x, y)
+    for k in ("keys", "votes", "offsets", "members"):
+        assert np.array_equal(v0[k], v1[k]), k
+    assert np.array_equal(b0[0], b1[0]) and np.array_equal(b0[1], b1[1])
+    assert np.array_equal(a0["survived"], a1["survived"])
+    assert np.array_equal(a0["params"], a1["params"])
