@@ -124,6 +124,26 @@ int sod_affine_get(sod_ctx* ctx, uint8_t* survived /* [V] */, int32_t* votes /* 
                    double* params /* [V*6] m1,m2,m3,m4,tx,ty */,
                    uint8_t* member_alive /* [M] */);
 
+/* ---- post-processing (PostProcessing.py:4-112, main.py:159-168) --
+ * group_position -> group_orientation -> find_max_orientation -> get_final_pose over the
+ * surviving bins (or the valid bins when no affine pass ran), in their list order.
+ * Outputs (caller-sized by the bin count n; every array may be NULL):
+ *   n_pos position clusters; pos_off[n_pos+1] / pos_members[n]: bin indices (into the
+ *     post-processed list) in the reference's DFS order;
+ *   n_ori orientation clusters; ori_pos_off[n_pos+1] = each position cluster's range of
+ *     orientation clusters; ori_off[n_ori+1] / ori_members[n]: bin indices;
+ *   final_orientation[n_pos]; final_pose[n_pos*6] = (x, y, orientation, scale, w, h) as
+ *     main.py's final_pose ((x, y), orientation, scale, (w, h)). */
+int sod_postprocess(sod_ctx* ctx, int32_t* n_bins, int32_t* bin_index /* [n] valid index */,
+                    int32_t* n_pos, int32_t* pos_off, int32_t* pos_members, int32_t* n_ori,
+                    int32_t* ori_pos_off, int32_t* ori_off, int32_t* ori_members,
+                    double* final_orientation, double* final_pose);
+/* the same on caller-supplied PoseBin means [n*6] = (x, y, angle, scale, w, h) */
+int sod_post_batch(sod_ctx* ctx, int32_t n, const double* means, int32_t* n_pos,
+                   int32_t* pos_off, int32_t* pos_members, int32_t* n_ori,
+                   int32_t* ori_pos_off, int32_t* ori_off, int32_t* ori_members,
+                   double* final_orientation, double* final_pose);
+
 /* ---- whole pipeline on one stream (bench / Main fast path) ------------------------ */
 typedef struct sod_pipeline_args {
   double ratio;           /* 0.75  main.py:82            */

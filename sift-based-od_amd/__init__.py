@@ -15,7 +15,9 @@ Drop-in surface (reference names, reference semantics):
 * ``PoseBin``                                              (``PoseBin.py``)
 * ``AffineParameters``, ``remove_outliers``                 (``AffineParameters.py``)
 * ``Main`` with ``run_matcher`` / ``apply_hough_transform`` / ``get_valid_bins`` /
-  ``apply_affine_parameters``                              (``main.py:17-157``)
+  ``apply_affine_parameters`` / ``post_process``            (``main.py:17-168``)
+* ``group_position``, ``group_orientation``, ``find_max_orientation``, ``get_final_pose``,
+  ``dfs``                                                  (``PostProcessing.py``)
 
 The native library is loaded lazily on first use and its absence is an error
 (there is no CPU fallback anywhere in this package).
@@ -30,6 +32,8 @@ from .hough import (calculate_bin_index, calculate_bin_index_batch,  # noqa: F40
 from .affine import (AffineParameters, Calc_x, Ext_Params, Gen_A, Gen_b,  # noqa: F401
                      remove_outliers, verify_bins)
 from .pipeline import Main  # noqa: F401
+from .postprocessing import (dfs, find_max_orientation, get_final_pose,  # noqa: F401
+                             group_orientation, group_position)
 from .sharded import HostComm, RcclComm, TorchHostComm, run_sharded, shard_range  # noqa: F401
 
 __all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid", "make_kp",
@@ -37,5 +41,6 @@ __all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid
            "ratio_match", "calculate_bin_index", "calculate_bin_index_batch",
            "estimate_object_pose", "estimate_object_pose_batch", "perform_hough_transform",
            "AffineParameters", "Calc_x", "Ext_Params", "Gen_A", "Gen_b", "remove_outliers",
-           "verify_bins", "Main", "HostComm", "RcclComm", "TorchHostComm", "run_sharded",
+           "verify_bins", "Main", "dfs", "group_position", "group_orientation",
+           "find_max_orientation", "get_final_pose", "HostComm", "RcclComm", "TorchHostComm", "run_sharded",
            "shard_range"]

@@ -70,6 +70,10 @@ SIGNATURES = {
                                      C.c_int32]),
     "sod_affine_get": (C.c_int, [c_ctx, c_u8p, c_i32p, c_f64p, c_u8p]),
     "sod_pipeline_enqueue": (C.c_int, [c_ctx, C.POINTER(PipelineArgs)]),
+    "sod_postprocess": (C.c_int, [c_ctx, c_i32p, c_i32p, c_i32p, c_i32p, c_i32p, c_i32p, c_i32p,
+                                  c_i32p, c_i32p, c_f64p, c_f64p]),
+    "sod_post_batch": (C.c_int, [c_ctx, C.c_int32, c_f64p, c_i32p, c_i32p, c_i32p, c_i32p, c_i32p,
+                                 c_i32p, c_i32p, c_f64p, c_f64p]),
     "sod_pose_batch": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_f32p, c_f32p,
                                  c_f32p, c_i32p, c_f64p, c_f64p, C.c_int32, C.c_int32, c_i32p,
                                  c_f64p, c_i32p]),
@@ -414,6 +418,50 @@ class Context:
             ptr(votes, C.c_int32), ptr(params, C.c_double), ptr(alive, C.c_uint8)))
         return {"survived": surv.astype(bool), "votes": votes, "params": params,
                 "alive": alive.astype(bool)}
+
+    def _post_arrays(self, n):
+        return dict(n_pos=C.c_int32(0), n_ori=C.c_int32(0),
+                    pos_off=np.empty(n + 1, np.int32), pos_members=np.empty(max(n, 1), np.int32),
+                    ori_pos_off=np.empty(n + 1, np.int32), ori_off=np.empty(n + 1, np.int32),
+                    ori_members=np.empty(max(n, 1), np.int32),
+                    orient=np.empty(max(n, 1), np.float64), pose=np.empty((max(n, 1), 6), np.float64))
+
+    @staticmethod
+    def _post_result(a, n):
+        npos, nori = a["n_pos"].value, a["n_ori"].value
+        return {"pos_off": a["pos_off"][:npos + 1].copy(), "pos_members": a["pos_members"][:n].copy(),
+                "ori_pos_off": a["ori_pos_off"][:npos + 1].copy(),
+                "ori_off": a["ori_off"][:nori + 1].copy(), "ori_members": a["ori_members"][:n].copy(),
+                "final_orientation": a["orient"][:npos].copy(), "final_pose": a["pose"][:npos].copy()}
+
+    def _post_call(self, fn, *head, n, a):
+        self._chk(fn(self._h, *head, C.byref(a["n_pos"]), ptr(a["pos_off"], C.c_int32),
+                     ptr(a["pos_members"], C.c_int32), C.byref(a["n_ori"]),
+                     ptr(a["ori_pos_off"], C.c_int32), ptr(a["ori_off"], C.c_int32),
+                     ptr(a["ori_members"], C.c_int32), ptr(a["orient"], C.c_double),
+                     ptr(a["pose"], C.c_double)))
+        return self._post_result(a, n)
+
+    def post_batch(self, means):
+        """PostProcessing.py:4-112 on PoseBin means [n, 6] = (x, y, angle, scale, w, h)."""
+        m = _c(means, np.float64).reshape(-1, 6)
+        n = len(m)
+        a = self._post_arrays(n)
+        return self._post_call(self._L.sod_post_batch, n, ptr(m, C.c_double), n=n, a=a)
+
+    def postprocess(self):
+        """main.py:159-168 on the pipeline's surviving (or valid) bins; ``bin_index`` maps
+        the post-processed list to valid-bin indices."""
+        V, _ = self.valid_counts()
+        a = self._post_arrays(V)
+        nb = C.c_int32(0)
+        idx = np.empty(max(V, 1), np.int32)
+        r = self._post_call(self._L.sod_postprocess, C.byref(nb), ptr(idx, C.c_int32), n=V, a=a)
+        n = nb.value
+        r["bin_index"] = idx[:n].copy()
+        r["pos_members"] = r["pos_members"][:n]
+        r["ori_members"] = r["ori_members"][:n]
+        return r
 
     def comm_init(self, nranks, rank, uid):
         buf = (C.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(uid)

@@ -1,0 +1,266 @@
+// post.hip -- SURVEY §8(f) row 1: post-processing of the verified pose bins
+// (PostProcessing.py:4-112, driven by main.py:159-168).
+//
+//   group_position      bins a, b are neighbours when |dx| <= w*s/4 and |dy| <= h*s/4 for
+//                       the means of a AND of b (PostProcessing.py:18-28); position
+//                       clusters are the components in recursive-DFS preorder from every
+//                       unseen bin in list order, neighbours ascending (:4-11, :32-36)
+//   group_orientation   inside each position cluster, neighbours when
+//                       |degrees(theta_a - theta_b)| <= 1 (:39-62), DFS in the cluster's
+//                       own (preorder) indexing
+//   find_max_orientation  mean angle of the LAST largest orientation cluster (:64-81)
+//   get_final_pose      mean centroid, that orientation, mean scale, img_size of the FIRST
+//                       bin of minimum (w*s)*(h*s) (:85-112)
+//
+// The O(n^2) part -- both neighbour relations over all pairs -- is one device kernel
+// writing two n x n bitmasks (bit j of row i, 64 per word); the components need the
+// reference's exact visit order (it fixes every later sum and tie), so the DFS walks the
+// bitmask rows on the host (set bits = ascending neighbours), O(n^2 / 64) word reads.
+// Compiled with -ffp-contract=off: the comparisons are the reference's Python floats.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "sod_internal.h"
+
+namespace {
+
+constexpr double kRadToDeg = 180.0 / 3.141592653589793;   // CPython math.degrees factor
+
+// one thread per (row i, 64-column word): bits of the position / orientation relations
+__global__ void post_adjacency_kernel(int n, int words, const double* __restrict__ m,
+                                      uint64_t* __restrict__ pos, uint64_t* __restrict__ ori) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n * words) return;
+  const int i = (int)(t / words), wd = (int)(t % words);
+  const double xi = m[6 * i], yi = m[6 * i + 1], ai = m[6 * i + 2], si = m[6 * i + 3];
+  const double txi = m[6 * i + 4] * si / 4, tyi = m[6 * i + 5] * si / 4;
+  uint64_t pb = 0, ob = 0;
+  for (int k = 0; k < 64; ++k) {
+    const int j = wd * 64 + k;
+    if (j >= n) break;
+    if (j == i) continue;
+    const double xj = m[6 * j], yj = m[6 * j + 1], aj = m[6 * j + 2], sj = m[6 * j + 3];
+    const double dx = fabs(xi - xj), dy = fabs(yi - yj);
+    const bool close = dx <= txi && dy <= tyi && dx <= m[6 * j + 4] * sj / 4 &&
+                       dy <= m[6 * j + 5] * sj / 4;
+    if (close) pb |= 1ull << k;
+    if (fabs((ai - aj) * kRadToDeg) <= 1) ob |= 1ull << k;
+  }
+  pos[t] = pb;
+  ori[t] = ob;
+}
+
+// Components in the order of the reference's recursive dfs, over the nodes `nodes`
+// (global ids) with neighbour test `adj(a, b)` on LOCAL indices; returns local index lists.
+template <typename Adj>
+void dfs_components(int n, Adj adj_next, std::vector<std::vector<int>>& comps) {
+  std::vector<char> seen((size_t)n, 0);
+  std::vector<std::pair<int, int>> stack;
+  for (int i = 0; i < n; ++i) {
+    if (seen[i]) continue;
+    comps.emplace_back();
+    auto& comp = comps.back();
+    seen[i] = 1;
+    comp.push_back(i);
+    stack.assign(1, {i, 0});
+    while (!stack.empty()) {
+      auto& top = stack.back();
+      const int nb = adj_next(top.first, top.second, seen);   // next unseen neighbour >= cursor
+      if (nb < 0) {
+        stack.pop_back();
+        continue;
+      }
+      top.second = nb + 1;
+      seen[nb] = 1;
+      comp.push_back(nb);
+      stack.push_back({nb, 0});
+    }
+  }
+}
+
+struct PostOut {
+  std::vector<std::vector<int>> pos;                 // global ids, DFS preorder
+  std::vector<std::vector<std::vector<int>>> ori;    // per position cluster
+  std::vector<double> orient;                        // final orientation per cluster
+  std::vector<double> pose;                          // 6 per cluster
+};
+
+int run_post(sod_ctx* ctx, int32_t n, const double* means_host, PostOut& out) {
+  if (n <= 0) return SOD_OK;
+  const int words = (n + 63) / 64;
+  DevBuf<double> dm;
+  DevBuf<uint64_t> dpos, dori;
+  int rc = sod_reserve(ctx, dm, (size_t)n * 6);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, dpos, (size_t)n * words);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, dori, (size_t)n * words);
+  std::vector<uint64_t> pos((size_t)n * words), ori((size_t)n * words);
+  if (rc == SOD_OK) {
+    hipError_t e = hipMemcpyAsync(dm.p, means_host, (size_t)n * 6 * sizeof(double),
+                                  hipMemcpyHostToDevice, ctx->stream);
+    const int64_t threads = (int64_t)n * words;
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(post_adjacency_kernel, dim3((unsigned)((threads + 255) / 256)),
+                         dim3(256), 0, ctx->stream, n, words, dm.p, dpos.p, dori.p);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(pos.data(), dpos.p, pos.size() * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(ori.data(), dori.p, ori.size() * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, std::string("post-processing: ") + hipGetErrorString(e));
+  }
+  sod_release(dm);
+  sod_release(dpos);
+  sod_release(dori);
+  if (rc != SOD_OK) return rc;
+
+  // position clusters: neighbours of a node = set bits of its row, ascending
+  auto pos_next = [&](int node, int from, const std::vector<char>& seen) -> int {
+    const uint64_t* row = pos.data() + (size_t)node * words;
+    for (int w = from >> 6; w < words; ++w) {
+      uint64_t bits = row[w];
+      if (w == (from >> 6)) bits &= ~0ull << (from & 63);
+      while (bits) {
+        const int j = w * 64 + __builtin_ctzll(bits);
+        if (!seen[j]) return j;
+        bits &= bits - 1;
+      }
+    }
+    return -1;
+  };
+  dfs_components(n, pos_next, out.pos);
+
+  for (const auto& cl : out.pos) {
+    // orientation clusters in the cluster's own indexing (local k -> global cl[k])
+    const int nc = (int)cl.size();
+    auto ori_next = [&](int k, int from, const std::vector<char>& seen) -> int {
+      const uint64_t* row = ori.data() + (size_t)cl[k] * words;
+      for (int m = from; m < nc; ++m) {
+        if (m == k || seen[m]) continue;
+        const int g = cl[m];
+        if ((row[g >> 6] >> (g & 63)) & 1) return m;
+      }
+      return -1;
+    };
+    std::vector<std::vector<int>> local;
+    dfs_components(nc, ori_next, local);
+    out.ori.emplace_back();
+    for (auto& comp : local) {
+      for (auto& k : comp) k = cl[k];
+      out.ori.back().push_back(std::move(comp));
+    }
+    // find_max_orientation: the last largest cluster's mean angle, summed in order
+    size_t max_vote = 0;
+    double final_o = 0;
+    for (const auto& comp : out.ori.back()) {
+      if (comp.size() >= max_vote) {
+        max_vote = comp.size();
+        double acc = 0;
+        for (int g : comp) acc += means_host[6 * g + 2];
+        final_o = acc / (double)comp.size();
+      }
+    }
+    out.orient.push_back(final_o);
+    // get_final_pose
+    double mx = 0, my = 0, ms = 0, min_area = INFINITY, mw = 0, mh = 0;
+    for (int g : cl) {
+      const double* r = means_host + 6 * g;
+      mx += r[0];
+      my += r[1];
+      ms += r[3];
+      const double area = (r[4] * r[3]) * (r[5] * r[3]);
+      if (area < min_area) {
+        min_area = area;
+        mw = r[4];
+        mh = r[5];
+      }
+    }
+    const double len = (double)cl.size();
+    const double p[6] = {mx / len, my / len, final_o, ms / len, mw, mh};
+    out.pose.insert(out.pose.end(), p, p + 6);
+  }
+  return SOD_OK;
+}
+
+int write_post(const PostOut& o, int32_t* n_pos, int32_t* pos_off, int32_t* pos_members,
+               int32_t* n_ori, int32_t* ori_pos_off, int32_t* ori_off, int32_t* ori_members,
+               double* final_orientation, double* final_pose) {
+  int32_t np_ = 0, no = 0, pm = 0, om = 0;
+  if (pos_off) pos_off[0] = 0;
+  if (ori_pos_off) ori_pos_off[0] = 0;
+  if (ori_off) ori_off[0] = 0;
+  for (size_t c = 0; c < o.pos.size(); ++c) {
+    for (int g : o.pos[c])
+      if (pos_members) pos_members[pm++] = g;
+      else ++pm;
+    ++np_;
+    if (pos_off) pos_off[np_] = pm;
+    for (const auto& comp : o.ori[c]) {
+      for (int g : comp)
+        if (ori_members) ori_members[om++] = g;
+        else ++om;
+      ++no;
+      if (ori_off) ori_off[no] = om;
+    }
+    if (ori_pos_off) ori_pos_off[np_] = no;
+    if (final_orientation) final_orientation[c] = o.orient[c];
+    if (final_pose) std::memcpy(final_pose + 6 * c, o.pose.data() + 6 * c, 6 * sizeof(double));
+  }
+  if (n_pos) *n_pos = np_;
+  if (n_ori) *n_ori = no;
+  return SOD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sod_post_batch(sod_ctx* ctx, int32_t n, const double* means, int32_t* n_pos,
+                   int32_t* pos_off, int32_t* pos_members, int32_t* n_ori,
+                   int32_t* ori_pos_off, int32_t* ori_off, int32_t* ori_members,
+                   double* final_orientation, double* final_pose) {
+  if (!ctx) return SOD_EINVAL;
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  if (n < 0 || (n > 0 && !means)) return sod_fail(ctx, SOD_EINVAL, "bad post-processing input");
+  if (n > (1 << 20)) return sod_fail(ctx, SOD_EINVAL, "too many bins for post-processing");
+  PostOut o;
+  SOD_TRY(run_post(ctx, n, means, o));
+  return write_post(o, n_pos, pos_off, pos_members, n_ori, ori_pos_off, ori_off, ori_members,
+                    final_orientation, final_pose);
+}
+
+int sod_postprocess(sod_ctx* ctx, int32_t* n_bins, int32_t* bin_index, int32_t* n_pos,
+                    int32_t* pos_off, int32_t* pos_members, int32_t* n_ori,
+                    int32_t* ori_pos_off, int32_t* ori_off, int32_t* ori_members,
+                    double* final_orientation, double* final_pose) {
+  int64_t V, M;
+  SOD_TRY(sod_valid_counts(ctx, &V, &M));   // joins the side stream (PoseBin means)
+  std::vector<double> means((size_t)V * 6);
+  std::vector<uint8_t> surv((size_t)V, 1);
+  if (V) {
+    SOD_HIP(ctx, hipMemcpyAsync(means.data(), ctx->means.p, means.size() * 8,
+                                hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->affined)   // main.py:155: post_process runs on the bins that survived
+      SOD_HIP(ctx, hipMemcpyAsync(surv.data(), ctx->surv.p, (size_t)V, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  std::vector<double> sel;
+  std::vector<int32_t> idx;
+  for (int64_t v = 0; v < V; ++v)
+    if (surv[(size_t)v]) {
+      idx.push_back((int32_t)v);
+      sel.insert(sel.end(), means.begin() + 6 * v, means.begin() + 6 * v + 6);
+    }
+  const int32_t n = (int32_t)idx.size();
+  if (n_bins) *n_bins = n;
+  if (bin_index && n) std::memcpy(bin_index, idx.data(), (size_t)n * sizeof(int32_t));
+  PostOut o;
+  SOD_TRY(run_post(ctx, n, sel.data(), o));
+  return write_post(o, n_pos, pos_off, pos_members, n_ori, ori_pos_off, ori_off, ori_members,
+                    final_orientation, final_pose);
+}
+
+}  // extern "C"

@@ -188,20 +188,31 @@ class Main:
         self.update_keypoint_pairs()
 
     def post_process(self):
-        raise NotImplementedError(
-            "post-processing (PostProcessing.py) is outside this build's hot path "
-            "(SURVEY.md §8(f), next row 1)")
+        """``main.py:159-168`` on ``self.valid_bins``: position clusters, orientation
+        clusters, dominant orientation, final pose (pairwise relations on the device)."""
+        from .postprocessing import (find_max_orientation, get_final_pose, group_orientation,
+                                     group_position)
+        pose_cluster = group_position(self.valid_bins, self.ctx)
+        orientation_cluster = group_orientation(pose_cluster, self.ctx)
+        final_orientation_list = find_max_orientation(orientation_cluster)
+        self.final_pose = get_final_pose(pose_cluster, final_orientation_list)
 
     # ---------------------------------------------------------------- fused
-    def run(self, bins=15, vote_threshold=5, affine_threshold=4, ratio=0.75, run_affine=True):
+    def run(self, bins=15, vote_threshold=5, affine_threshold=4, ratio=0.75, run_affine=True,
+            post_process=True):
         """The whole path on one stream, results left on the device; returns a dict of
-        arrays (matches, valid bins, members, means, affine survivors/params)."""
+        arrays (matches, valid bins, members, means, affine survivors/params, and the
+        post-processing clusters / final poses)."""
         self.ctx.pipeline(self.rgb_query.shape, bins, ratio, vote_threshold, affine_threshold,
                           POS_FACTOR * 4.0, POS_FACTOR * 4.0, run_affine)
         idx1, d1, d2, good = self.ctx.match_result()
         out = {"idx1": idx1, "d1": d1, "d2": d2, "good": good, "valid": self.ctx.valid_result()}
         if run_affine:
             out["affine"] = self.ctx.affine_result()
+        if post_process:
+            from .postprocessing import final_pose_from_arrays
+            out["post"] = self.ctx.postprocess()
+            self.final_pose = final_pose_from_arrays(out["post"])
         self._match = (idx1, good)
         self._hough_bins = bins
         return out

@@ -220,6 +220,71 @@ def edge_case(rng):
     return qkp, dbkp, img, cen, size, matches
 
 
+def post_case(rng, n, n_centers, spread, ang_spread, field=(1000, 800)):
+    """Synthetic PoseBin means (x, y, angle, scale, w, h) for the post-processing stage:
+    positions around n_centers centres (spread in units of the w*s/4 threshold, so
+    clusters chain, touch and separate), angles around per-centre values (spread in
+    degrees around the 1 degree threshold), model sizes / scales like the DB's."""
+    cx = rng.uniform(0, field[0], n_centers)
+    cy = rng.uniform(0, field[1], n_centers)
+    ca = rng.uniform(0, 2 * math.pi, n_centers)
+    c = rng.integers(0, n_centers, n)
+    s = 2.0 ** rng.integers(-1, 2, n) * rng.uniform(0.9, 1.1, n)
+    w = rng.choice([1500.0, 1200.0, 900.0], n)
+    h = rng.uniform(800, 1200, n)
+    x = cx[c] + rng.normal(0, spread, n) * w * s / 4
+    y = cy[c] + rng.normal(0, spread, n) * h * s / 4
+    a = ca[c] + np.radians(rng.normal(0, ang_spread, n))
+    return np.stack([x, y, a, s, w, h], 1)
+
+
+def post_edge_case():
+    """Exact threshold equalities, orientation-cluster size ties (the LAST largest wins),
+    equal minimum areas (the FIRST wins), a singleton."""
+    rows = [
+        # x, y, angle, scale, w, h
+        (100.0, 100.0, 1.0, 1.0, 1500.0, 1000.0),
+        (475.0, 100.0, 1.0, 1.0, 1500.0, 1000.0),     # |dx| == 1500*1/4: close
+        (850.0000000001, 100.0, 1.0, 1.0, 1500.0, 1000.0),   # just beyond 475 + 375
+        (100.0, 350.0, 1.0 + math.radians(1.0), 1.0, 1500.0, 1000.0),  # |dy| == 250
+        (100.0, 350.0, 1.0 + math.radians(2.5), 1.0, 1500.0, 1000.0),
+        (100.0, 350.0, 1.0 + math.radians(2.5), 1.0, 1500.0, 1000.0),
+        (3000.0, 3000.0, 0.5, 2.0, 900.0, 800.0),      # far away: own cluster
+        (3000.0, 3000.0, 0.5 + math.radians(5.0), 2.0, 900.0, 800.0),
+        (3000.0, 3000.0, 0.5 + math.radians(10.0), 1.0, 1800.0, 1600.0),  # equal area
+        (9000.0, 9000.0, 0.0, 0.5, 1500.0, 800.0),     # singleton
+    ]
+    return np.array(rows, np.float64)
+
+
+def run_post(ref_pp, ref_pb, means):
+    bins = [ref_pb.PoseBin((0, 0, 0, 0), (float(r[4]), float(r[5])), 1, [],
+                           (float(r[0]), float(r[1]), float(r[2]), float(r[3])))
+            for r in means]
+    ident = {id(b): i for i, b in enumerate(bins)}
+    pc = ref_pp.group_position(bins)
+    oc = ref_pp.group_orientation(pc)
+    fo = ref_pp.find_max_orientation(oc)
+    fp = ref_pp.get_final_pose(pc, fo)
+    pos_off, pos_mem = [0], []
+    for cl in pc:
+        pos_mem.extend(ident[id(b)] for b in cl)
+        pos_off.append(len(pos_mem))
+    ori_pos_off, ori_off, ori_mem = [0], [0], []
+    for clusters in oc:
+        for comp in clusters:
+            ori_mem.extend(ident[id(b)] for b in comp)
+            ori_off.append(len(ori_mem))
+        ori_pos_off.append(len(ori_off) - 1)
+    return dict(means=means, pos_off=np.array(pos_off, np.int32),
+                pos_members=np.array(pos_mem, np.int32),
+                ori_pos_off=np.array(ori_pos_off, np.int32),
+                ori_off=np.array(ori_off, np.int32), ori_members=np.array(ori_mem, np.int32),
+                final_orientation=np.array(fo, np.float64),
+                final_pose=np.array([[p[0][0], p[0][1], p[1], p[2], float(p[3][0]),
+                                      float(p[3][1])] for p in fp], np.float64).reshape(-1, 6))
+
+
 def save(name, **arrays):
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **arrays)
@@ -281,6 +346,20 @@ def main():
              match_q=np.array([q for q, _ in matches], np.int32),
              match_m=np.array([m for _, m in matches], np.int32),
              **kp_arrays("q_", qkp), **kp_arrays("db_", dbkp), **out)
+
+    # ---- post-processing (section 8(f) row 1): reference PostProcessing on PoseBins ----
+    import PostProcessing as ref_pp  # noqa: E402
+    import PoseBin as ref_pb  # noqa: E402
+    prng = np.random.default_rng(77)
+    post = {"post_edge": post_edge_case(),
+            "post_small": post_case(prng, 40, 6, 1.0, 1.0),
+            "post_medium": post_case(prng, 400, 25, 0.8, 0.8, (12000, 9000)),
+            "post_chain": post_case(prng, 300, 3, 2.5, 2.0)}
+    for name, means in post.items():
+        out = run_post(ref_pp, ref_pb, means)
+        print(name, "bins", len(means), "position clusters", len(out["final_pose"]),
+              "orientation clusters", len(out["ori_off"]) - 1)
+        save(name, **out)
 
     # ---- matcher edge cases (int64 brute force; OpenCV absent: unpinned) ----
     rng = np.random.default_rng(5)

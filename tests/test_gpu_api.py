@@ -107,6 +107,9 @@ def test_main_stages_match_golden():
     for b, prm in zip(m.valid_bins, g["surv_params"]):
         np.testing.assert_allclose(b.affine_parameters, prm, rtol=0, atol=1e-4)
     assert len(m.keypoint_pairs) == int(g["surv_votes"].sum())
+    m.post_process()                                   # main.py:186
+    got = np.array([[p[0][0], p[0][1], p[1], p[2], p[3][0], p[3][1]] for p in m.final_pose])
+    np.testing.assert_allclose(got.reshape(-1, 6), g["final_pose"], rtol=1e-12, atol=1e-9)
 
 
 class ThreadComm:
