@@ -171,6 +171,24 @@ def cpu_hough_baseline(qs, kp_all, img, cent, size, idx1, good, bins):
                       "%d votes, %.1f s" % (len(matches), votes, dt)}
 
 
+def cpu_post_baseline(ctx, post):
+    """The oracle's restatement of PostProcessing.py (pure Python, like the reference) on
+    the same surviving bins' PoseBin means."""
+    from oracle import oracle as orc
+    means = ctx.valid_result()["means"][post["bin_index"]]
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        orc.post_process(means)
+        reps += 1
+        if time.perf_counter() - t0 > 0.5:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": dt * 1000.0, "unit": "ms", "cores": 1, "kind": "port",
+            "sample": "oracle PostProcessing (Python, PostProcessing.py:4-112) on the %d "
+                      "surviving bins, mean of %d runs" % (len(means), reps)}
+
+
 def pmc_traffic(kernel, config):
     """HBM bytes per matcher launch from the committed PMC summary of the same kernel and
     workload (profiles/*_pmc_<kernel>_<config>.json, from tools/gpu_pmc.sh +
@@ -272,6 +290,15 @@ def main():
     match_ms = float(np.mean(match_ms))
     stage = np.mean(np.array(stage), axis=0)
 
+    # post-processing (main.py:159-168) over the surviving bins: timed
+    # separately (it ends in a host DFS, so it is not inside the stream-ordered step)
+    post_ms = None
+    post = None
+    if run_affine:
+        t0 = time.perf_counter()
+        for _ in range(5):
+            post = ctx.postprocess()
+        post_ms = 1000.0 * (time.perf_counter() - t0) / 5
     V, M = ctx.valid_counts()
     keys, votes = ctx.all_bins()
     n_votes = int(votes.sum())
@@ -313,7 +340,8 @@ def main():
         "surviving_bins": int(aff["survived"].sum()) if aff else None,
         "stage_ms": {"match_kernel": match_ms, "merge_gather_ratio": float(stage[1]),
                      "hough_vote": float(stage[2]), "select": float(stage[3]),
-                     "affine": float(stage[4])},
+                     "affine": float(stage[4]), "post_process": post_ms},
+        "final_poses": int(len(post["final_pose"])) if post is not None else None,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
                      "unit": peak_unit, "frac": achieved / peak, "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, 2*FETCH_SIZE+WRITE_SIZE)",
@@ -329,6 +357,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(qs.des, shard, a.cpu_queries)
         out["cpu_baseline_hough"] = cpu_hough_baseline(qs, (x, y, ang, octv), img, cent, size,
                                                        idx1, good, bins)
+        if post is not None:
+            out["cpu_baseline_post"] = cpu_post_baseline(ctx, post)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -64,6 +64,14 @@ int sod_db_set_keypoints(sod_ctx* ctx, int64_t n_total, const float* x, const fl
 int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t n,
                               int64_t row_offset);
 
+/* ---- packed DB image (replaces the GenerateDatabaseInfo.py:35 pickle
+ * + main.py:53-66 flattening as the descriptor store): the device's own fragment layout
+ * with its norm words behind a 64-byte header, so a later upload is one copy (no
+ * validation / packing pass).  The image is tied to the matcher impl it was packed for. */
+int sod_db_packed_size(sod_ctx* ctx, int64_t* bytes);
+int sod_db_export_packed(sod_ctx* ctx, void* out, int64_t bytes);
+int sod_db_import_packed(sod_ctx* ctx, const void* in, int64_t bytes);
+
 /* ---- query image features (replaces main.py:43 detectAndCompute output) ---------- */
 int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq,
                      const float* x, const float* y, const float* angle,

@@ -50,6 +50,9 @@ SIGNATURES = {
     "sod_db_set_keypoints": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_i32p,
                                        C.c_int32, c_f64p, c_i32p]),
     "sod_db_upload_descriptors": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int64, C.c_int64]),
+    "sod_db_packed_size": (C.c_int, [c_ctx, c_i64p]),
+    "sod_db_export_packed": (C.c_int, [c_ctx, c_vp, C.c_int64]),
+    "sod_db_import_packed": (C.c_int, [c_ctx, c_vp, C.c_int64]),
     "sod_query_upload": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int32, c_f32p, c_f32p, c_f32p,
                                    c_i32p]),
     "sod_match_enqueue": (C.c_int, [c_ctx]),
@@ -462,6 +465,19 @@ class Context:
         r["pos_members"] = r["pos_members"][:n]
         r["ori_members"] = r["ori_members"][:n]
         return r
+
+    def export_packed(self):
+        """The DB shard as a packed image (uint8 array): header + fragments + norm words."""
+        n = C.c_int64(0)
+        self._chk(self._L.sod_db_packed_size(self._h, C.byref(n)))
+        out = np.empty(n.value, np.uint8)
+        self._chk(self._L.sod_db_export_packed(self._h, out.ctypes.data_as(c_vp), n.value))
+        return out
+
+    def import_packed(self, image):
+        """Upload a packed DB image (one host->device copy, no packing pass)."""
+        a = np.ascontiguousarray(image, np.uint8)
+        self._chk(self._L.sod_db_import_packed(self._h, a.ctypes.data_as(c_vp), a.size))
 
     def comm_init(self, nranks, rank, uid):
         buf = (C.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(uid)

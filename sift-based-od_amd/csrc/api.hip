@@ -116,6 +116,7 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->allbin); sod_release(ctx->amx); sod_release(ctx->amy); sod_release(ctx->aqx);
   sod_release(ctx->aqy); sod_release(ctx->aisig); sod_release(ctx->surv);
   sod_release(ctx->fvotes); sod_release(ctx->params); sod_release(ctx->alive);
+  sod_release(ctx->post_m); sod_release(ctx->post_pos); sod_release(ctx->post_ori);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
@@ -223,6 +224,101 @@ int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
   SOD_TRY(upload_descriptors(ctx, des, dtype, n, true));
   ctx->n_shard = n;
   ctx->row_offset = row_offset;
+  ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+// ---- packed DB image (DB on-disk format, upload = one memcpy) -----
+// [header 64 B][packed descriptor fragments][norm words]; the fragment and norm layouts are
+// the matcher's own (see match_i8.hip / match.hip), so an import is a plain copy.
+namespace {
+struct PackedHeader {
+  char magic[8];        // "SODPK01\0"
+  int32_t impl;         // matcher layout the image was packed for
+  int32_t sub_bytes;    // bytes per subtile
+  int64_t n_rows;       // real descriptor rows
+  int64_t row_offset;   // global index of row 0
+  int64_t nsub;         // subtiles (padded)
+  int64_t norm_bytes;   // bytes of norm words
+  uint32_t max_norm;    // raw max ||d||^2 (float bits) for sod_match_exact_order
+  uint32_t pad[3];
+};
+static_assert(sizeof(PackedHeader) == 64, "header is 64 bytes");
+
+int packed_layout(const sod_ctx* ctx, int* sub_bytes, int64_t* norm_bytes) {
+  const int rows = ctx->impl == 2 ? 32 : kSubRows;
+  *sub_bytes = ctx->impl == 0 ? kSubBytes : rows * kDim;   // bf16 4 KiB, int8 rows*128 B
+  const int64_t npad = ctx->nsub * rows;
+  // int8: c and parity words (2 x i32 per row); bf16: one f32 norm per row
+  *norm_bytes = ctx->impl == 0 ? npad * 4 : npad * 8;
+  return SOD_OK;
+}
+}  // namespace
+
+int sod_db_packed_size(sod_ctx* ctx, int64_t* bytes) {
+  SOD_TRY(set_dev(ctx));
+  if (!ctx->nsub) return sod_fail(ctx, SOD_ESTATE, "no descriptors uploaded");
+  int sb;
+  int64_t nb;
+  packed_layout(ctx, &sb, &nb);
+  *bytes = (int64_t)sizeof(PackedHeader) + ctx->nsub * sb + nb;
+  return SOD_OK;
+}
+
+int sod_db_export_packed(sod_ctx* ctx, void* out, int64_t bytes) {
+  int64_t need;
+  SOD_TRY(sod_db_packed_size(ctx, &need));
+  if (!out || bytes < need) return sod_fail(ctx, SOD_EINVAL, "output buffer too small");
+  int sb;
+  int64_t nb;
+  packed_layout(ctx, &sb, &nb);
+  PackedHeader h{};
+  std::memcpy(h.magic, "SODPK01", 8);
+  h.impl = ctx->impl;
+  h.sub_bytes = sb;
+  h.n_rows = ctx->n_shard;
+  h.row_offset = ctx->row_offset;
+  h.nsub = ctx->nsub;
+  h.norm_bytes = nb;
+  uint8_t* o = static_cast<uint8_t*>(out);
+  SOD_HIP(ctx, hipMemcpyAsync(&h.max_norm, ctx->flags.p + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(o + sizeof(h), ctx->dbpack.p, (size_t)(ctx->nsub * sb),
+                              hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(o + sizeof(h) + ctx->nsub * sb, ctx->dn.p, (size_t)nb,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  std::memcpy(o, &h, sizeof(h));
+  return SOD_OK;
+}
+
+int sod_db_import_packed(sod_ctx* ctx, const void* in, int64_t bytes) {
+  SOD_TRY(set_dev(ctx));
+  PackedHeader h;
+  if (!in || bytes < (int64_t)sizeof(h)) return sod_fail(ctx, SOD_EINVAL, "not a packed DB image");
+  std::memcpy(&h, in, sizeof(h));
+  if (std::memcmp(h.magic, "SODPK01", 8) != 0) return sod_fail(ctx, SOD_EINVAL, "not a packed DB image");
+  if (h.impl != ctx->impl)
+    return sod_fail(ctx, SOD_EINVAL, "packed for matcher impl " + std::to_string(h.impl) +
+                                         ", context uses " + std::to_string(ctx->impl));
+  const int rows = ctx->impl == 2 ? 32 : kSubRows;
+  const int want_sb = ctx->impl == 0 ? kSubBytes : rows * kDim;
+  const int64_t want_nb = (ctx->impl == 0 ? 4 : 8) * h.nsub * rows;
+  if (h.sub_bytes != want_sb || h.norm_bytes != want_nb || h.nsub < 1 || h.n_rows < 1 ||
+      h.n_rows > h.nsub * rows || h.row_offset < 0 || h.row_offset + h.n_rows > 0x7fffffffLL ||
+      bytes < (int64_t)sizeof(h) + h.nsub * h.sub_bytes + h.norm_bytes)
+    return sod_fail(ctx, SOD_EINVAL, "inconsistent packed DB image");
+  const uint8_t* src = static_cast<const uint8_t*>(in) + sizeof(h);
+  SOD_TRY(sod_reserve(ctx, ctx->dbpack, (size_t)(h.nsub * h.sub_bytes)));
+  SOD_TRY(sod_reserve(ctx, ctx->dn, (size_t)(h.norm_bytes / 4)));
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->dbpack.p, src, (size_t)(h.nsub * h.sub_bytes),
+                              hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->dn.p, src + h.nsub * h.sub_bytes, (size_t)h.norm_bytes,
+                              hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->flags.p + 1, &h.max_norm, 4, hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->nsub = h.nsub;
+  ctx->n_shard = h.n_rows;
+  ctx->row_offset = h.row_offset;
   ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
 }

@@ -89,8 +89,9 @@ struct PostOut {
 int run_post(sod_ctx* ctx, int32_t n, const double* means_host, PostOut& out) {
   if (n <= 0) return SOD_OK;
   const int words = (n + 63) / 64;
-  DevBuf<double> dm;
-  DevBuf<uint64_t> dpos, dori;
+  DevBuf<double>& dm = ctx->post_m;
+  DevBuf<uint64_t>& dpos = ctx->post_pos;
+  DevBuf<uint64_t>& dori = ctx->post_ori;
   int rc = sod_reserve(ctx, dm, (size_t)n * 6);
   if (rc == SOD_OK) rc = sod_reserve(ctx, dpos, (size_t)n * words);
   if (rc == SOD_OK) rc = sod_reserve(ctx, dori, (size_t)n * words);
@@ -111,9 +112,6 @@ int run_post(sod_ctx* ctx, int32_t n, const double* means_host, PostOut& out) {
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, std::string("post-processing: ") + hipGetErrorString(e));
   }
-  sod_release(dm);
-  sod_release(dpos);
-  sod_release(dori);
   if (rc != SOD_OK) return rc;
 
   // position clusters: neighbours of a node = set bits of its row, ascending

@@ -107,6 +107,10 @@ struct sod_ctx {
   DevBuf<uint8_t> alive;        // [mmax]
   bool affined = false;
 
+  // ---- post-processing (post.hip) ----
+  DevBuf<double> post_m;        // [n*6] bin means
+  DevBuf<uint64_t> post_pos, post_ori;   // [n * ceil(n/64)] relation bitmasks
+
   // ---- comm ----
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;

@@ -81,19 +81,67 @@ class SiftDatabase:
     img: np.ndarray
     centroid: np.ndarray
     size: np.ndarray
+    packed: np.ndarray | None = None   # device image (Context.export_packed), optional
 
     def __post_init__(self):
-        self.des = np.ascontiguousarray(self.des)
-        if self.des.ndim != 2 or self.des.shape[1] != DESC_DIM:
-            raise ValueError("descriptors must be [N,128]")
         self.img = np.ascontiguousarray(self.img, np.int32)
         self.centroid = np.ascontiguousarray(self.centroid, np.float64).reshape(-1, 2)
         self.size = np.ascontiguousarray(self.size, np.int32).reshape(-1, 2)
-        if len(self.kp) != self.des.shape[0] or self.img.shape[0] != self.des.shape[0]:
-            raise ValueError("descriptor / keypoint / image-id counts differ")
+        if self.des is None:
+            if self.packed is None:
+                raise ValueError("need descriptors or a packed image")
+        else:
+            self.des = np.ascontiguousarray(self.des)
+            if self.des.ndim != 2 or self.des.shape[1] != DESC_DIM:
+                raise ValueError("descriptors must be [N,128]")
+            if self.img.shape[0] != self.des.shape[0]:
+                raise ValueError("descriptor / image-id counts differ")
+        if len(self.kp) != self.img.shape[0]:
+            raise ValueError("keypoint / image-id counts differ")
 
     def __len__(self):
-        return int(self.des.shape[0])
+        return int(self.img.shape[0])
+
+    # ---- on-disk format -------------------------------------------
+    def save(self, path, ctx=None, keep_descriptors=True):
+        """Write the flat database as one ``.npz`` (plain arrays, no pickle): keypoint SoA,
+        image table, and -- when a context is given -- the device-packed descriptor image
+        of the whole DB (``Context.export_packed``), so :meth:`upload` is a single copy.
+        The reference stores a pickle of per-image records instead
+        (``GenerateDatabaseInfo.py:35``)."""
+        arrays = dict(x=self.kp.x, y=self.kp.y, angle=self.kp.angle, octave=self.kp.octave,
+                      img=self.img, centroid=self.centroid, size=self.size)
+        if keep_descriptors and self.des is not None:
+            arrays["des"] = np.asarray(self.des, np.uint8)
+        if ctx is not None and self.des is not None:
+            ctx.upload_db(self.des)
+            arrays["packed"] = ctx.export_packed()
+        elif self.packed is not None:
+            arrays["packed"] = self.packed
+        np.savez(path, **arrays)
+
+    @classmethod
+    def load(cls, path):
+        """Read a file written by :meth:`save` (``numpy.load``, pickles refused)."""
+        with np.load(path, allow_pickle=False) as z:
+            kp = Keypoints(z["x"], z["y"], z["angle"], z["octave"])
+            des = z["des"] if "des" in z.files else None
+            packed = z["packed"] if "packed" in z.files else None
+            return cls(des, kp, z["img"], z["centroid"], z["size"], packed)
+
+    def upload(self, ctx):
+        """Keypoints + image table, then the descriptors: the packed image in one copy when
+        present and laid out for the context's matcher, else the upload + pack pass."""
+        from ._lib import SodError
+        ctx.set_keypoints(self.kp, self.img, self.centroid, self.size)
+        if self.packed is not None:
+            try:
+                ctx.import_packed(self.packed)
+                return
+            except SodError:   # packed for another matcher impl: pack from descriptors
+                if self.des is None:
+                    raise
+        ctx.upload_db(self.des)
 
     @property
     def n_images(self):

@@ -57,13 +57,15 @@ class Main:
     # ---------------------------------------------------------------- inputs
     def set_database(self, db):
         """The flattened training database (``main.py:53-66``): a :class:`SiftDatabase`
-        or the reference's pickle payload (list of per-image records)."""
+        (e.g. ``SiftDatabase.load`` of a saved file, packed image included), a path to such
+        a file, or the reference's pickle payload (list of per-image records)."""
+        if isinstance(db, (str, bytes)) or hasattr(db, "__fspath__"):
+            db = SiftDatabase.load(db)
         if not isinstance(db, SiftDatabase):
             db = SiftDatabase.from_records(db)
         self.db = db
         self.des = db.des
-        self.ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
-        self.ctx.upload_db(db.des)
+        db.upload(self.ctx)
         self.kp = _LazyKeypoints(self, "db")
 
     def get_query_features(self, des_query, kp_query, image_shape, database=None):

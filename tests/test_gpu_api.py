@@ -209,3 +209,37 @@ def test_rccl_single_rank_collectives():
     assert np.array_equal(b0[0], b1[0]) and np.array_equal(b0[1], b1[1])
     assert np.array_equal(a0["survived"], a1["survived"])
     assert np.array_equal(a0["params"], a1["params"])
+
+
+@pytest.mark.parametrize("impl", ["i8", "bf16", "i8w"])
+def test_packed_db_roundtrip(tmp_path, impl):
+    """save the DB with its device-packed image, load it (no pickle) and
+    upload with one copy -- the pipeline results equal the upload + pack path's."""
+    db = synthetic.make_database(10, 400, seed=51)
+    qs = synthetic.make_queries(2500, seed=52, db_seed=51, kp_per_image=400)
+    with _lib.Context(0) as c:
+        c.set_impl(impl)
+        path = tmp_path / "db.npz"
+        db.save(path, ctx=c, keep_descriptors=False)
+        loaded = sod.SiftDatabase.load(path)
+        assert loaded.des is None and loaded.packed is not None
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        c.upload_queries(qs.des, qs.kp)
+        c.pipeline(qs.shape, 15)
+        ref = (c.match_result(), c.valid_result())
+    with _lib.Context(0) as c:
+        c.set_impl(impl)
+        loaded.upload(c)
+        c.upload_queries(qs.des, qs.kp)
+        c.pipeline(qs.shape, 15)
+        got = (c.match_result(), c.valid_result())
+        assert c.exact_order()
+        other = "bf16" if impl != "bf16" else "i8"
+        c.set_impl(other)
+        with pytest.raises(_lib.SodError):
+            c.import_packed(loaded.packed)      # laid out for another matcher
+    for x, y in zip(ref[0], got[0]):
+        assert np.array_equal(x, y)
+    for k in ("keys", "votes", "offsets", "members"):
+        assert np.array_equal(ref[1][k], got[1][k])
