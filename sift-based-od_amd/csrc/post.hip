@@ -51,8 +51,9 @@ __global__ void post_adjacency_kernel(int n, int words, const double* __restrict
   ori[t] = ob;
 }
 
-// Components in the order of the reference's recursive dfs, over the nodes `nodes`
-// (global ids) with neighbour test `adj(a, b)` on LOCAL indices; returns local index lists.
+// Components over indices 0..n-1 in the order of the reference's recursive dfs started
+// from every unseen index in order; adj_next(node, from, seen) returns the node's next
+// unseen neighbour >= from (neighbours ascending) or -1.
 template <typename Adj>
 void dfs_components(int n, Adj adj_next, std::vector<std::vector<int>>& comps) {
   std::vector<char> seen((size_t)n, 0);
