@@ -77,6 +77,14 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq,
                      const float* x, const float* y, const float* angle,
                      const int32_t* octave);   /* des may be NULL: keypoints only */
 
+/* ---- query batching -------------------------------------------
+ * Upload the keypoints/descriptors of several query images back to back, match and
+ * ratio-test them in ONE pass over the DB, then run the per-image stages (Hough, select,
+ * affine, post-processing) with the window set to each image's query range [first,
+ * first+count); member lists then hold window-local query indices.  count < 0 restores
+ * the whole query set (the default after sod_query_upload). */
+int sod_query_window(sod_ctx* ctx, int32_t first, int32_t count);
+
 /* ---- A1/A2: cv2.BFMatcher().knnMatch(des_query, des, k=2) + ratio test ------------
  * main.py:70-86.  enqueue: local shard top-2 (exact squared distances), merged over
  * this ctx's descriptor shard. */

@@ -55,6 +55,7 @@ SIGNATURES = {
     "sod_db_import_packed": (C.c_int, [c_ctx, c_vp, C.c_int64]),
     "sod_query_upload": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int32, c_f32p, c_f32p, c_f32p,
                                    c_i32p]),
+    "sod_query_window": (C.c_int, [c_ctx, C.c_int32, C.c_int32]),
     "sod_match_enqueue": (C.c_int, [c_ctx]),
     "sod_match_set_impl": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
@@ -465,6 +466,11 @@ class Context:
         r["pos_members"] = r["pos_members"][:n]
         r["ori_members"] = r["ori_members"][:n]
         return r
+
+    def query_window(self, first=0, count=-1):
+        """Restrict the Hough-side stages to queries [first, first+count) (one image of a
+        batch matched together); count < 0 = all queries."""
+        self._chk(self._L.sod_query_window(self._h, int(first), int(count)))
 
     def export_packed(self):
         """The DB shard as a packed image (uint8 array): header + fragments + norm words."""

@@ -334,6 +334,8 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq, const
     ctx->nqt = 0;  // keypoints only: hough on externally set matches
   }
   ctx->nq = nq;
+  ctx->win0 = 0;
+  ctx->winn = -1;
   if (x && y && angle && octave) {
     SOD_TRY(upload(ctx, ctx->qx, x, (size_t)nq));
     SOD_TRY(upload(ctx, ctx->qy, y, (size_t)nq));
@@ -342,6 +344,22 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq, const
     SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
   ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+// ---- query window (several query images share one matcher pass) --
+int sod_query_window(sod_ctx* ctx, int32_t first, int32_t count) {
+  SOD_TRY(set_dev(ctx));
+  if (count < 0) {
+    ctx->win0 = 0;
+    ctx->winn = -1;
+  } else {
+    if (first < 0 || count < 1 || (int64_t)first + count > ctx->nq)
+      return sod_fail(ctx, SOD_EINVAL, "query window outside the uploaded queries");
+    ctx->win0 = first;
+    ctx->winn = count;
+  }
+  ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
 }
 

@@ -940,7 +940,7 @@ int launch_bin_index_batch(sod_ctx* ctx, int64_t n, const double* pose, int32_t*
 }
 
 int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
-  const int64_t nq = ctx->nq;
+  const int64_t nq = sod_win_n(ctx), q0 = sod_win0(ctx);
   SOD_TRY(sod_reserve(ctx, ctx->pose, (size_t)nq * 4));
   SOD_TRY(sod_reserve(ctx, ctx->basekey, (size_t)nq));
   SOD_TRY(sod_reserve(ctx, ctx->vmask, (size_t)nq));
@@ -950,7 +950,8 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
   SOD_HIP(ctx, hipMemsetAsync(ctx->first.p, 0xFF, ctx->nbins * 4, ctx->stream));
   const int bs = 256;
   hipLaunchKernelGGL(pose_kernel, dim3((unsigned)cdiv(nq, bs)), dim3(bs), 0, ctx->stream, nq,
-                     ctx->good.p, ctx->idx1.p, ctx->qx.p, ctx->qy.p, ctx->qang.p, ctx->qoct.p,
+                     ctx->good.p + q0, ctx->idx1.p + q0, ctx->qx.p + q0, ctx->qy.p + q0,
+                     ctx->qang.p + q0, ctx->qoct.p + q0,
                      ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p,
                      ctx->qh, ctx->qw, ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
                      ctx->basekey.p, ctx->vmask.p);
@@ -964,7 +965,7 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
 
 static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* total_slot,
                           uint32_t* vidx) {
-  const int64_t nq = ctx->nq;
+  const int64_t nq = sod_win_n(ctx);
   const int64_t nblk = cdiv(nq, kSelThreads);
   SOD_TRY(sod_reserve(ctx, ctx->blk, (size_t)nblk));
   hipLaunchKernelGGL(select_count_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream,
@@ -982,7 +983,7 @@ static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* t
 }
 
 int launch_select(sod_ctx* ctx, int32_t thr) {
-  const int64_t nq = ctx->nq;
+  const int64_t nq = sod_win_n(ctx);
   if (thr < 1) thr = 1;  // a bin exists only once voted for
   ctx->vmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * nq));
   ctx->mmax = std::max<int64_t>(1, 16 * nq);
@@ -1021,7 +1022,7 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   SOD_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
   SOD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
   hipLaunchKernelGGL(means_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
-                     ctx->side, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p,
+                     ctx->side, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p + sod_win0(ctx),
                      ctx->mimg.p, ctx->isize.p, ctx->mmax, ctx->mq.p);
   SOD_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(recip_table_kernel, dim3(std::max(1, ctx->num_cus)), dim3(256), 0,
@@ -1036,7 +1037,7 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
 }
 
 int launch_all_bins(sod_ctx* ctx) {
-  const int64_t bmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * (int64_t)ctx->nq));
+  const int64_t bmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * sod_win_n(ctx)));
   SOD_TRY(sod_reserve(ctx, ctx->scal, 4));
   SOD_TRY(sod_reserve(ctx, ctx->allbin, (size_t)bmax));
   return run_compaction(ctx, 1u, ctx->allbin.p, ctx->scal.p + 2, nullptr);
@@ -1049,8 +1050,9 @@ int launch_affine_gather(sod_ctx* ctx) {
   SOD_TRY(sod_reserve(ctx, ctx->aqy, (size_t)ctx->mmax));
   SOD_TRY(sod_reserve(ctx, ctx->aisig, (size_t)ctx->vmax));
   hipLaunchKernelGGL(affine_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
-                     ctx->stream, ctx->scal.p, ctx->members.p, ctx->idx1.p, ctx->mx.p, ctx->my.p,
-                     ctx->qx.p, ctx->qy.p, ctx->vbin.p, ctx_bins(ctx), ctx->amx.p, ctx->amy.p,
+                     ctx->stream, ctx->scal.p, ctx->members.p, ctx->idx1.p + sod_win0(ctx),
+                     ctx->mx.p, ctx->my.p, ctx->qx.p + sod_win0(ctx), ctx->qy.p + sod_win0(ctx),
+                     ctx->vbin.p, ctx_bins(ctx), ctx->amx.p, ctx->amy.p,
                      ctx->aqx.p, ctx->aqy.p, ctx->aisig.p);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;

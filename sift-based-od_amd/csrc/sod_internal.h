@@ -53,6 +53,8 @@ struct sod_ctx {
   DevBuf<float> qn;             // nqt * 16
   DevBuf<float> qx, qy, qang;
   DevBuf<int32_t> qoct;
+  int32_t win0 = 0, winn = -1;  // query window of the Hough / select / affine stages
+                                // (-1 = all queries): one query image of a batch
   DevBuf<uint8_t> stage_u8;     // upload staging for descriptors
   DevBuf<float> stage_f32;
 
@@ -163,6 +165,10 @@ void sod_release(DevBuf<T>& b) {
 }
 
 // kernel launchers implemented in the .hip files ----------------------------------------
+// the query window the Hough-side stages work on (query batching)
+inline int64_t sod_win_n(const sod_ctx* ctx) { return ctx->winn < 0 ? ctx->nq : ctx->winn; }
+inline int64_t sod_win0(const sod_ctx* ctx) { return ctx->winn < 0 ? 0 : ctx->win0; }
+
 // queries covered by the packed query tiles (tile height depends on the matcher)
 inline int64_t sod_nq_pad(const sod_ctx* ctx) { return (int64_t)ctx->nqt * (ctx->impl == 2 ? 32 : kSubRows); }
 int launch_pack_db(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n);

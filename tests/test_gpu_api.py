@@ -243,3 +243,34 @@ def test_packed_db_roundtrip(tmp_path, impl):
         assert np.array_equal(x, y)
     for k in ("keys", "votes", "offsets", "members"):
         assert np.array_equal(ref[1][k], got[1][k])
+
+
+def test_query_batch_equals_per_image():
+    """three query images matched in one DB pass, then per-image
+    Hough / select / affine / post-processing on query windows == each image alone."""
+    db = synthetic.make_database(8, 500, seed=61)
+    imgs = []
+    for k, nq in enumerate((1200, 700, 1500)):
+        qs = synthetic.make_queries(nq, seed=62 + k, db_seed=61, kp_per_image=500,
+                                    n_objects=3)
+        imgs.append((qs.des, qs.kp, qs.shape))
+    with _lib.Context(0) as c:
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        batch = sod.run_query_batch(c, imgs, bins=15)
+        for (des, kp_, shape), b in zip(imgs, batch):
+            c.upload_queries(des, kp_)
+            c.pipeline(shape, 15)
+            i1, d1, d2, g = c.match_result()
+            assert np.array_equal(i1, b["idx1"]) and np.array_equal(d1, b["d1"])
+            assert np.array_equal(d2, b["d2"]) and np.array_equal(g, b["good"])
+            v = c.valid_result()
+            assert len(v["keys"]) > 0
+            for k in ("keys", "votes", "offsets", "members"):
+                assert np.array_equal(v[k], b["valid"][k]), k
+            np.testing.assert_array_equal(v["means"], b["valid"]["means"])
+            a = c.affine_result()
+            assert np.array_equal(a["survived"], b["affine"]["survived"])
+            np.testing.assert_array_equal(a["params"], b["affine"]["params"])
+            p = c.postprocess()
+            np.testing.assert_array_equal(p["final_pose"], b["post"]["final_pose"])
