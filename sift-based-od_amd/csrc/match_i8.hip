@@ -49,11 +49,18 @@ constexpr int QT = 8;          // 16-query tiles per wave
 // in-kernel stamps).
 constexpr int NW16 = SOD_I8_NW;
 constexpr int NT16 = NW16 * 64;
-constexpr int SPS = 8;         // subtiles per stage (128 rows)
+#ifndef SOD_I8_SPS
+#define SOD_I8_SPS 16
+#endif
+#ifndef SOD_I8_UNROLL
+#define SOD_I8_UNROLL 0    // subtile-loop unroll (0 = full)
+#endif
+constexpr int SPS = SOD_I8_SPS;   // subtiles per stage (one barrier per stage)
+constexpr int kStageRows = SPS * 16;
 constexpr int kSub = 2048;     // bytes per 16-row subtile
 constexpr int kStageBytes = SPS * kSub;          // 16 KiB
 // per stage (128 rows) and wave w (rows 32w..32w+31): [c: 32 x i32 | p: 32 x i32]
-constexpr int kStageNorm = 2 * SPS * kSubRows * 4;   // 1 KiB
+constexpr int kStageNorm = 2 * SPS * kSubRows * 4;   // c and parity words
 constexpr int kStageSlot = kStageBytes + kStageNorm;
 constexpr int kPiecesPerWave = kStageBytes / 1024 / NW16;   // 1 KiB LDS-DMA pieces
 constexpr int kPadNormI = 1 << 30;                        // ||d'||^2 of padding rows (w = -2^30)
@@ -138,10 +145,11 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* lds_base) {
 // norms of the stage's 128 rows, wave w of NWx covering rows R*w .. R*w+R-1 (R = 128/NWx):
 // lanes 0..R/4-1 fetch c, the next R/4 lanes parity -> one run [c: R x i32 | p: R x i32]
 // per wave (global_load_lds writes lane i at M0 + 16 i)
-template <int NWx>
+template <int NWx, int kRows>
 __device__ __forceinline__ void issue_norms(const int* __restrict__ dn, int64_t npad, int64_t row0,
                                             uint8_t* slot_norm, int wave, int lane) {
-  constexpr int R = 128 / NWx, L = R / 4;
+  constexpr int R = kRows / NWx, L = R / 4;
+  static_assert(2 * L <= 64 && R % 4 == 0, "one glds per wave covers its norm rows");
   const int* src = dn + (lane < L ? 0 : npad) + row0 + wave * R + (lane % L) * 4;
   if (lane < 2 * L) glds16(src, slot_norm + wave * (8 * R));
 }
@@ -155,12 +163,12 @@ __device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
     const int piece = wave * kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  issue_norms<NW16>(dn, npad, sub0 * kSubRows, slot + kStageBytes, wave, lane);
+  issue_norms<NW16, kStageRows>(dn, npad, sub0 * kSubRows, slot + kStageBytes, wave, lane);
 }
 
 // LDS offset of a 16-row subtile's c for lane group g = lane >> 4 (its 4 rows 16u+4g..);
 // the parity words follow at +kParOff
-constexpr int kNormRows = 128 / NW16;
+constexpr int kNormRows = kStageRows / NW16;
 constexpr int kParOff = 4 * kNormRows;
 __device__ __forceinline__ int norm_off(int u, int g) {
   const int row = 16 * u + 4 * g;
@@ -340,7 +348,11 @@ __device__ __forceinline__ void match_unit(
     i32x4 fa1 = *reinterpret_cast<const i32x4*>(sb + 1024 + lane * 16);
     i32x4 fc = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4));
     i32x4 fp = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4) + kParOff);
+#if SOD_I8_UNROLL
+#pragma unroll SOD_I8_UNROLL
+#else
 #pragma unroll
+#endif
     for (int u = 0; u < SPS; ++u) {
       const i32x4 a0 = fa0, a1 = fa1, c = fc, p = fp;   // c = floor(-||d'||^2 / 2)
       i32x4 acc[QT];
@@ -480,7 +492,7 @@ __device__ __forceinline__ void issue_stage_w(const uint8_t* __restrict__ dbpack
     const int piece = wave * w::kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  issue_norms<w::NW>(dn, npad, sub0 * 32, slot + w::kStageBytes, wave, lane);
+  issue_norms<w::NW, 128>(dn, npad, sub0 * 32, slot + w::kStageBytes, wave, lane);
 }
 
 __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
@@ -633,7 +645,9 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   const bool wide = ctx->impl == 2;
   const int rows = wide ? 32 : kSubRows;            // rows per subtile / queries per tile
   const int sub_bytes = wide ? w::kSub : kSub;
-  const int64_t npad = db ? cdiv(n, 128) * 128 : cdiv(n, rows) * rows;
+  // DB padded to whole stages of both layouts (kStageRows and the 128-row wide stage)
+  const int64_t spad = std::max(kStageRows, 128);
+  const int64_t npad = db ? cdiv(n, spad) * spad : cdiv(n, rows) * rows;
   uint8_t* pack;
   int* norms;
   if (db) {
