@@ -202,6 +202,9 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_SGB
 #define SOD_I8_SGB 1       // explicit MFMA / VALU interleave of the subtile block (+3 %)
 #endif
+#ifndef SOD_I8_COLD
+#define SOD_I8_COLD 1      // mark the slow path unlikely (compact hot loop in the i-cache)
+#endif
 #ifndef SOD_I8_XCD
 #define SOD_I8_XCD 1       // XCD-aware work-group -> (chunk, query block) order
 #endif
@@ -254,7 +257,11 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 
     if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
   }
 #endif
+#if SOD_I8_COLD
+  if (__builtin_expect(any != 0, 0)) {   // slow path laid out away from the hot loop
+#else
   if (any) {
+#endif
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
       if (hit[t]) {
