@@ -63,6 +63,11 @@ def parse():
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-queries", type=int, default=4096)
+    p.add_argument("--contexts", type=int, default=0,
+                   help="query streams over the one resident DB (sod_db_share): consecutive "
+                        "query images alternate between them, so one image's Hough/select/"
+                        "affine tail overlaps the next image's matcher.  Default: 2 on one "
+                        "GPU, 1 with several ranks")
     p.add_argument("--impl", default="i8", choices=sorted(IMPLS),
                    help="matcher kernel: int8 MFMA 16x16x64 (default, fastest), int8 32x32x32 "
                         "or bf16 MFMA; all bit-exact")
@@ -253,28 +258,43 @@ def main():
     elif world > 1:
         comm = TorchHostComm()
     own = (rank * n_shard, (rank + 1) * n_shard)
+    ncontexts = a.contexts if a.contexts > 0 else (2 if world == 1 else 1)
+    ctxs = [ctx]
+    for _ in range(ncontexts - 1):
+        c = _lib.Context(dev)
+        c.set_impl(a.impl)
+        c.share_db(ctx)
+        c.upload_queries(qs.des, qs.kp)
+        ctxs.append(c)
+    turn = [0]
 
     def step():
+        c = ctxs[turn[0] % ncontexts]
+        turn[0] += 1
         if comm is None or comm.kind == "rccl":
             # one enqueue: match, all-gather, ratio, vote, all-reduce, select, affine
-            ctx.pipeline(qs.shape, bins, ratio=0.75, vote_threshold=5, affine_threshold=4,
-                         x_factor=128.0, y_factor=128.0, run_affine=run_affine)
+            c.pipeline(qs.shape, bins, ratio=0.75, vote_threshold=5, affine_threshold=4,
+                       x_factor=128.0, y_factor=128.0, run_affine=run_affine)
         else:
-            run_sharded(ctx, comm, own, qs.shape, bins, 0.75, 5, 4, 128.0, 128.0, run_affine)
+            run_sharded(c, comm, own, qs.shape, bins, 0.75, 5, 4, 128.0, 128.0, run_affine)
+
+    def sync_all():
+        for c in ctxs:
+            c.synchronize()
 
     for _ in range(a.warmup):
         step()
-    ctx.synchronize()
+    sync_all()
 
     # ---- timed region ----------------------------------------------------------------
     match_ms, stage = [], []
     D.barrier()
-    ctx.synchronize()
+    sync_all()
     device_sync(world)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    ctx.synchronize()
+    sync_all()
     device_sync(world)
     D.barrier()
     t1 = time.perf_counter()
@@ -283,6 +303,7 @@ def main():
 
     # ---- per-kernel timing (HIP events on the ctx stream), separate untimed steps -------
     for _ in range(max(3, min(a.steps, 10))):
+        turn[0] = 0            # always the first context (its events are read below)
         step()
         ctx.synchronize()
         match_ms.append(ctx.last_match_ms())
@@ -332,6 +353,7 @@ def main():
             " + affine verify" if run_affine else ""),
             "queries": nq, "db_rows_per_gpu": n_shard, "db_rows_total": world * n_shard,
             "bins": list(bins), "parallelism": "db-shard%d" % world,
+            "query_streams": ncontexts,
             "comm": a.comm if world > 1 else None},
         "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
         "hough_stage_votes_per_s": n_votes / ((float(stage[2]) + float(stage[3])) / 1000.0),
@@ -364,6 +386,8 @@ def main():
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
+    for c in ctxs[1:]:
+        c.close()
     ctx.close()
     if world > 1:
         D.dist.destroy_process_group()

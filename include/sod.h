@@ -64,6 +64,12 @@ int sod_db_set_keypoints(sod_ctx* ctx, int64_t n_total, const float* x, const fl
 int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t n,
                               int64_t row_offset);
 
+/* dst uses src's resident database (keypoints, image table, packed descriptors) without
+ * a copy: several contexts -- each with its own stream and query state -- serve query
+ * images concurrently over one DB.  src must outlive dst and must not re-upload its DB
+ * while dst uses it; a later upload into dst gives dst its own buffers. */
+int sod_db_share(sod_ctx* dst, const sod_ctx* src);
+
 /* ---- packed DB image (replaces the GenerateDatabaseInfo.py:35 pickle
  * + main.py:53-66 flattening as the descriptor store): the device's own fragment layout
  * with its norm words behind a 64-byte header, so a later upload is one copy (no

@@ -50,6 +50,7 @@ SIGNATURES = {
     "sod_db_set_keypoints": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_i32p,
                                        C.c_int32, c_f64p, c_i32p]),
     "sod_db_upload_descriptors": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int64, C.c_int64]),
+    "sod_db_share": (C.c_int, [c_ctx, c_ctx]),
     "sod_db_packed_size": (C.c_int, [c_ctx, c_i64p]),
     "sod_db_export_packed": (C.c_int, [c_ctx, c_vp, C.c_int64]),
     "sod_db_import_packed": (C.c_int, [c_ctx, c_vp, C.c_int64]),
@@ -471,6 +472,12 @@ class Context:
         """Restrict the Hough-side stages to queries [first, first+count) (one image of a
         batch matched together); count < 0 = all queries."""
         self._chk(self._L.sod_query_window(self._h, int(first), int(count)))
+
+    def share_db(self, src):
+        """Use ``src``'s resident database (no copy); ``src`` must outlive this context."""
+        self._chk(self._L.sod_db_share(self._h, src._h))
+        self.n_total = src.n_total
+        self._db_src = src
 
     def export_packed(self):
         """The DB shard as a packed image (uint8 array): header + fragments + norm words."""

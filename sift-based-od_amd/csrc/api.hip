@@ -228,6 +228,37 @@ int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
   return SOD_OK;
 }
 
+// ---- DB shared between contexts (several query streams over one resident DB) ---------
+int sod_db_share(sod_ctx* dst, const sod_ctx* src) {
+  SOD_TRY(set_dev(dst));
+  if (!src || src == dst) return sod_fail(dst, SOD_EINVAL, "bad source context");
+  if (src->device != dst->device) return sod_fail(dst, SOD_EINVAL, "contexts on different devices");
+  if (!src->nsub || !src->n_total) return sod_fail(dst, SOD_ESTATE, "source has no database");
+  sod_view(dst->mx, src->mx);
+  sod_view(dst->my, src->my);
+  sod_view(dst->mang, src->mang);
+  sod_view(dst->moct, src->moct);
+  sod_view(dst->mimg, src->mimg);
+  sod_view(dst->cent, src->cent);
+  sod_view(dst->isize, src->isize);
+  sod_view(dst->dbpack, src->dbpack);
+  sod_view(dst->dn, src->dn);
+  dst->impl = src->impl;
+  dst->n_total = src->n_total;
+  dst->n_images = src->n_images;
+  dst->n_shard = src->n_shard;
+  dst->row_offset = src->row_offset;
+  dst->nsub = src->nsub;
+  dst->nqt = 0;   // queries must be re-uploaded in the (possibly new) layout
+  // raw max ||d||^2 for sod_match_exact_order; the source's uploads are complete
+  SOD_HIP(dst, hipStreamSynchronize(src->stream));
+  SOD_HIP(dst, hipMemcpyAsync(dst->flags.p + 1, src->flags.p + 1, 4, hipMemcpyDeviceToDevice,
+                              dst->stream));
+  SOD_HIP(dst, hipStreamSynchronize(dst->stream));
+  dst->matched = dst->ratio_done = dst->houghed = dst->selected = dst->affined = false;
+  return SOD_OK;
+}
+
 // ---- packed DB image (DB on-disk format, upload = one memcpy) -----
 // [header 64 B][packed descriptor fragments][norm words]; the fragment and norm layouts are
 // the matcher's own (see match_i8.hip / match.hip), so an import is a plain copy.

@@ -23,7 +23,8 @@ constexpr int kSigmaLutSize = 2 * kSigmaLutHalf + 1;
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
-  size_t n = 0;  // capacity in elements
+  size_t n = 0;      // capacity in elements
+  bool own = true;   // false: a view of another context's buffer (sod_db_share)
 };
 
 struct sod_ctx {
@@ -145,9 +146,10 @@ template <typename T>
 int sod_reserve(sod_ctx* ctx, DevBuf<T>& b, size_t n) {
   if (n == 0) n = 1;
   if (b.n >= n) return SOD_OK;
-  if (b.p) (void)hipFree(b.p);
+  if (b.p && b.own) (void)hipFree(b.p);
   b.p = nullptr;
   b.n = 0;
+  b.own = true;
   hipError_t e = hipMalloc((void**)&b.p, n * sizeof(T));
   if (e != hipSuccess) {
     b.p = nullptr;
@@ -159,9 +161,17 @@ int sod_reserve(sod_ctx* ctx, DevBuf<T>& b, size_t n) {
 }
 template <typename T>
 void sod_release(DevBuf<T>& b) {
-  if (b.p) (void)hipFree(b.p);
+  if (b.p && b.own) (void)hipFree(b.p);
   b.p = nullptr;
   b.n = 0;
+  b.own = true;
+}
+template <typename T>
+void sod_view(DevBuf<T>& dst, const DevBuf<T>& src) {   // non-owning alias
+  sod_release(dst);
+  dst.p = src.p;
+  dst.n = src.n;
+  dst.own = false;
 }
 
 // kernel launchers implemented in the .hip files ----------------------------------------

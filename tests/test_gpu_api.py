@@ -274,3 +274,31 @@ def test_query_batch_equals_per_image():
             np.testing.assert_array_equal(a["params"], b["affine"]["params"])
             p = c.postprocess()
             np.testing.assert_array_equal(p["final_pose"], b["post"]["final_pose"])
+
+
+def test_shared_db_contexts():
+    """sod_db_share: a second context over the first one's resident DB (no copy) gives the
+    same results, also while both run interleaved on their own streams."""
+    db = synthetic.make_database(10, 500, seed=71)
+    qa = synthetic.make_queries(2000, seed=72, db_seed=71, kp_per_image=500)
+    qb = synthetic.make_queries(1500, seed=73, db_seed=71, kp_per_image=500)
+    with _lib.Context(0) as c0:
+        c0.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c0.upload_db(db.des)
+        c0.upload_queries(qb.des, qb.kp)
+        c0.pipeline(qb.shape, 15)
+        ref_b = (c0.match_result(), c0.valid_result(), c0.affine_result())
+        c0.upload_queries(qa.des, qa.kp)
+        with _lib.Context(0) as c1:
+            c1.share_db(c0)
+            c1.upload_queries(qb.des, qb.kp)
+            for _ in range(3):            # interleaved on two streams
+                c0.pipeline(qa.shape, 15)
+                c1.pipeline(qb.shape, 15)
+            got_b = (c1.match_result(), c1.valid_result(), c1.affine_result())
+            assert c1.exact_order()
+    for x, y in zip(ref_b[0], got_b[0]):
+        assert np.array_equal(x, y)
+    for k in ("keys", "votes", "offsets", "members"):
+        assert np.array_equal(ref_b[1][k], got_b[1][k])
+    np.testing.assert_array_equal(ref_b[2]["params"], got_b[2]["params"])
