@@ -90,6 +90,16 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq,
  * first+count); member lists then hold window-local query indices.  count < 0 restores
  * the whole query set (the default after sod_query_upload). */
 int sod_query_window(sod_ctx* ctx, int32_t first, int32_t count);
+/* The same batch with the per-image stages FUSED: declare the images (query offsets
+ * [n+1] covering all uploaded queries, shapes [n*2] = rgb_query.shape (h, w) each); then
+ * ONE sod_hough_enqueue / sod_select_enqueue / sod_affine_enqueue / sod_postprocess
+ * covers every image (their query_h / query_w arguments are ignored): the bin key space is
+ * image-major (image * nbins + bin), valid bins come out image by image in each image's
+ * reference order, member lists hold batch-global query indices, and
+ * sod_valid_images_get gives each valid bin's image.  n_images = 0 returns to one image. */
+int sod_query_images(sod_ctx* ctx, int32_t n_images, const int32_t* q_offsets,
+                     const int32_t* shapes);
+int sod_valid_images_get(sod_ctx* ctx, int32_t* image /* [V] */);
 
 /* ---- A1/A2: cv2.BFMatcher().knnMatch(des_query, des, k=2) + ratio test ------------
  * main.py:70-86.  enqueue: local shard top-2 (exact squared distances), merged over

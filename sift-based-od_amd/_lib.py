@@ -57,6 +57,8 @@ SIGNATURES = {
     "sod_query_upload": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int32, c_f32p, c_f32p, c_f32p,
                                    c_i32p]),
     "sod_query_window": (C.c_int, [c_ctx, C.c_int32, C.c_int32]),
+    "sod_query_images": (C.c_int, [c_ctx, C.c_int32, c_i32p, c_i32p]),
+    "sod_valid_images_get": (C.c_int, [c_ctx, c_i32p]),
     "sod_match_enqueue": (C.c_int, [c_ctx]),
     "sod_match_set_impl": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
@@ -478,6 +480,21 @@ class Context:
         self._chk(self._L.sod_db_share(self._h, src._h))
         self.n_total = src.n_total
         self._db_src = src
+
+    def query_images(self, offsets, shapes):
+        """Declare the uploaded queries as a batch of images (offsets [n+1], shapes [n, 2+]
+        = rgb_query.shape) for fused per-image stages; an empty list returns to one image."""
+        off = _c(offsets, np.int32)
+        n = max(0, len(off) - 1)
+        shp = np.ascontiguousarray(np.asarray(shapes, np.int64)[:, :2], np.int32) if n else \
+            np.zeros((0, 2), np.int32)
+        self._chk(self._L.sod_query_images(self._h, n, ptr(off, C.c_int32), ptr(shp, C.c_int32)))
+
+    def valid_images(self):
+        V, _ = self.valid_counts()
+        img = np.empty(max(V, 1), np.int32)
+        self._chk(self._L.sod_valid_images_get(self._h, ptr(img, C.c_int32)))
+        return img[:V]
 
     def export_packed(self):
         """The DB shard as a packed image (uint8 array): header + fragments + norm words."""

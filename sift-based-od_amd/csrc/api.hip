@@ -47,6 +47,7 @@ int check_bins(sod_ctx* ctx, const int32_t bins[4]) {
   const bool changed_sigma = bins[3] != ctx->bins[3] || !ctx->sig_lut.p;
   std::memcpy(ctx->bins, bins, sizeof(ctx->bins));
   ctx->nbins = nb;
+  ctx->nbins1 = nb;
   if (changed_sigma) SOD_TRY(sod_build_sigma_lut(ctx, bins[3]));
   return SOD_OK;
 }
@@ -117,6 +118,8 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->aqy); sod_release(ctx->aisig); sod_release(ctx->surv);
   sod_release(ctx->fvotes); sod_release(ctx->params); sod_release(ctx->alive);
   sod_release(ctx->post_m); sod_release(ctx->post_pos); sod_release(ctx->post_ori);
+  sod_release(ctx->post_img); sod_release(ctx->qimg); sod_release(ctx->qshape);
+  sod_release(ctx->hist_rng); sod_release(ctx->bwh);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
@@ -367,6 +370,7 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq, const
   ctx->nq = nq;
   ctx->win0 = 0;
   ctx->winn = -1;
+  ctx->n_qimg = 0;
   if (x && y && angle && octave) {
     SOD_TRY(upload(ctx, ctx->qx, x, (size_t)nq));
     SOD_TRY(upload(ctx, ctx->qy, y, (size_t)nq));
@@ -389,8 +393,47 @@ int sod_query_window(sod_ctx* ctx, int32_t first, int32_t count) {
       return sod_fail(ctx, SOD_EINVAL, "query window outside the uploaded queries");
     ctx->win0 = first;
     ctx->winn = count;
+    ctx->n_qimg = 0;   // a window and an image batch are exclusive
   }
   ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_query_images(sod_ctx* ctx, int32_t n_images, const int32_t* q_offsets,
+                     const int32_t* shapes) {
+  SOD_TRY(set_dev(ctx));
+  if (n_images <= 0) {
+    ctx->n_qimg = 0;
+    ctx->houghed = ctx->selected = ctx->affined = false;
+    return SOD_OK;
+  }
+  if (!q_offsets || !shapes || q_offsets[0] != 0 || q_offsets[n_images] != ctx->nq)
+    return sod_fail(ctx, SOD_EINVAL, "image offsets must cover the uploaded queries");
+  for (int32_t b = 0; b < n_images; ++b)
+    if (q_offsets[b + 1] < q_offsets[b] || shapes[2 * b] < 1 || shapes[2 * b + 1] < 1)
+      return sod_fail(ctx, SOD_EINVAL, "bad image offsets or shapes");
+  ctx->qoff_h.assign(q_offsets, q_offsets + n_images + 1);
+  ctx->qshape_h.assign(shapes, shapes + 2 * n_images);
+  std::vector<int32_t> img((size_t)ctx->nq);
+  for (int32_t b = 0; b < n_images; ++b)
+    for (int32_t q = q_offsets[b]; q < q_offsets[b + 1]; ++q) img[(size_t)q] = b;
+  SOD_TRY(upload(ctx, ctx->qimg, img.data(), img.size()));
+  SOD_TRY(upload(ctx, ctx->qshape, ctx->qshape_h.data(), ctx->qshape_h.size()));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->n_qimg = n_images;
+  ctx->win0 = 0;
+  ctx->winn = -1;
+  ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_valid_images_get(sod_ctx* ctx, int32_t* image) {
+  int64_t V, M;
+  SOD_TRY(sod_valid_counts(ctx, &V, &M));
+  std::vector<uint32_t> lin((size_t)V);
+  SOD_TRY(download(ctx, lin.data(), ctx->vbin.p, (size_t)V));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (int64_t v = 0; v < V; ++v) image[v] = (int32_t)(lin[(size_t)v] / ctx->nbins1);
   return SOD_OK;
 }
 
@@ -500,6 +543,11 @@ int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int3
   if (!ctx->n_total || !ctx->qx.p) return sod_fail(ctx, SOD_ESTATE, "keypoints not uploaded");
   if (query_h < 1 || query_w < 1) return sod_fail(ctx, SOD_EINVAL, "bad query image shape");
   SOD_TRY(check_bins(ctx, bins));
+  if (ctx->n_qimg) {   // one bin space per query image, image-major
+    if (ctx->winn >= 0) return sod_fail(ctx, SOD_EINVAL, "query window and image batch are exclusive");
+    ctx->nbins = ctx->nbins1 * ctx->n_qimg;
+    if (ctx->nbins > 0x7fffffffLL) return sod_fail(ctx, SOD_EINVAL, "too many bins x images");
+  }
   ctx->qh = query_h;
   ctx->qw = query_w;
   SOD_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
@@ -552,7 +600,7 @@ int sod_valid_counts(sod_ctx* ctx, int64_t* n_valid, int64_t* n_members) {
 static void decode_keys(const sod_ctx* ctx, const std::vector<uint32_t>& lin, int32_t* keys) {
   const int by = ctx->bins[1], bt = ctx->bins[2], bs = ctx->bins[3];
   for (size_t i = 0; i < lin.size(); ++i) {
-    const uint32_t l = lin[i];
+    const uint32_t l = (uint32_t)(lin[i] % ctx->nbins1);   // bin within its query image
     keys[4 * i + 3] = l % bs;
     keys[4 * i + 2] = (l / bs) % bt;
     keys[4 * i + 1] = (l / (bs * bt)) % by;
@@ -616,7 +664,8 @@ int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_
   SOD_TRY(sod_reserve(ctx, ctx->params, (size_t)ctx->vmax * 6));
   SOD_TRY(sod_reserve(ctx, ctx->alive, (size_t)ctx->mmax));
   SOD_TRY(launch_affine(ctx, 0, true, ctx->voff.p, ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p,
-                        ctx->aisig.p, query_w, query_h, x_factor, y_factor, threshold, 1 << 30,
+                        ctx->aisig.p, query_w, query_h, ctx->n_qimg ? ctx->bwh.p : nullptr,
+                        x_factor, y_factor, threshold, 1 << 30,
                         nullptr, ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p,
                         ctx->scal.p));
   SOD_HIP(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
@@ -725,7 +774,7 @@ int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets, const
   if (rc == SOD_OK) rc = sod_reserve(ctx, pr, (size_t)n_bins * 6);
   if (rc == SOD_OK)
     rc = launch_affine(ctx, n_bins, false, off.p, p[0].p, p[1].p, p[2].p, p[3].p, is.p, query_w,
-                       query_h, x_factor, y_factor, threshold, max_iter,
+                       query_h, nullptr, x_factor, y_factor, threshold, max_iter,
                        params_in ? pin.p : nullptr, sv.p, vo.p, pr.p, al.p, nullptr);
   if (rc == SOD_OK) rc = download(ctx, survived, sv.p, (size_t)n_bins);
   if (rc == SOD_OK) rc = download(ctx, votes, vo.p, (size_t)n_bins);

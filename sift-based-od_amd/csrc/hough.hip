@@ -21,6 +21,8 @@
 //   means_kernel     PoseBin running means, sequential per bin (PoseBin.py:19-43)
 //   affine_kernel    one wave per bin: decoupled 3x3 normal equations, pinv by Jacobi,
 //                    outlier rejection, fixed point (AffineParameters.py:89-160)
+#include <algorithm>
+
 #include "sod_internal.h"
 
 namespace {
@@ -104,12 +106,17 @@ __global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
                             const int* __restrict__ qo, const float* __restrict__ mx,
                             const float* __restrict__ my, const float* __restrict__ ma,
                             const int* __restrict__ mo, const int* __restrict__ mimg,
-                            const double* __restrict__ cent, int H, int W, Bins b,
+                            const double* __restrict__ cent, int H, int W,
+                            const int* __restrict__ qimg, const int* __restrict__ qshape, Bins b,
                             const int* __restrict__ lut, int64_t own_lo, int64_t own_hi,
                             double* __restrict__ pose, uint32_t* __restrict__ basekey,
                             uint32_t* __restrict__ vmask) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
+  if (qimg) {   // batch of query images: this query's image shape (main.py:102)
+    H = qshape[2 * qimg[q]];
+    W = qshape[2 * qimg[q] + 1];
+  }
   if (!good[q]) {
     vmask[q] = 0;
     return;
@@ -184,10 +191,14 @@ constexpr int kHistThreads = 512;
 
 __global__ __launch_bounds__(kHistThreads) void hist_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
-    int64_t nbins, uint32_t* __restrict__ gcount, uint32_t* __restrict__ gfirst) {
+    int64_t nbins, const int* __restrict__ qimg, int64_t nbins1, const int* __restrict__ rng,
+    uint32_t* __restrict__ gcount, uint32_t* __restrict__ gfirst) {
   __shared__ uint32_t cnt[kSlab];
   __shared__ uint32_t fst[kSlab];
-  const uint32_t slab0 = blockIdx.x * kSlab;
+  // batch of query images: a chunk only visits the slabs of its images' bin ranges
+  const int64_t slab = rng ? (int64_t)rng[2 * blockIdx.y] + blockIdx.x : blockIdx.x;
+  if (rng && slab > rng[2 * blockIdx.y + 1]) return;
+  const uint32_t slab0 = (uint32_t)(slab * kSlab);
   for (int i = threadIdx.x; i < kSlab; i += kHistThreads) {
     cnt[i] = 0;
     fst[i] = 0xFFFFFFFFu;
@@ -200,11 +211,12 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
     if (!(m & 0x10000u)) continue;  // no vote, or the match's DB row is not in this shard
     const uint32_t key = basekey[q];
     const int ix = key & 0xFF, iy = (key >> 8) & 0xFF, it = (key >> 16) & 0xFF, is = key >> 24;
+    const uint32_t base = qimg ? (uint32_t)(qimg[q] * nbins1) : 0u;
 #pragma unroll
     for (int slot = 0; slot < 16; ++slot) {
       if (!((m >> slot) & 1u)) continue;
-      const uint32_t lb = lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
-                                  it + ((slot >> 1) & 1), is + (slot & 1), b) - slab0;
+      const uint32_t lb = base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                         it + ((slot >> 1) & 1), is + (slot & 1), b) - slab0;
       if (lb < (uint32_t)kSlab) {
         atomicAdd(&cnt[lb], 1u);
         atomicMin(&fst[lb], (uint32_t)(q * 16 + slot));
@@ -229,7 +241,8 @@ __device__ __forceinline__ uint32_t first_touch_slots(int64_t q, const uint32_t*
                                                       const uint32_t* vmask,
                                                       const uint32_t* gcount,
                                                       const uint32_t* gfirst, Bins b,
-                                                      uint32_t thr, uint32_t bins_out[16]) {
+                                                      uint32_t qbase, uint32_t thr,
+                                                      uint32_t bins_out[16]) {
   const uint32_t m = vmask[q] & 0xFFFFu;
   uint32_t n = 0;
   if (!m) return 0;
@@ -237,8 +250,8 @@ __device__ __forceinline__ uint32_t first_touch_slots(int64_t q, const uint32_t*
   const int ix = key & 0xFF, iy = (key >> 8) & 0xFF, it = (key >> 16) & 0xFF, is = key >> 24;
   for (int slot = 0; slot < 16; ++slot) {
     if (!((m >> slot) & 1u)) continue;
-    const uint32_t lb = lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
-                                it + ((slot >> 1) & 1), is + (slot & 1), b);
+    const uint32_t lb = qbase + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                        it + ((slot >> 1) & 1), is + (slot & 1), b);
     if (gcount[lb] >= thr && gfirst[lb] == (uint32_t)(q * 16 + slot)) bins_out[n++] = lb;
   }
   return n;
@@ -288,12 +301,13 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
 
 __global__ __launch_bounds__(kSelThreads) void select_count_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
-    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b, uint32_t thr,
-    uint32_t* __restrict__ blk) {
+    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b,
+    const int* __restrict__ qimg, int64_t nbins1, uint32_t thr, uint32_t* __restrict__ blk) {
   __shared__ uint32_t sh[kSelThreads / 64];
   const int64_t q = (int64_t)blockIdx.x * kSelThreads + threadIdx.x;
   uint32_t tmp[16];
-  const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, thr, tmp) : 0;
+  const uint32_t qb = (qimg && q < nq) ? (uint32_t)(qimg[q] * nbins1) : 0u;
+  const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, qb, thr, tmp) : 0;
   uint32_t tot;
   block_excl_scan(n, sh, &tot);
   if (threadIdx.x == 0) blk[blockIdx.x] = tot;
@@ -334,12 +348,14 @@ __global__ __launch_bounds__(1024) void scan_u32_kernel(uint32_t* __restrict__ a
 
 __global__ __launch_bounds__(kSelThreads) void select_write_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
-    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b, uint32_t thr,
-    const uint32_t* __restrict__ blk, uint32_t* __restrict__ out, uint32_t* __restrict__ vidx) {
+    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b,
+    const int* __restrict__ qimg, int64_t nbins1, uint32_t thr, const uint32_t* __restrict__ blk,
+    uint32_t* __restrict__ out, uint32_t* __restrict__ vidx) {
   __shared__ uint32_t sh[kSelThreads / 64];
   const int64_t q = (int64_t)blockIdx.x * kSelThreads + threadIdx.x;
   uint32_t tmp[16];
-  const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, thr, tmp) : 0;
+  const uint32_t qb = (qimg && q < nq) ? (uint32_t)(qimg[q] * nbins1) : 0u;
+  const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, qb, thr, tmp) : 0;
   uint32_t tot;
   const uint32_t pos = blk[blockIdx.x] + block_excl_scan(n, sh, &tot);
   for (uint32_t i = 0; i < n; ++i) {
@@ -460,7 +476,8 @@ __device__ void sort_block_u64(uint64_t* key, int p) {
 constexpr int kFillCap = kFillQ * 16;
 __global__ __launch_bounds__(256) void member_fill_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
-    const uint32_t* __restrict__ vidx, const int64_t* __restrict__ voff,
+    const int* __restrict__ qimg, int64_t nbins1, const uint32_t* __restrict__ vidx,
+    const int64_t* __restrict__ voff,
     uint32_t* __restrict__ cursor, int32_t* __restrict__ members) {
   __shared__ uint64_t key[kFillCap];
   __shared__ uint32_t nvote;
@@ -474,10 +491,11 @@ __global__ __launch_bounds__(256) void member_fill_kernel(
     if (m) {
       const uint32_t k = basekey[q];
       const int ix = k & 0xFF, iy = (k >> 8) & 0xFF, it = (k >> 16) & 0xFF, is = k >> 24;
+      const uint32_t base = qimg ? (uint32_t)(qimg[q] * nbins1) : 0u;
       for (int slot = 0; slot < 16; ++slot) {
         if (!((m >> slot) & 1u)) continue;
-        const uint32_t lb = lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
-                                    it + ((slot >> 1) & 1), is + (slot & 1), b);
+        const uint32_t lb = base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                           it + ((slot >> 1) & 1), is + (slot & 1), b);
         const uint32_t v = vidx[lb];
         if (v == 0xFFFFFFFFu) continue;
         key[atomicAdd(&nvote, 1u)] = ((uint64_t)v << 32) | (uint32_t)q;
@@ -603,15 +621,18 @@ __global__ __launch_bounds__(256) void members_kernel(
     int64_t nq, const uint32_t* __restrict__ scal, const uint32_t* __restrict__ vbin,
     const int64_t* __restrict__ voff, const uint32_t* __restrict__ gcount,
     const uint32_t* __restrict__ gfirst, const uint32_t* __restrict__ basekey,
-    const uint32_t* __restrict__ vmask, Bins b, int nblk, int32_t* __restrict__ members) {
+    const uint32_t* __restrict__ vmask, Bins b, const int* __restrict__ qimg, int64_t nbins1,
+    int nblk, int32_t* __restrict__ members) {
   constexpr int U = 4;
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t V = scal[0];
   for (int64_t v = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < V; v += nwaves) {
     const uint32_t lb = vbin[v];
-    const int bs_ = lb % b.s, bt_ = (lb / b.s) % b.t, by_ = (lb / (b.s * b.t)) % b.y,
-              bx_ = lb / (b.s * b.t * b.y);
+    const int img = qimg ? (int)(lb / nbins1) : 0;
+    const uint32_t ll = qimg ? (uint32_t)(lb % nbins1) : lb;   // bin within its image
+    const int bs_ = ll % b.s, bt_ = (ll / b.s) % b.t, by_ = (ll / (b.s * b.t)) % b.y,
+              bx_ = ll / (b.s * b.t * b.y);
     const uint32_t need = gcount[lb];
     if (need <= (uint32_t)kOrderCap && nblk <= kOrderCap) continue;   // fill + order
     const int64_t off = voff[v];
@@ -621,7 +642,7 @@ __global__ __launch_bounds__(256) void members_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t q = q0 + u * 64 + lane;
-        m[u] = q < nq ? (vmask[q] & 0xFFFFu) : 0u;
+        m[u] = (q < nq && (!qimg || qimg[q] == img)) ? (vmask[q] & 0xFFFFu) : 0u;
         key[u] = q < nq ? basekey[q] : 0u;
       }
 #pragma unroll
@@ -744,9 +765,10 @@ __global__ void affine_gather_kernel(const uint32_t* __restrict__ scal,
                                      const int* __restrict__ idx1, const float* __restrict__ mx,
                                      const float* __restrict__ my, const float* __restrict__ qx,
                                      const float* __restrict__ qy, const uint32_t* __restrict__ vbin,
-                                     Bins b, float* __restrict__ amx, float* __restrict__ amy,
+                                     Bins b, int64_t nbins1, const int* __restrict__ qshape,
+                                     float* __restrict__ amx, float* __restrict__ amy,
                                      float* __restrict__ aqx, float* __restrict__ aqy,
-                                     int32_t* __restrict__ aisig) {
+                                     int32_t* __restrict__ aisig, int32_t* __restrict__ bwh) {
   const int64_t M = scal[1], V = scal[0];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += stride) {
@@ -757,8 +779,14 @@ __global__ void affine_gather_kernel(const uint32_t* __restrict__ scal,
     aqx[e] = qx[q];
     aqy[e] = qy[q];
   }
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += stride)
-    aisig[v] = (int32_t)(vbin[v] % b.s);
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += stride) {
+    aisig[v] = (int32_t)(vbin[v] % b.s);   // nbins1 is a multiple of b.s
+    if (qshape) {   // batch of query images: the bin's image (w, h) = image_query_size
+      const int img = (int)(vbin[v] / nbins1);
+      bwh[2 * v] = qshape[2 * img + 1];
+      bwh[2 * v + 1] = qshape[2 * img];
+    }
+  }
 }
 
 __device__ __forceinline__ double wave_sum(double x) {
@@ -817,8 +845,9 @@ __device__ void pinv3_sym(const double g[3][3], double p[3][3]) {
 __global__ __launch_bounds__(256) void affine_kernel(
     int64_t nb_host, const uint32_t* __restrict__ nb_dev, const int64_t* __restrict__ off,
     const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
-    const float* __restrict__ qy, const int32_t* __restrict__ isig, int qw, int qh, double xf,
-    double yf, int thr, int max_iter, const double* __restrict__ params_in,
+    const float* __restrict__ qy, const int32_t* __restrict__ isig, int qw, int qh,
+    const int32_t* __restrict__ bwh, double xf, double yf, int thr, int max_iter,
+    const double* __restrict__ params_in,
     uint8_t* __restrict__ surv, int32_t* __restrict__ votes, double* __restrict__ params,
     uint8_t* __restrict__ alive) {
   const int lane = threadIdx.x & 63;
@@ -828,8 +857,9 @@ __global__ __launch_bounds__(256) void affine_kernel(
     const int64_t a = off[v], e = off[v + 1];
     for (int64_t j = a + lane; j < e; j += 64) alive[j] = 1;
     // AffineParameters.py:120-121: tolerance scales with the scale-bin INDEX pose[3]
-    const double xref = (double)((int64_t)qw * isig[v]) / xf;
-    const double yref = (double)((int64_t)qh * isig[v]) / yf;
+    const int64_t bw = bwh ? bwh[2 * v] : qw, bh = bwh ? bwh[2 * v + 1] : qh;
+    const double xref = (double)(bw * isig[v]) / xf;
+    const double yref = (double)(bh * isig[v]) / yf;
     int64_t n = e - a;
     double prm[6] = {0, 0, 0, 0, 0, 0};
     bool ok = false;
@@ -898,6 +928,8 @@ __global__ __launch_bounds__(256) void affine_kernel(
 // ---------------------------------------------------------------------------------------
 static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static Bins ctx_bins(const sod_ctx* c) { return Bins{c->bins[0], c->bins[1], c->bins[2], c->bins[3]}; }
+// image of each query when a batch of query images is declared (nullptr: one image)
+static const int* qimg_p(const sod_ctx* c) { return c->n_qimg ? c->qimg.p : nullptr; }
 
 int sod_build_sigma_lut(sod_ctx* ctx, int32_t bs) {
   // HTHF:66-70 evaluated with the same libm calls CPython's math.log(x, 2) makes:
@@ -953,12 +985,37 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
                      ctx->good.p + q0, ctx->idx1.p + q0, ctx->qx.p + q0, ctx->qy.p + q0,
                      ctx->qang.p + q0, ctx->qoct.p + q0,
                      ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p,
-                     ctx->qh, ctx->qw, ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
+                     ctx->qh, ctx->qw, qimg_p(ctx), ctx->n_qimg ? ctx->qshape.p : nullptr,
+                     ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
                      ctx->basekey.p, ctx->vmask.p);
   SOD_HIP(ctx, hipGetLastError());
-  dim3 grid((unsigned)cdiv(ctx->nbins, kSlab), (unsigned)cdiv(nq, kChunk));
+  const int64_t nchunk = cdiv(nq, kChunk);
+  dim3 grid((unsigned)cdiv(ctx->nbins, kSlab), (unsigned)nchunk);
+  const int* rng = nullptr;
+  if (ctx->n_qimg) {
+    // a chunk of queries spans a few consecutive images: only their bin slabs
+    std::vector<int32_t> r((size_t)nchunk * 2);
+    int64_t span = 1;
+    for (int64_t c = 0; c < nchunk; ++c) {
+      const int64_t qa = c * kChunk, qb = std::min(nq, qa + kChunk) - 1;
+      auto img_of = [&](int64_t q) {
+        return (int64_t)(std::upper_bound(ctx->qoff_h.begin(), ctx->qoff_h.end(), (int32_t)q) -
+                         ctx->qoff_h.begin()) - 1;
+      };
+      r[2 * c] = (int32_t)((img_of(qa) * ctx->nbins1) / kSlab);
+      r[2 * c + 1] = (int32_t)(((img_of(qb) + 1) * ctx->nbins1 - 1) / kSlab);
+      span = std::max<int64_t>(span, r[2 * c + 1] - r[2 * c] + 1);
+    }
+    SOD_TRY(sod_reserve(ctx, ctx->hist_rng, r.size()));
+    SOD_HIP(ctx, hipMemcpyAsync(ctx->hist_rng.p, r.data(), r.size() * 4, hipMemcpyHostToDevice,
+                                ctx->stream));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));   // r is a host temporary
+    grid.x = (unsigned)span;
+    rng = ctx->hist_rng.p;
+  }
   hipLaunchKernelGGL(hist_kernel, grid, dim3(kHistThreads), 0, ctx->stream, nq, ctx->basekey.p,
-                     ctx->vmask.p, ctx_bins(ctx), ctx->nbins, ctx->counts.p, ctx->first.p);
+                     ctx->vmask.p, ctx_bins(ctx), ctx->nbins, qimg_p(ctx), ctx->nbins1, rng,
+                     ctx->counts.p, ctx->first.p);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
@@ -970,14 +1027,14 @@ static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* t
   SOD_TRY(sod_reserve(ctx, ctx->blk, (size_t)nblk));
   hipLaunchKernelGGL(select_count_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream,
                      nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
-                     thr, ctx->blk.p);
+                     qimg_p(ctx), ctx->nbins1, thr, ctx->blk.p);
   SOD_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(scan_u32_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->blk.p, nblk,
                      total_slot);
   SOD_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(select_write_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream,
                      nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
-                     thr, ctx->blk.p, out, vidx);
+                     qimg_p(ctx), ctx->nbins1, thr, ctx->blk.p, out, vidx);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
@@ -1002,8 +1059,8 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
                      ctx->counts.p, ctx->scal.p, ctx->voff.p, ctx->cursor.p);
   SOD_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(member_fill_kernel, dim3((unsigned)cdiv(nq, kFillQ)), dim3(256), 0, ctx->stream,
-                     nq, ctx->basekey.p, ctx->vmask.p, ctx_bins(ctx), ctx->vidx.p, ctx->voff.p,
-                     ctx->cursor.p, ctx->members.p);
+                     nq, ctx->basekey.p, ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1,
+                     ctx->vidx.p, ctx->voff.p, ctx->cursor.p, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   const int nblk = (int)cdiv(nq, kFillQ);
   hipLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->num_cus * 2)), dim3(kOrderT), 0,
@@ -1013,7 +1070,7 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   const int wg = std::max(1, ctx->num_cus * 4);
   hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
                      ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
-                     ctx->vmask.p, ctx_bins(ctx), nblk, ctx->members.p);
+                     ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, nblk, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   // PoseBin means depend only on the member lists: they run on the side stream, beside the
   // affine verification, and the main stream joins them at the next entry point (set_dev)
@@ -1049,24 +1106,25 @@ int launch_affine_gather(sod_ctx* ctx) {
   SOD_TRY(sod_reserve(ctx, ctx->aqx, (size_t)ctx->mmax));
   SOD_TRY(sod_reserve(ctx, ctx->aqy, (size_t)ctx->mmax));
   SOD_TRY(sod_reserve(ctx, ctx->aisig, (size_t)ctx->vmax));
+  if (ctx->n_qimg) SOD_TRY(sod_reserve(ctx, ctx->bwh, (size_t)ctx->vmax * 2));
   hipLaunchKernelGGL(affine_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
                      ctx->stream, ctx->scal.p, ctx->members.p, ctx->idx1.p + sod_win0(ctx),
                      ctx->mx.p, ctx->my.p, ctx->qx.p + sod_win0(ctx), ctx->qy.p + sod_win0(ctx),
-                     ctx->vbin.p, ctx_bins(ctx), ctx->amx.p, ctx->amy.p,
-                     ctx->aqx.p, ctx->aqy.p, ctx->aisig.p);
+                     ctx->vbin.p, ctx_bins(ctx), ctx->nbins1, ctx->n_qimg ? ctx->qshape.p : nullptr,
+                     ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p, ctx->aisig.p, ctx->bwh.p);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
 
 int launch_affine(sod_ctx* ctx, int64_t nb_host, bool count_on_device, const int64_t* offsets,
                   const float* mx, const float* my, const float* qx, const float* qy,
-                  const int32_t* isig, int32_t qw, int32_t qh, double xf, double yf, int32_t thr,
-                  int32_t max_iter, const double* params_in, uint8_t* surv, int32_t* votes,
-                  double* params, uint8_t* alive, const uint32_t* dev_count) {
+                  const int32_t* isig, int32_t qw, int32_t qh, const int32_t* bwh, double xf,
+                  double yf, int32_t thr, int32_t max_iter, const double* params_in, uint8_t* surv,
+                  int32_t* votes, double* params, uint8_t* alive, const uint32_t* dev_count) {
   const int wg = std::max(1, ctx->num_cus * 4);
   hipLaunchKernelGGL(affine_kernel, dim3(wg), dim3(256), 0, ctx->stream, nb_host,
                      count_on_device ? dev_count : nullptr, offsets, mx, my, qx, qy, isig, qw, qh,
-                     xf, yf, thr, max_iter, params_in, surv, votes, params, alive);
+                     bwh, xf, yf, thr, max_iter, params_in, surv, votes, params, alive);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }

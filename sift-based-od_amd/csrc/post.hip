@@ -29,6 +29,7 @@ constexpr double kRadToDeg = 180.0 / 3.141592653589793;   // CPython math.degree
 
 // one thread per (row i, 64-column word): bits of the position / orientation relations
 __global__ void post_adjacency_kernel(int n, int words, const double* __restrict__ m,
+                                      const int32_t* __restrict__ img,
                                       uint64_t* __restrict__ pos, uint64_t* __restrict__ ori) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)n * words) return;
@@ -39,7 +40,7 @@ __global__ void post_adjacency_kernel(int n, int words, const double* __restrict
   for (int k = 0; k < 64; ++k) {
     const int j = wd * 64 + k;
     if (j >= n) break;
-    if (j == i) continue;
+    if (j == i || (img && img[j] != img[i])) continue;   // batch: one image's bins only
     const double xj = m[6 * j], yj = m[6 * j + 1], aj = m[6 * j + 2], sj = m[6 * j + 3];
     const double dx = fabs(xi - xj), dy = fabs(yi - yj);
     const bool close = dx <= txi && dy <= tyi && dx <= m[6 * j + 4] * sj / 4 &&
@@ -87,23 +88,29 @@ struct PostOut {
   std::vector<double> pose;                          // 6 per cluster
 };
 
-int run_post(sod_ctx* ctx, int32_t n, const double* means_host, PostOut& out) {
+int run_post(sod_ctx* ctx, int32_t n, const double* means_host, const int32_t* img_host,
+             PostOut& out) {
   if (n <= 0) return SOD_OK;
   const int words = (n + 63) / 64;
   DevBuf<double>& dm = ctx->post_m;
   DevBuf<uint64_t>& dpos = ctx->post_pos;
   DevBuf<uint64_t>& dori = ctx->post_ori;
   int rc = sod_reserve(ctx, dm, (size_t)n * 6);
+  if (rc == SOD_OK && img_host) rc = sod_reserve(ctx, ctx->post_img, (size_t)n);
   if (rc == SOD_OK) rc = sod_reserve(ctx, dpos, (size_t)n * words);
   if (rc == SOD_OK) rc = sod_reserve(ctx, dori, (size_t)n * words);
   std::vector<uint64_t> pos((size_t)n * words), ori((size_t)n * words);
   if (rc == SOD_OK) {
     hipError_t e = hipMemcpyAsync(dm.p, means_host, (size_t)n * 6 * sizeof(double),
                                   hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess && img_host)
+      e = hipMemcpyAsync(ctx->post_img.p, img_host, (size_t)n * 4, hipMemcpyHostToDevice,
+                         ctx->stream);
     const int64_t threads = (int64_t)n * words;
     if (e == hipSuccess) {
       hipLaunchKernelGGL(post_adjacency_kernel, dim3((unsigned)((threads + 255) / 256)),
-                         dim3(256), 0, ctx->stream, n, words, dm.p, dpos.p, dori.p);
+                         dim3(256), 0, ctx->stream, n, words, dm.p,
+                         img_host ? ctx->post_img.p : nullptr, dpos.p, dori.p);
       e = hipGetLastError();
     }
     if (e == hipSuccess)
@@ -225,7 +232,7 @@ int sod_post_batch(sod_ctx* ctx, int32_t n, const double* means, int32_t* n_pos,
   if (n < 0 || (n > 0 && !means)) return sod_fail(ctx, SOD_EINVAL, "bad post-processing input");
   if (n > (1 << 20)) return sod_fail(ctx, SOD_EINVAL, "too many bins for post-processing");
   PostOut o;
-  SOD_TRY(run_post(ctx, n, means, o));
+  SOD_TRY(run_post(ctx, n, means, nullptr, o));
   return write_post(o, n_pos, pos_off, pos_members, n_ori, ori_pos_off, ori_off, ori_members,
                     final_orientation, final_pose);
 }
@@ -246,18 +253,26 @@ int sod_postprocess(sod_ctx* ctx, int32_t* n_bins, int32_t* bin_index, int32_t* 
                                   ctx->stream));
     SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
+  std::vector<uint32_t> lin;
+  if (ctx->n_qimg && V) {   // batch of query images: post-process each image's bins apart
+    lin.resize((size_t)V);
+    SOD_HIP(ctx, hipMemcpyAsync(lin.data(), ctx->vbin.p, (size_t)V * 4, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
   std::vector<double> sel;
-  std::vector<int32_t> idx;
+  std::vector<int32_t> idx, img;
   for (int64_t v = 0; v < V; ++v)
     if (surv[(size_t)v]) {
       idx.push_back((int32_t)v);
       sel.insert(sel.end(), means.begin() + 6 * v, means.begin() + 6 * v + 6);
+      if (!lin.empty()) img.push_back((int32_t)(lin[(size_t)v] / ctx->nbins1));
     }
   const int32_t n = (int32_t)idx.size();
   if (n_bins) *n_bins = n;
   if (bin_index && n) std::memcpy(bin_index, idx.data(), (size_t)n * sizeof(int32_t));
   PostOut o;
-  SOD_TRY(run_post(ctx, n, sel.data(), o));
+  SOD_TRY(run_post(ctx, n, sel.data(), img.empty() ? nullptr : img.data(), o));
   return write_post(o, n_pos, pos_off, pos_members, n_ori, ori_pos_off, ori_off, ori_members,
                     final_orientation, final_pose);
 }

@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 #include <stdint.h>
 #include <string>
+#include <vector>
 
 #include "../../include/sod.h"
 
@@ -54,6 +55,15 @@ struct sod_ctx {
   DevBuf<float> qn;             // nqt * 16
   DevBuf<float> qx, qy, qang;
   DevBuf<int32_t> qoct;
+  // batch of query images: image of each query, (h, w) per image;
+  // the bin key space is n_qimg x nbins (image-major), 0 = one image
+  int32_t n_qimg = 0;
+  DevBuf<int32_t> qimg;         // [nq]
+  DevBuf<int32_t> qshape;       // [n_qimg * 2] (h, w)
+  std::vector<int32_t> qoff_h, qshape_h;
+  int64_t nbins1 = 0;           // bins of one image (nbins = nbins1 * max(1, n_qimg))
+  DevBuf<int32_t> hist_rng;     // per query chunk: first / last bin slab it can touch
+  DevBuf<int32_t> bwh;          // per valid bin: query image (w, h) for the affine tolerance
   int32_t win0 = 0, winn = -1;  // query window of the Hough / select / affine stages
                                 // (-1 = all queries): one query image of a batch
   DevBuf<uint8_t> stage_u8;     // upload staging for descriptors
@@ -113,6 +123,7 @@ struct sod_ctx {
   // ---- post-processing (post.hip) ----
   DevBuf<double> post_m;        // [n*6] bin means
   DevBuf<uint64_t> post_pos, post_ori;   // [n * ceil(n/64)] relation bitmasks
+  DevBuf<int32_t> post_img;     // [n] query image of each bin (image batches)
 
   // ---- comm ----
   ncclComm_t comm = nullptr;
@@ -195,7 +206,8 @@ int launch_all_bins(sod_ctx* ctx);
 int launch_affine_gather(sod_ctx* ctx);
 int launch_affine(sod_ctx* ctx, int64_t nbins_dev_scalar_or_host, bool count_on_device,
                   const int64_t* offsets, const float* mx, const float* my, const float* qx,
-                  const float* qy, const int32_t* isig, int32_t qw, int32_t qh, double xf,
+                  const float* qy, const int32_t* isig, int32_t qw, int32_t qh,
+                  const int32_t* bwh /* per-bin (w, h) or nullptr */, double xf,
                   double yf, int32_t thr, int32_t max_iter, const double* params_in,
                   uint8_t* surv, int32_t* votes, double* params, uint8_t* alive,
                   const uint32_t* dev_count);

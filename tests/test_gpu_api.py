@@ -245,19 +245,22 @@ def test_packed_db_roundtrip(tmp_path, impl):
         assert np.array_equal(ref[1][k], got[1][k])
 
 
-def test_query_batch_equals_per_image():
-    """three query images matched in one DB pass, then per-image
-    Hough / select / affine / post-processing on query windows == each image alone."""
+@pytest.mark.parametrize("fused", [False, True])
+def test_query_batch_equals_per_image(fused):
+    """three query images matched in one DB pass, then the per-image
+    Hough / select / affine / post-processing (on query windows, or fused into one launch
+    per stage with image-major bin keys) == each image alone."""
     db = synthetic.make_database(8, 500, seed=61)
     imgs = []
-    for k, nq in enumerate((1200, 700, 1500)):
+    for k, (nq, shape) in enumerate(((1200, (800, 1000, 3)), (700, (600, 900, 3)),
+                                     (1500, (1000, 1200, 3)))):
         qs = synthetic.make_queries(nq, seed=62 + k, db_seed=61, kp_per_image=500,
-                                    n_objects=3)
+                                    n_objects=3, shape=shape)
         imgs.append((qs.des, qs.kp, qs.shape))
     with _lib.Context(0) as c:
         c.set_keypoints(db.kp, db.img, db.centroid, db.size)
         c.upload_db(db.des)
-        batch = sod.run_query_batch(c, imgs, bins=15)
+        batch = sod.run_query_batch(c, imgs, bins=15, fused=fused)
         for (des, kp_, shape), b in zip(imgs, batch):
             c.upload_queries(des, kp_)
             c.pipeline(shape, 15)

@@ -32,7 +32,11 @@ def per_image():
 
 
 def batched():
-    run_query_batch(ctx, imgs, bins=(32, 32, 8, 12), results=False)
+    run_query_batch(ctx, imgs, bins=(32, 32, 8, 12), results=False, fused=False)
+
+
+def fused():
+    run_query_batch(ctx, imgs, bins=(32, 32, 8, 12), results=False, fused=True)
 
 
 def match_only():
@@ -41,8 +45,8 @@ def match_only():
     ctx.match()
 
 
-for name, fn in (("per-image pipeline", per_image), ("batched (one DB pass)", batched),
-                 ("batched matcher alone", match_only)):
+for name, fn in (("per-image pipeline", per_image), ("batched, windowed stages", batched),
+                 ("batched, fused stages", fused), ("batched matcher alone", match_only)):
     fn()
     ctx.synchronize()
     t0 = time.perf_counter()
