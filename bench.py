@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)   # the clock settles over ~10 launches
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the SURVEY 8(f) side measurements (query batching, packed DB upload)")
     p.add_argument("--cpu-queries", type=int, default=4096)
     p.add_argument("--contexts", type=int, default=0,
                    help="query streams over the one resident DB (sod_db_share): consecutive "
@@ -192,6 +194,46 @@ def cpu_post_baseline(ctx, post):
     return {"value": dt * 1000.0, "unit": "ms", "cores": 1, "kind": "port",
             "sample": "oracle PostProcessing (Python, PostProcessing.py:4-112) on the %d "
                       "surviving bins, mean of %d runs" % (len(means), reps)}
+
+
+def extras(c, ctx, shard, bins, n_images=64, per_image=500):
+    """SURVEY 8(f) rows 2-3 on the same resident DB (outside the timed region):
+    * query batching: n_images small query images (per_image keypoints) in one matcher pass
+      with the fused per-image stages, vs one pipeline per image;
+    * DB upload: the packed image (one copy) vs raw descriptors (+ validation and packing)."""
+    from sift_based_od_amd import run_query_batch
+    imgs = []
+    for k in range(n_images):
+        q = synthetic.make_queries(per_image, seed=1000 + k, db_seed=0, kp_per_image=1000)
+        imgs.append((q.des, q.kp, q.shape))
+
+    def timed(fn, reps=3):
+        fn()
+        c.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        c.synchronize()
+        return (time.perf_counter() - t0) / reps * 1000.0
+
+    def one_by_one():
+        for d, k, shp in imgs:
+            c.upload_queries(d, k)
+            c.pipeline(shp, bins)
+
+    t_single = timed(one_by_one)
+    t_fused = timed(lambda: run_query_batch(c, imgs, bins=bins, results=False, fused=True))
+    packed = ctx.export_packed()
+    t_raw = timed(lambda: c.upload_db(shard))
+    t_packed = timed(lambda: c.import_packed(packed))
+    if c is not ctx:
+        c.share_db(ctx)     # back to the shared resident DB
+    return {"query_batch": {"images": n_images, "queries_per_image": per_image,
+                            "per_image_pipeline_ms": t_single, "fused_batch_ms": t_fused,
+                            "images_per_s": n_images / (t_fused / 1000.0),
+                            "speedup": t_single / t_fused},
+            "db_upload_ms": {"raw_descriptors": t_raw, "packed_image": t_packed,
+                             "rows": len(shard)}}
 
 
 def pmc_traffic(kernel, config):
@@ -376,6 +418,8 @@ def main():
         "exact_order": ctx.exact_order(),
         "datagen_s": gen_s,
     }
+    if world == 1 and not a.no_extras:
+        out["extras"] = extras(ctxs[-1], ctx, shard, bins)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(qs.des, shard, a.cpu_queries)
         out["cpu_baseline_hough"] = cpu_hough_baseline(qs, (x, y, ang, octv), img, cent, size,
