@@ -208,6 +208,9 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_XCD
 #define SOD_I8_XCD 1       // XCD-aware work-group -> (chunk, query block) order
 #endif
+#ifndef SOD_I8_EXP
+#define SOD_I8_EXP 0       // timing experiments only (wrong results): 1 no refill DMA,
+#endif                     // 2 no prefilter, 4 no stage wait/barrier
 #ifndef SOD_SHARED_T
 #define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
 #endif
@@ -337,15 +340,16 @@ __device__ __forceinline__ void match_unit(
     // the wave's loads of stage s are complete when at most the later prefetched stages'
     // loads remain in flight (vector memory returns in order)
     const int64_t younger = min<int64_t>(kRing - 2, nst - 1 - s);   // stages issued after s
-    if (kRing >= 4 && younger >= 2)
+    if (SOD_I8_EXP & 4) {
+    } else if (kRing >= 4 && younger >= 2)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kLoadsPerStage) : "memory");
     else if (kRing >= 3 && younger >= 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLoadsPerStage) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(SOD_I8_EXP & 4)) __builtin_amdgcn_s_barrier();
     // every wave has finished stage s-1, so its slot takes stage s+kRing-1
-    if (s + kRing - 1 < nst) {
+    if (!(SOD_I8_EXP & 1) && s + kRing - 1 < nst) {
       const int ns = slot == 0 ? kRing - 1 : slot - 1;
       issue_stage(dbpack, dn, npad, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageSlot, wave, lane);
     }
@@ -377,7 +381,16 @@ __device__ __forceinline__ void match_unit(
       for (int t = 0; t < QT; ++t)
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq[t][1], acc[t], 0, 0, 0);
       const int rowb = rowl + (int)((s * SPS + u) * kSubRows);
-#if SOD_I8_PIPE
+#if SOD_I8_EXP & 2
+#pragma unroll
+      for (int t = 0; t < QT; ++t) y1[t] = max(y1[t], acc[t][(u & 3)]);
+#pragma unroll
+      for (int i = 0; i < 2 * QT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        if (i < QT / 2) __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);
+        if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#elif SOD_I8_PIPE
       tile_update(accp, pp, rowp, y1, y2, t2, id);
 #pragma unroll
       for (int t = 0; t < QT; ++t) accp[t] = acc[t];
@@ -549,7 +562,7 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(w::kLoadsPerStage) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(SOD_I8_EXP & 4)) __builtin_amdgcn_s_barrier();
     if (s + w::kRing - 1 < nst) {
       const int ns = slot == 0 ? w::kRing - 1 : slot - 1;
       issue_stage_w(dbpack, dn, npad, s_lo + (s + w::kRing - 1) * w::SPS, lds + ns * w::kStageSlot,
