@@ -212,6 +212,29 @@ int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets,
                      const double* params_in, uint8_t* survived, int32_t* votes,
                      double* params, uint8_t* member_alive);
 
+/* ---- SIFT detect + describe on the device ------------------------
+ * Replaces `sift = cv2.SIFT_create()` + `sift.detectAndCompute(gray, None)` (main.py:179,
+ * :43; GenerateDatabaseInfo.py:16, :32).  OpenCV's algorithm (restated in
+ * oracle/sift_oracle.c) with default parameters unless sod_sift_set_params is called
+ * (nfeatures is applied by the Python layer).  detect runs the whole pyramid / extrema /
+ * orientation / ordering / descriptor pipeline on the device and returns the keypoint
+ * count; the keypoints are in OpenCV's output order (sorted by x, y, -size, angle,
+ * -response, -octave, duplicates removed) with OpenCV's fields (pt in input pixels, size,
+ * angle in degrees, response, packed octave) and descriptors are integer-valued floats
+ * [n*128].  detect_bgr takes an interleaved 8-bit BGR image (cvtColor BGR2GRAY first). */
+int sod_sift_set_params(sod_ctx* ctx, int32_t n_octave_layers, double contrast_threshold,
+                        double edge_threshold, double sigma);
+int sod_sift_detect(sod_ctx* ctx, const uint8_t* gray /* [h*w] */, int32_t width,
+                    int32_t height, int32_t* n_keypoints);
+int sod_sift_detect_bgr(sod_ctx* ctx, const uint8_t* bgr /* [h*w*3] */, int32_t width,
+                        int32_t height, int32_t* n_keypoints);
+/* copies min(n, cap) keypoints out; every pointer may be NULL */
+int sod_sift_get(sod_ctx* ctx, int32_t cap, float* x, float* y, float* size, float* angle,
+                 float* response, int32_t* octave, float* descriptors /* [cap*128] */);
+/* the last detection becomes the query set (descriptors + keypoints, device to device):
+ * main.py's get_query_features followed by run_matcher without a host round trip */
+int sod_sift_to_queries(sod_ctx* ctx);
+
 /* ---- host-side exchange (multi-rank over a host communicator, e.g. gloo) ------------
  * The same two exchange steps as the RCCL path, with the data staged through the host:
  * candidates_get -> all-gather -> candidates_merge; partial_get -> all-reduce ->

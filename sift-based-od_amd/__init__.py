@@ -16,6 +16,7 @@ Drop-in surface (reference names, reference semantics):
 * ``AffineParameters``, ``remove_outliers``                 (``AffineParameters.py``)
 * ``Main`` with ``run_matcher`` / ``apply_hough_transform`` / ``get_valid_bins`` /
   ``apply_affine_parameters`` / ``post_process``            (``main.py:17-168``)
+* ``SIFT_create().detectAndCompute(gray, None)`` on the device (``main.py:43,179``)
 * ``group_position``, ``group_orientation``, ``find_max_orientation``, ``get_final_pose``,
   ``dfs``                                                  (``PostProcessing.py``)
 
@@ -36,6 +37,7 @@ from .postprocessing import (dfs, find_max_orientation, get_final_pose,  # noqa:
                              group_orientation, group_position)
 from .sharded import HostComm, RcclComm, TorchHostComm, run_sharded, shard_range  # noqa: F401
 from .batch import run_query_batch  # noqa: F401
+from .sift import SIFT, SIFT_create, bgr_to_gray  # noqa: F401
 
 __all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid", "make_kp",
            "make_temp_kp", "unpack_sift_octave", "PoseBin", "BFMatcher", "DMatch", "knn2",
@@ -44,4 +46,4 @@ __all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid
            "AffineParameters", "Calc_x", "Ext_Params", "Gen_A", "Gen_b", "remove_outliers",
            "verify_bins", "Main", "dfs", "group_position", "group_orientation",
            "find_max_orientation", "get_final_pose", "run_query_batch", "HostComm", "RcclComm", "TorchHostComm", "run_sharded",
-           "shard_range"]
+           "shard_range", "SIFT", "SIFT_create", "bgr_to_gray"]

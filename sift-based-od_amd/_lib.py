@@ -93,6 +93,12 @@ SIGNATURES = {
     "sod_match_candidates_merge": (C.c_int, [c_ctx, C.c_int32, c_f32p, c_i32p, c_f32p]),
     "sod_hough_partial_get": (C.c_int, [c_ctx, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "sod_hough_partial_set": (C.c_int, [c_ctx, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "sod_sift_set_params": (C.c_int, [c_ctx, C.c_int32, C.c_double, C.c_double, C.c_double]),
+    "sod_sift_detect": (C.c_int, [c_ctx, c_u8p, C.c_int32, C.c_int32, c_i32p]),
+    "sod_sift_detect_bgr": (C.c_int, [c_ctx, c_u8p, C.c_int32, C.c_int32, c_i32p]),
+    "sod_sift_get": (C.c_int, [c_ctx, C.c_int32, c_f32p, c_f32p, c_f32p, c_f32p, c_f32p, c_i32p,
+                               c_f32p]),
+    "sod_sift_to_queries": (C.c_int, [c_ctx]),
     "sod_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
     "sod_comm_init": (C.c_int, [c_ctx, C.c_int32, C.c_int32, C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
 }
@@ -448,6 +454,49 @@ class Context:
                      ptr(a["ori_members"], C.c_int32), ptr(a["orient"], C.c_double),
                      ptr(a["pose"], C.c_double)))
         return self._post_result(a, n)
+
+    # -- SIFT on the device --
+    def sift_params(self, n_octave_layers=3, contrast_threshold=0.04, edge_threshold=10.0,
+                    sigma=1.6):
+        self._chk(self._L.sod_sift_set_params(self._h, int(n_octave_layers),
+                                              float(contrast_threshold), float(edge_threshold),
+                                              float(sigma)))
+
+    def sift_detect(self, image, descriptors=True):
+        """detectAndCompute on an 8-bit gray [h, w] or BGR [h, w, 3|4] image: SoA keypoints
+        (x, y, size, angle, response, octave) in OpenCV's order (+ float32 [n, 128])."""
+        img = np.asarray(image)
+        if img.dtype != np.uint8:
+            raise TypeError("SIFT input must be an 8-bit image")
+        n = C.c_int32()
+        if img.ndim == 2:
+            g = _c(img, np.uint8)
+            self._chk(self._L.sod_sift_detect(self._h, ptr(g, C.c_uint8), g.shape[1], g.shape[0],
+                                              C.byref(n)))
+        elif img.ndim == 3 and img.shape[2] in (3, 4):
+            b = _c(img[:, :, :3], np.uint8)
+            self._chk(self._L.sod_sift_detect_bgr(self._h, ptr(b, C.c_uint8), b.shape[1],
+                                                  b.shape[0], C.byref(n)))
+        else:
+            raise ValueError("SIFT input must be [h, w] or [h, w, 3|4]")
+        n = n.value
+        out = {k: np.zeros(n, np.float32) for k in ("x", "y", "size", "angle", "response")}
+        out["octave"] = np.zeros(n, np.int32)
+        desc = np.zeros((n, 128), np.float32) if descriptors else None
+        self._chk(self._L.sod_sift_get(
+            self._h, n, ptr(out["x"], C.c_float), ptr(out["y"], C.c_float),
+            ptr(out["size"], C.c_float), ptr(out["angle"], C.c_float),
+            ptr(out["response"], C.c_float), ptr(out["octave"], C.c_int32),
+            ptr(desc, C.c_float)))
+        if descriptors:
+            out["descriptors"] = desc
+        self._sift_n = n
+        return out
+
+    def sift_to_queries(self):
+        """The last SIFT detection becomes the query set (device to device)."""
+        self._chk(self._L.sod_sift_to_queries(self._h))
+        self.nq = self._sift_n
 
     def post_batch(self, means):
         """PostProcessing.py:4-112 on PoseBin means [n, 6] = (x, y, angle, scale, w, h)."""

@@ -99,6 +99,7 @@ void sod_destroy(sod_ctx* ctx) {
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
+  sod_sift_free(ctx);
   sod_release(ctx->mx); sod_release(ctx->my); sod_release(ctx->mang);
   sod_release(ctx->moct); sod_release(ctx->mimg); sod_release(ctx->cent); sod_release(ctx->isize);
   sod_release(ctx->dbpack); sod_release(ctx->dn); sod_release(ctx->qpack); sod_release(ctx->qn);

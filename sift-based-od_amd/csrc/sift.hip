@@ -1,0 +1,946 @@
+// sift.hip -- SIFT detect + describe on the device (the step before
+// matching; the reference calls `cv2.SIFT_create().detectAndCompute(gray, None)` at
+// main.py:43 and GenerateDatabaseInfo.py:32, OpenCV >= 4.4, default parameters).
+//
+// The algorithm is OpenCV's (features2d/src/sift.simd.hpp, restated in
+// oracle/sift_oracle.c); the arithmetic OpenCV leaves to SIMD/IPP/its math kernels is
+// fixed to one definition shared by both sides, so device and oracle agree bit for bit:
+// separable blur as row pass then column pass with symmetric-pair sums in increasing
+// tap order, no FMA (this file is compiled with -ffp-contract=off), exp / sin / cos /
+// 2^y through double-precision Cody-Waite + Taylor kernels, correctly rounded float sqrt,
+// OpenCV's fastAtan2 polynomial.
+//
+// Device pipeline for one image (all on the context stream, one host sync at the end):
+//   upscale x2 (exact) -> blur -> per octave: 5 incremental blurs, the column pass also
+//   writing the DoG layer -> nearest /2 for the next octave ->
+//   extrema (one thread per pixel of DoG layers 1..L, 26-neighbour test, compacted by an
+//   atomic counter) -> refine (one thread per candidate: Newton steps, contrast / edge
+//   tests, 36-bin orientation histogram, one keypoint per peak) ->
+//   order (OpenCV sorts and removes duplicates, so the output order is the sort order and
+//   independent of discovery order: rank = number of keypoints before it) ->
+//   descriptors (one thread per keypoint, 4x4x8 trilinear histogram).
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "sod_internal.h"
+
+namespace {
+
+constexpr int kBorder = 5;              // SIFT_IMG_BORDER
+constexpr int kMaxInterp = 5;           // SIFT_MAX_INTERP_STEPS
+constexpr int kOriBins = 36;            // SIFT_ORI_HIST_BINS
+constexpr float kOriSigFctr = 1.5f;     // SIFT_ORI_SIG_FCTR
+constexpr float kOriRadius = 3 * kOriSigFctr;
+constexpr float kOriPeakRatio = 0.8f;
+constexpr int kD = 4, kN = 8;           // SIFT_DESCR_WIDTH, SIFT_DESCR_HIST_BINS
+constexpr float kDescrSclFctr = 3.f, kDescrMagThr = 0.2f, kIntDescrFctr = 512.f;
+constexpr int kFirstOctave = -1;
+constexpr int kMaxOct = 24;
+constexpr int kMaxLayers = 8;           // nOctaveLayers + 3 <= kMaxLayers
+constexpr int kMaxTaps = 64;
+
+struct Oct {
+  int w, h;
+  int64_t g;   // offset of layer 0 of this octave in the Gaussian buffer
+  int64_t d;   // offset of layer 0 in the DoG buffer
+};
+struct Pyr {
+  Oct o[kMaxOct];
+  int n, L;
+};
+
+struct Kp {   // final form (firstOctave rescale applied)
+  float x, y, size, angle, response;
+  int octave;
+  int pad0, pad1;
+};
+
+// ---- arithmetic shared with oracle/sift_oracle.c --------------------------------------
+__host__ __device__ inline int reflect101(int p, int len) {
+  if ((unsigned)p < (unsigned)len) return p;
+  if (len == 1) return 0;
+  do {
+    p = p < 0 ? -p : len - 1 - (p - len) - 1;
+  } while ((unsigned)p >= (unsigned)len);
+  return p;
+}
+
+__device__ inline int rnd(float v) { return (int)__builtin_rintf(v); }   // cvRound
+__device__ inline int flo(float v) {                                     // cvFloor
+  const int i = (int)v;
+  return i - (i > v);
+}
+
+// e^x: Cody-Waite reduction by ln2 and a Taylor polynomial to r^13 (|r| <= 0.35)
+__device__ inline double s_exp(double x) {
+  if (x < -740.0) return 0.0;
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double n = __builtin_rint(x * 1.44269504088896338700e+00);
+  const double r = (x - n * ln2_hi) - n * ln2_lo;
+  double p = 1.0 / 6227020800.0;
+  p = p * r + 1.0 / 479001600.0;
+  p = p * r + 1.0 / 39916800.0;
+  p = p * r + 1.0 / 3628800.0;
+  p = p * r + 1.0 / 362880.0;
+  p = p * r + 1.0 / 40320.0;
+  p = p * r + 1.0 / 5040.0;
+  p = p * r + 1.0 / 720.0;
+  p = p * r + 1.0 / 120.0;
+  p = p * r + 1.0 / 24.0;
+  p = p * r + 1.0 / 6.0;
+  p = p * r + 0.5;
+  p = p * r + 1.0;
+  p = p * r + 1.0;
+  return __builtin_ldexp(p, (int)n);
+}
+
+// sin and cos: reduction by pi/2 (two-part constant), Taylor polynomials to r^21 / r^22
+// (|r| <= pi/4: truncation below 1e-24)
+__device__ inline void s_sincos(double a, double* sn, double* cs) {
+  const double pio2_hi = 1.57079632673412561417e+00, pio2_lo = 6.07710050650619224932e-11;
+  const double k = __builtin_rint(a * 6.36619772367581382433e-01);
+  const double r = (a - k * pio2_hi) - k * pio2_lo;
+  const double r2 = r * r;
+  double s = 1.0 / 51090942171709440000.0;   // 1/21!
+  s = s * r2 - 1.0 / 121645100408832000.0;   // 1/19!
+  s = s * r2 + 1.0 / 355687428096000.0;      // 1/17!
+  s = s * r2 - 1.0 / 1307674368000.0;        // 1/15!
+  s = s * r2 + 1.0 / 6227020800.0;           // 1/13!
+  s = s * r2 - 1.0 / 39916800.0;             // 1/11!
+  s = s * r2 + 1.0 / 362880.0;               // 1/9!
+  s = s * r2 - 1.0 / 5040.0;                 // 1/7!
+  s = s * r2 + 1.0 / 120.0;                  // 1/5!
+  s = s * r2 - 1.0 / 6.0;                    // 1/3!
+  s = r + r * r2 * s;
+  double c = -1.0 / 1124000727777607680000.0;   // 1/22!
+  c = c * r2 + 1.0 / 2432902008176640000.0;     // 1/20!
+  c = c * r2 - 1.0 / 6402373705728000.0;        // 1/18!
+  c = c * r2 + 1.0 / 20922789888000.0;          // 1/16!
+  c = c * r2 - 1.0 / 87178291200.0;             // 1/14!
+  c = c * r2 + 1.0 / 479001600.0;               // 1/12!
+  c = c * r2 - 1.0 / 3628800.0;                 // 1/10!
+  c = c * r2 + 1.0 / 40320.0;                   // 1/8!
+  c = c * r2 - 1.0 / 720.0;                     // 1/6!
+  c = c * r2 + 1.0 / 24.0;                      // 1/4!
+  c = c * r2 - 0.5;
+  c = 1.0 + r2 * c;
+  switch (((int)k) & 3) {
+    case 0: *sn = s; *cs = c; break;
+    case 1: *sn = c; *cs = -s; break;
+    case 2: *sn = -s; *cs = -c; break;
+    default: *sn = -c; *cs = s; break;
+  }
+}
+
+// floor(sqrt(v)) exactly
+__host__ __device__ inline int isqrt64(int64_t v) {
+  int64_t d = (int64_t)__builtin_sqrt((double)v);
+  while (d > 0 && d * d > v) --d;
+  while ((d + 1) * (d + 1) <= v) ++d;
+  return (int)d;
+}
+
+// correctly rounded float sqrt: double estimate, then the exact midpoint tests (a float
+// midpoint has 25 significant bits, its square is exact in double)
+__device__ inline float sqrt_rn(float x) {
+  if (!(x > 0.f)) return x == 0.f ? 0.f : __builtin_nanf("");
+  float s = (float)__builtin_sqrt((double)x);
+  const double xd = (double)x;
+  const unsigned bits = __float_as_uint(s);   // s > 0 and finite
+  const float up = __uint_as_float(bits + 1u), dn = __uint_as_float(bits - 1u);
+  const double mu = ((double)s + (double)up) * 0.5, md = ((double)s + (double)dn) * 0.5;
+  if (mu * mu < xd) s = up;
+  else if (md * md > xd) s = dn;
+  return s;
+}
+
+__device__ inline float fexp(float x) { return (float)s_exp((double)x); }
+__device__ inline float fmag(float x, float y) { return sqrt_rn(x * x + y * y); }
+
+// cv::hal::fastAtan2 (degrees), scalar form
+__device__ inline float fast_atan2(float y, float x) {
+  const float d2r = (float)(180 / 3.14159265358979323846);
+  const float p1 = 0.9997878412794807f * d2r, p3 = -0.3258083974640975f * d2r,
+              p5 = 0.1555786518463281f * d2r, p7 = -0.04432655554792128f * d2r;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)2.220446049250313e-16);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + (float)2.220446049250313e-16);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+// ---- pyramid kernels ------------------------------------------------------------------
+// x2 INTER_LINEAR of an 8-bit image (every value is a multiple of 1/16: exact)
+__device__ inline float up_row(const uint8_t* g, int w, int y, int d) {
+  const int i = d >> 1;
+  const uint8_t* r = g + (size_t)y * w;
+  if (d & 1) return i + 1 < w ? 0.75f * r[i] + 0.25f * r[i + 1] : (float)r[i];
+  return i > 0 ? 0.25f * r[i - 1] + 0.75f * r[i] : (float)r[i];
+}
+__global__ void upscale_kernel(const uint8_t* __restrict__ g, int w, int h, float* __restrict__ u) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, d = blockIdx.y;
+  if (x >= 2 * w) return;
+  const int i = d >> 1;
+  float v;
+  if (d & 1)
+    v = i + 1 < h ? 0.75f * up_row(g, w, i, x) + 0.25f * up_row(g, w, i + 1, x) : up_row(g, w, i, x);
+  else
+    v = i > 0 ? 0.25f * up_row(g, w, i - 1, x) + 0.75f * up_row(g, w, i, x) : up_row(g, w, i, x);
+  u[(size_t)d * 2 * w + x] = v;
+}
+
+// row pass: out = k0*x + sum_i k_i * (x[-i] + x[+i]), BORDER_REFLECT_101
+__global__ void blur_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, int w,
+                                 const float* __restrict__ k, int r) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w) return;
+  const float* row = src + (size_t)y * w;
+  float s = k[0] * row[x];
+  if (x >= r && x + r < w) {
+    for (int i = 1; i <= r; ++i) s += k[i] * (row[x - i] + row[x + i]);
+  } else {
+    for (int i = 1; i <= r; ++i) s += k[i] * (row[reflect101(x - i, w)] + row[reflect101(x + i, w)]);
+  }
+  dst[(size_t)y * w + x] = s;
+}
+
+// column pass; with `dog` it also writes dog = out - prev (the layer the blur started from)
+__global__ void blur_cols_kernel(const float* __restrict__ src, float* __restrict__ dst, int w,
+                                 int h, const float* __restrict__ k, int r,
+                                 const float* __restrict__ prev, float* __restrict__ dog) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w) return;
+  float s = k[0] * src[(size_t)y * w + x];
+  if (y >= r && y + r < h) {
+    for (int i = 1; i <= r; ++i)
+      s += k[i] * (src[(size_t)(y - i) * w + x] + src[(size_t)(y + i) * w + x]);
+  } else {
+    for (int i = 1; i <= r; ++i)
+      s += k[i] * (src[(size_t)reflect101(y - i, h) * w + x] + src[(size_t)reflect101(y + i, h) * w + x]);
+  }
+  const size_t o = (size_t)y * w + x;
+  dst[o] = s;
+  if (dog) dog[o] = s - prev[o];
+}
+
+__global__ void down2_kernel(const float* __restrict__ src, int sw, float* __restrict__ dst, int dw) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= dw) return;
+  dst[(size_t)y * dw + x] = src[(size_t)(2 * y) * sw + 2 * x];
+}
+
+// ---- extrema --------------------------------------------------------------------------
+__global__ void extrema_kernel(const float* __restrict__ dogs, Pyr P, int o, float thr,
+                               int4* __restrict__ cand, unsigned* __restrict__ ncand, int cap) {
+  const Oct& q = P.o[o];
+  const int x = blockIdx.x * blockDim.x + threadIdx.x + kBorder, y = blockIdx.y + kBorder;
+  const int layer = blockIdx.z + 1;
+  if (x >= q.w - kBorder) return;
+  const size_t plane = (size_t)q.w * q.h;
+  const float* cur = dogs + q.d + plane * layer;
+  const size_t c = (size_t)y * q.w + x;
+  const float val = cur[c];
+  if (!(fabsf(val) > thr)) return;
+  const int step = q.w;
+  bool ext = true;
+#pragma unroll
+  for (int dl = -1; dl <= 1; ++dl) {
+    const float* m = cur + (ptrdiff_t)plane * dl;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!dl && !dy && !dx) continue;
+        const float v = m[c + (ptrdiff_t)dy * step + dx];
+        ext = ext && (val > 0 ? val >= v : val <= v);
+      }
+  }
+  if (!ext) return;
+  const unsigned i = atomicAdd(ncand, 1u);
+  if (i < (unsigned)cap) cand[i] = make_int4(o, layer, y, x);
+}
+
+// ---- refine + orientation -------------------------------------------------------------
+__device__ inline float at(const float* img, int w, int y, int x) { return img[(size_t)y * w + x]; }
+
+__device__ bool adjust_local_extrema(const float* dogs, const Pyr& P, int octv, int& layer,
+                                     int& r, int& c, float contrastThreshold,
+                                     float edgeThreshold, float sigma, Kp& kpt) {
+  const int L = P.L;
+  const Oct& q = P.o[octv];
+  const size_t plane = (size_t)q.w * q.h;
+  const int w = q.w;
+  const float img_scale = 1.f / (255 * 1);
+  const float deriv_scale = img_scale * 0.5f;
+  const float second_deriv_scale = img_scale;
+  const float cross_deriv_scale = img_scale * 0.25f;
+  float xi = 0, xr = 0, xc = 0, contr = 0;
+  int i = 0;
+  for (; i < kMaxInterp; i++) {
+    const float* img = dogs + q.d + plane * layer;
+    const float* prev = img - plane;
+    const float* next = img + plane;
+    const float dD0 = (at(img, w, r, c + 1) - at(img, w, r, c - 1)) * deriv_scale;
+    const float dD1 = (at(img, w, r + 1, c) - at(img, w, r - 1, c)) * deriv_scale;
+    const float dD2 = (at(next, w, r, c) - at(prev, w, r, c)) * deriv_scale;
+    const float v2 = at(img, w, r, c) * 2;
+    const float dxx = (at(img, w, r, c + 1) + at(img, w, r, c - 1) - v2) * second_deriv_scale;
+    const float dyy = (at(img, w, r + 1, c) + at(img, w, r - 1, c) - v2) * second_deriv_scale;
+    const float dss = (at(next, w, r, c) + at(prev, w, r, c) - v2) * second_deriv_scale;
+    const float dxy = (at(img, w, r + 1, c + 1) - at(img, w, r + 1, c - 1) -
+                       at(img, w, r - 1, c + 1) + at(img, w, r - 1, c - 1)) * cross_deriv_scale;
+    const float dxs = (at(next, w, r, c + 1) - at(next, w, r, c - 1) - at(prev, w, r, c + 1) +
+                       at(prev, w, r, c - 1)) * cross_deriv_scale;
+    const float dys = (at(next, w, r + 1, c) - at(next, w, r - 1, c) - at(prev, w, r + 1, c) +
+                       at(prev, w, r - 1, c)) * cross_deriv_scale;
+    // Matx33f::solve(DECOMP_LU): Cramer's rule in float, zero vector when det == 0
+    const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs,
+                a21 = dys, a22 = dss;
+    float det = a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) +
+                a02 * (a10 * a21 - a20 * a11);
+    float X0 = 0, X1 = 0, X2 = 0;
+    if (det != 0) {
+      det = 1 / det;
+      X0 = det * (dD0 * (a11 * a22 - a12 * a21) - a01 * (dD1 * a22 - a12 * dD2) +
+                  a02 * (dD1 * a21 - a11 * dD2));
+      X1 = det * (a00 * (dD1 * a22 - a12 * dD2) - dD0 * (a10 * a22 - a12 * a20) +
+                  a02 * (a10 * dD2 - dD1 * a20));
+      X2 = det * (a00 * (a11 * dD2 - dD1 * a21) - a01 * (a10 * dD2 - dD1 * a20) +
+                  dD0 * (a10 * a21 - a11 * a20));
+    }
+    xi = -X2;
+    xr = -X1;
+    xc = -X0;
+    if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+    if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) ||
+        fabsf(xc) > (float)(INT_MAX / 3))
+      return false;
+    c += rnd(xc);
+    r += rnd(xr);
+    layer += rnd(xi);
+    if (layer < 1 || layer > L || c < kBorder || c >= q.w - kBorder || r < kBorder ||
+        r >= q.h - kBorder)
+      return false;
+  }
+  if (i >= kMaxInterp) return false;
+  {
+    const float* img = dogs + q.d + plane * layer;
+    const float* prev = img - plane;
+    const float* next = img + plane;
+    const float dD0 = (at(img, w, r, c + 1) - at(img, w, r, c - 1)) * deriv_scale;
+    const float dD1 = (at(img, w, r + 1, c) - at(img, w, r - 1, c)) * deriv_scale;
+    const float dD2 = (at(next, w, r, c) - at(prev, w, r, c)) * deriv_scale;
+    float t = 0;
+    t += dD0 * xc;
+    t += dD1 * xr;
+    t += dD2 * xi;
+    contr = at(img, w, r, c) * img_scale + t * 0.5f;
+    if (fabsf(contr) * L < contrastThreshold) return false;
+    const float v2 = at(img, w, r, c) * 2.f;
+    const float dxx = (at(img, w, r, c + 1) + at(img, w, r, c - 1) - v2) * second_deriv_scale;
+    const float dyy = (at(img, w, r + 1, c) + at(img, w, r - 1, c) - v2) * second_deriv_scale;
+    const float dxy = (at(img, w, r + 1, c + 1) - at(img, w, r + 1, c - 1) -
+                       at(img, w, r - 1, c + 1) + at(img, w, r - 1, c - 1)) * cross_deriv_scale;
+    const float tr = dxx + dyy;
+    const float dt = dxx * dyy - dxy * dxy;
+    if (dt <= 0 || tr * tr * edgeThreshold >= (edgeThreshold + 1) * (edgeThreshold + 1) * dt)
+      return false;
+  }
+  kpt.x = (c + xc) * (1 << octv);
+  kpt.y = (r + xr) * (1 << octv);
+  kpt.octave = octv + (layer << 8) + ((int)__builtin_rint(((double)xi + 0.5) * 255) << 16);
+  kpt.size = sigma * (float)s_exp((double)((layer + xi) / L) * 0.6931471805599453) * (1 << octv) * 2;
+  kpt.response = fabsf(contr);
+  return true;
+}
+
+__global__ void refine_kernel(const float* __restrict__ gauss, const float* __restrict__ dogs,
+                              Pyr P, const int4* __restrict__ cand,
+                              const unsigned* __restrict__ ncand, int cap, float contrastThreshold,
+                              float edgeThreshold, float sigma, Kp* __restrict__ kps,
+                              unsigned* __restrict__ nkp, int kcap) {
+  const unsigned id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= min(*ncand, (unsigned)cap)) return;
+  const int4 cd = cand[id];
+  const int o = cd.x;
+  int layer = cd.y, r = cd.z, c = cd.w;
+  Kp kpt;
+  if (!adjust_local_extrema(dogs, P, o, layer, r, c, contrastThreshold, edgeThreshold, sigma, kpt))
+    return;
+  // calcOrientationHist on Gaussian layer `layer` of octave o at (c, r)
+  const Oct& q = P.o[o];
+  const float* img = gauss + q.g + (size_t)q.w * q.h * layer;
+  const float scl_octv = kpt.size * 0.5f / (1 << o);
+  const int radius = rnd(kOriRadius * scl_octv);
+  const float osig = kOriSigFctr * scl_octv;
+  const float expf_scale = -1.f / (2.f * osig * osig);
+  float tmp[kOriBins + 4];
+  float* temphist = tmp + 2;
+  for (int i = 0; i < kOriBins; i++) temphist[i] = 0.f;
+  for (int i = -radius; i <= radius; i++) {
+    const int y = r + i;
+    if (y <= 0 || y >= q.h - 1) continue;
+    for (int j = -radius; j <= radius; j++) {
+      const int x = c + j;
+      if (x <= 0 || x >= q.w - 1) continue;
+      const float dx = at(img, q.w, y, x + 1) - at(img, q.w, y, x - 1);
+      const float dy = at(img, q.w, y - 1, x) - at(img, q.w, y + 1, x);
+      const float wgt = fexp((i * i + j * j) * expf_scale);
+      const float ori = fast_atan2(dy, dx);
+      const float mag = fmag(dx, dy);
+      int bin = rnd((kOriBins / 360.f) * ori);
+      if (bin >= kOriBins) bin -= kOriBins;
+      if (bin < 0) bin += kOriBins;
+      temphist[bin] += wgt * mag;
+    }
+  }
+  temphist[-1] = temphist[kOriBins - 1];
+  temphist[-2] = temphist[kOriBins - 2];
+  temphist[kOriBins] = temphist[0];
+  temphist[kOriBins + 1] = temphist[1];
+  float hist[kOriBins];
+  for (int i = 0; i < kOriBins; i++)
+    hist[i] = (temphist[i - 2] + temphist[i + 2]) * (1.f / 16.f) +
+              (temphist[i - 1] + temphist[i + 1]) * (4.f / 16.f) + temphist[i] * (6.f / 16.f);
+  float omax = hist[0];
+  for (int i = 1; i < kOriBins; i++) omax = fmaxf(omax, hist[i]);
+  const float mag_thr = omax * kOriPeakRatio;
+  // firstOctave = -1 rescale (exact, so it commutes with OpenCV's later sort / dedup)
+  const float scale = 1.f / (float)(1 << -kFirstOctave);
+  Kp out = kpt;
+  out.octave = (kpt.octave & ~255) | ((kpt.octave + kFirstOctave) & 255);
+  out.x = kpt.x * scale;
+  out.y = kpt.y * scale;
+  out.size = kpt.size * scale;
+  out.pad0 = out.pad1 = 0;
+  for (int j = 0; j < kOriBins; j++) {
+    const int l = j > 0 ? j - 1 : kOriBins - 1;
+    const int r2 = j < kOriBins - 1 ? j + 1 : 0;
+    if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+      float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
+      bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
+      out.angle = 360.f - (float)((360.f / kOriBins) * bin);
+      if (fabsf(out.angle - 360.f) < 1.1920928955078125e-07f) out.angle = 0.f;
+      const unsigned k = atomicAdd(nkp, 1u);
+      if (k < (unsigned)kcap) kps[k] = out;
+    }
+  }
+}
+
+// ---- OpenCV order: KeyPointsFilter::removeDuplicatedSorted ----------------------------
+// KeyPoint12_LessThan, with the array index as the last key (a total order)
+__device__ inline bool kp_less(const Kp& a, int ia, const Kp& b, int ib) {
+  if (a.x != b.x) return a.x < b.x;
+  if (a.y != b.y) return a.y < b.y;
+  if (a.size != b.size) return a.size > b.size;
+  if (a.angle != b.angle) return a.angle < b.angle;
+  if (a.response != b.response) return a.response > b.response;
+  if (a.octave != b.octave) return a.octave > b.octave;
+  return ia < ib;
+}
+__device__ inline bool kp_same(const Kp& a, const Kp& b) {
+  return a.x == b.x && a.y == b.y && a.size == b.size && a.angle == b.angle;
+}
+
+constexpr int kRankTile = 256;
+// pass 0: dup[i] = an equal (x, y, size, angle) keypoint precedes i;
+// pass 1: pos[i] = number of kept keypoints before i (sorted position), -1 when dropped
+__global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ kps,
+                                                         const unsigned* __restrict__ nkp, int kcap,
+                                                         int pass, uint8_t* __restrict__ dup,
+                                                         int* __restrict__ pos,
+                                                         unsigned* __restrict__ nfinal) {
+  __shared__ Kp tile[kRankTile];
+  __shared__ uint8_t tdup[kRankTile];
+  const int n = (int)min(*nkp, (unsigned)kcap);
+  const int i = blockIdx.x * kRankTile + threadIdx.x;
+  if (blockIdx.x * kRankTile >= n) return;
+  Kp me{};
+  if (i < n) me = kps[i];
+  int cnt = 0;
+  bool d = false;
+  for (int t0 = 0; t0 < n; t0 += kRankTile) {
+    __syncthreads();
+    if (t0 + (int)threadIdx.x < n) {
+      tile[threadIdx.x] = kps[t0 + threadIdx.x];
+      tdup[threadIdx.x] = pass ? dup[t0 + threadIdx.x] : 0;
+    }
+    __syncthreads();
+    const int m = min(kRankTile, n - t0);
+    if (i < n) {
+      for (int j = 0; j < m; ++j) {
+        const Kp& o = tile[j];
+        const bool lt = kp_less(o, t0 + j, me, i);
+        if (pass == 0)
+          d = d || (lt && kp_same(o, me));
+        else
+          cnt += (lt && !tdup[j]) ? 1 : 0;
+      }
+    }
+  }
+  if (i >= n) return;
+  if (pass == 0) {
+    dup[i] = d ? 1 : 0;
+    if (!d) atomicAdd(nfinal, 1u);
+  } else {
+    pos[i] = dup[i] ? -1 : cnt;
+  }
+}
+
+__global__ void scatter_kernel(const Kp* __restrict__ kps, const unsigned* __restrict__ nkp,
+                               int kcap, const int* __restrict__ pos, Kp* __restrict__ sorted) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int)min(*nkp, (unsigned)kcap)) return;
+  const int p = pos[i];
+  if (p >= 0) sorted[p] = kps[i];
+}
+
+// ---- descriptors: calcSIFTDescriptor, one thread per keypoint -------------------------
+__global__ void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
+                                  const Kp* __restrict__ sorted, const unsigned* __restrict__ nfinal,
+                                  float* __restrict__ desc) {
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (int)*nfinal) return;
+  const Kp k = sorted[id];
+  int octave = k.octave & 255;
+  const int layer = (k.octave >> 8) & 255;
+  octave = octave < 128 ? octave : (-128 | octave);
+  const float sc = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
+  const float size = k.size * sc;
+  const Oct& q = P.o[octave - kFirstOctave];
+  const float* img = gauss + q.g + (size_t)q.w * q.h * layer;
+  float ori = 360.f - k.angle;
+  if (fabsf(ori - 360.f) < 1.1920928955078125e-07f) ori = 0.f;
+  const float scl = size * 0.5f;
+  const float ptx = k.x * sc, pty = k.y * sc;
+
+  const int px = rnd(ptx), py = rnd(pty);
+  double sd, cd;
+  s_sincos((double)(ori * (float)(3.14159265358979323846 / 180)), &sd, &cd);
+  float cos_t = (float)cd, sin_t = (float)sd;
+  const float bins_per_rad = kN / 360.f;
+  const float exp_scale = -1.f / (kD * kD * 0.5f);
+  const float hist_width = kDescrSclFctr * scl;
+  int radius = rnd(hist_width * 1.4142135623730951f * (kD + 1) * 0.5f);
+  const int diag = isqrt64((int64_t)q.w * q.w + (int64_t)q.h * q.h);
+  radius = min(radius, diag);
+  cos_t /= hist_width;
+  sin_t /= hist_width;
+  const int rows = q.h, cols = q.w;
+  float hist[(kD + 2) * (kD + 2) * (kN + 2)];
+  for (int i = 0; i < (kD + 2) * (kD + 2) * (kN + 2); i++) hist[i] = 0.f;
+  for (int i = -radius; i <= radius; i++)
+    for (int j = -radius; j <= radius; j++) {
+      const float c_rot = j * cos_t - i * sin_t;
+      const float r_rot = j * sin_t + i * cos_t;
+      float rbin = r_rot + kD / 2 - 0.5f;
+      float cbin = c_rot + kD / 2 - 0.5f;
+      const int r = py + i, c = px + j;
+      if (!(rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 &&
+            c < cols - 1))
+        continue;
+      const float dx = at(img, cols, r, c + 1) - at(img, cols, r, c - 1);
+      const float dy = at(img, cols, r - 1, c) - at(img, cols, r + 1, c);
+      const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
+      const float o_k = fast_atan2(dy, dx);
+      const float mag_k = fmag(dx, dy);
+      const float w_k = fexp(wexp);
+      float obin = (o_k - ori) * bins_per_rad;
+      const float mag = mag_k * w_k;
+      const int r0 = flo(rbin), c0 = flo(cbin);
+      int o0 = flo(obin);
+      rbin -= r0;
+      cbin -= c0;
+      obin -= o0;
+      if (o0 < 0) o0 += kN;
+      if (o0 >= kN) o0 -= kN;
+      const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+      const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+      const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+      const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+      const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+      const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+      const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+      const int idx = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
+      hist[idx] += v_rco000;
+      hist[idx + 1] += v_rco001;
+      hist[idx + (kN + 2)] += v_rco010;
+      hist[idx + (kN + 3)] += v_rco011;
+      hist[idx + (kD + 2) * (kN + 2)] += v_rco100;
+      hist[idx + (kD + 2) * (kN + 2) + 1] += v_rco101;
+      hist[idx + (kD + 3) * (kN + 2)] += v_rco110;
+      hist[idx + (kD + 3) * (kN + 2) + 1] += v_rco111;
+    }
+  float raw[kD * kD * kN];
+  for (int i = 0; i < kD; i++)
+    for (int j = 0; j < kD; j++) {
+      const int idx = ((i + 1) * (kD + 2) + (j + 1)) * (kN + 2);
+      hist[idx] += hist[idx + kN];
+      hist[idx + 1] += hist[idx + kN + 1];
+      for (int k2 = 0; k2 < kN; k2++) raw[(i * kD + j) * kN + k2] = hist[idx + k2];
+    }
+  constexpr int len = kD * kD * kN;
+  float nrm2 = 0;
+  for (int k2 = 0; k2 < len; k2++) nrm2 += raw[k2] * raw[k2];
+  const float thr = sqrt_rn(nrm2) * kDescrMagThr;
+  nrm2 = 0;
+  for (int i = 0; i < len; i++) {
+    const float val = fminf(raw[i], thr);
+    raw[i] = val;
+    nrm2 += val * val;
+  }
+  nrm2 = kIntDescrFctr / fmaxf(sqrt_rn(nrm2), 1.1920928955078125e-07f);
+  float* dst = desc + (size_t)id * 128;
+  for (int k2 = 0; k2 < len; k2++) {
+    const int v = rnd(raw[k2] * nrm2);
+    dst[k2] = (float)(v < 0 ? 0 : v > 255 ? 255 : v);
+  }
+}
+
+__global__ void bgr2gray_kernel(const uint8_t* __restrict__ bgr, int64_t n, uint8_t* __restrict__ g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g[i] = (uint8_t)((bgr[3 * i] * 1868 + bgr[3 * i + 1] * 9617 + bgr[3 * i + 2] * 4899 + (1 << 13)) >> 14);
+}
+
+__global__ void unpack_kp_kernel(const Kp* __restrict__ sorted, const unsigned* __restrict__ nfinal,
+                                 float* __restrict__ x, float* __restrict__ y,
+                                 float* __restrict__ ang, int32_t* __restrict__ oct) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int)*nfinal) return;
+  const Kp k = sorted[i];
+  x[i] = k.x;
+  y[i] = k.y;
+  ang[i] = k.angle;
+  oct[i] = k.octave;
+}
+
+// ---- host side ------------------------------------------------------------------------
+// cv::getGaussianKernel(n, sigma, CV_32F) with the GaussianBlur size rule for float images
+int gauss_kernel(double sigma, float* k) {
+  const int n = (int)std::lrint(sigma * 4 * 2 + 1) | 1;
+  const int r = n / 2;
+  if (r + 1 > kMaxTaps) return -1;
+  std::vector<float> cf((size_t)n);
+  const double scale2X = -0.5 / (sigma * sigma);
+  double sum = 0;
+  for (int i = 0; i < n; i++) {
+    const double x = i - (n - 1) * 0.5;
+    cf[(size_t)i] = (float)std::exp(scale2X * x * x);
+    sum += cf[(size_t)i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < n; i++) cf[(size_t)i] = (float)(cf[(size_t)i] * sum);
+  for (int i = 0; i <= r; i++) k[i] = cf[(size_t)(r + i)];
+  return r;
+}
+
+}  // namespace
+
+struct SiftWork {
+  int L = 3;
+  double contrast = 0.04, edge = 10.0, sigma = 1.6;
+  int radius[kMaxLayers] = {};
+  DevBuf<float> kern;          // [kMaxLayers][kMaxTaps]
+  bool kern_ok = false;
+  Pyr P{};
+  DevBuf<uint8_t> gray;
+  DevBuf<float> gauss, dogs, tmp, up;
+  DevBuf<int4> cand;
+  DevBuf<Kp> kps, sorted;
+  DevBuf<uint8_t> dup;
+  DevBuf<int32_t> pos;
+  DevBuf<unsigned> cnt;        // [0] candidates, [1] raw keypoints, [2] final keypoints
+  DevBuf<float> desc;          // [n * 128]
+  int cap = 1 << 16;
+  int64_t n = 0;               // final keypoints of the last image
+  bool valid = false;
+};
+
+void sod_sift_free(sod_ctx* ctx) {
+  SiftWork* S = ctx->sift;
+  if (!S) return;
+  sod_release(S->kern);
+  sod_release(S->gray);
+  sod_release(S->gauss);
+  sod_release(S->dogs);
+  sod_release(S->tmp);
+  sod_release(S->up);
+  sod_release(S->cand);
+  sod_release(S->kps);
+  sod_release(S->sorted);
+  sod_release(S->dup);
+  sod_release(S->pos);
+  sod_release(S->cnt);
+  sod_release(S->desc);
+  delete S;
+  ctx->sift = nullptr;
+}
+
+namespace {
+
+SiftWork* work(sod_ctx* ctx) {
+  if (!ctx->sift) ctx->sift = new SiftWork();
+  return ctx->sift;
+}
+
+int set_kernels(sod_ctx* ctx, SiftWork& S) {
+  if (S.kern_ok) return SOD_OK;
+  // sig[0] = the base blur sqrt(max(sigma^2 - 4 * 0.5^2, 0.01)) in float (createInitialImage);
+  // sig[i] as buildGaussianPyramid (double)
+  double sig[kMaxLayers];
+  const float s = (float)S.sigma;
+  sig[0] = (double)std::sqrt(std::max(s * s - 0.5f * 0.5f * 4, 0.01f));
+  const double k = std::pow(2., 1. / S.L);
+  for (int i = 1; i < S.L + 3; i++) {
+    const double sig_prev = std::pow(k, (double)(i - 1)) * S.sigma;
+    const double sig_total = sig_prev * k;
+    sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
+  }
+  std::vector<float> h((size_t)kMaxLayers * kMaxTaps, 0.f);
+  for (int i = 0; i < S.L + 3; i++) {
+    S.radius[i] = gauss_kernel(sig[i], h.data() + (size_t)i * kMaxTaps);
+    if (S.radius[i] < 0) return sod_fail(ctx, SOD_EINVAL, "sigma too large for the blur kernel");
+  }
+  SOD_TRY(sod_reserve(ctx, S.kern, h.size()));
+  SOD_HIP(ctx, hipMemcpyAsync(S.kern.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  S.kern_ok = true;
+  return SOD_OK;
+}
+
+int blur(sod_ctx* ctx, SiftWork& S, const float* src, float* dst, int w, int h, int layer,
+         const float* prev, float* dog) {
+  const float* k = S.kern.p + (size_t)layer * kMaxTaps;
+  const int r = S.radius[layer];
+  dim3 g((unsigned)((w + 255) / 256), (unsigned)h);
+  hipLaunchKernelGGL(blur_rows_kernel, g, dim3(256), 0, ctx->stream, src, S.tmp.p, w, k, r);
+  hipLaunchKernelGGL(blur_cols_kernel, g, dim3(256), 0, ctx->stream, S.tmp.p, dst, w, h, k, r,
+                     prev, dog);
+  return SOD_OK;
+}
+
+// detect + describe one image already in S.gray; leaves the results on the device
+int run_image(sod_ctx* ctx, SiftWork& S, int w, int h) {
+  SOD_TRY(set_kernels(ctx, S));
+  const int L = S.L;
+  Pyr& P = S.P;
+  P.L = L;
+  const int bw = 2 * w, bh = 2 * h;
+  int nOct = (int)std::lrint(std::log((double)std::min(bw, bh)) / std::log(2.) - 2) - kFirstOctave;
+  nOct = std::max(1, std::min(nOct, kMaxOct));
+  P.n = nOct;
+  int64_t go = 0, dof = 0;
+  int ow = bw, oh = bh;
+  for (int o = 0; o < nOct; ++o) {
+    P.o[o] = Oct{ow, oh, go, dof};
+    go += (int64_t)(L + 3) * ow * oh;
+    dof += (int64_t)(L + 2) * ow * oh;
+    ow /= 2;
+    oh /= 2;
+    if (ow < 1 || oh < 1) {   // OpenCV would build empty layers here; none hold keypoints
+      P.n = nOct = o + 1;
+      break;
+    }
+  }
+  SOD_TRY(sod_reserve(ctx, S.gauss, (size_t)go));
+  SOD_TRY(sod_reserve(ctx, S.dogs, (size_t)dof));
+  SOD_TRY(sod_reserve(ctx, S.tmp, (size_t)bw * bh));
+  SOD_TRY(sod_reserve(ctx, S.up, (size_t)bw * bh));
+  SOD_TRY(sod_reserve(ctx, S.cnt, 4));
+
+  hipLaunchKernelGGL(upscale_kernel, dim3((unsigned)((bw + 255) / 256), (unsigned)bh), dim3(256), 0,
+                     ctx->stream, S.gray.p, w, h, S.up.p);
+  for (int o = 0; o < nOct; ++o) {
+    const Oct& q = P.o[o];
+    const size_t plane = (size_t)q.w * q.h;
+    float* g0 = S.gauss.p + q.g;
+    if (o == 0) {
+      SOD_TRY(blur(ctx, S, S.up.p, g0, q.w, q.h, 0, nullptr, nullptr));
+    } else {
+      const Oct& pq = P.o[o - 1];
+      hipLaunchKernelGGL(down2_kernel, dim3((unsigned)((q.w + 255) / 256), (unsigned)q.h), dim3(256),
+                         0, ctx->stream, S.gauss.p + pq.g + (size_t)pq.w * pq.h * L, pq.w, g0, q.w);
+    }
+    for (int i = 1; i < L + 3; ++i)
+      SOD_TRY(blur(ctx, S, g0 + plane * (i - 1), g0 + plane * i, q.w, q.h, i, g0 + plane * (i - 1),
+                   S.dogs.p + q.d + plane * (i - 1)));
+  }
+  const float thr = (float)(int)std::floor(0.5 * S.contrast / L * 255 * 1);
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    SOD_TRY(sod_reserve(ctx, S.cand, (size_t)S.cap));
+    SOD_TRY(sod_reserve(ctx, S.kps, (size_t)S.cap));
+    SOD_TRY(sod_reserve(ctx, S.sorted, (size_t)S.cap));
+    SOD_TRY(sod_reserve(ctx, S.dup, (size_t)S.cap));
+    SOD_TRY(sod_reserve(ctx, S.pos, (size_t)S.cap));
+    SOD_HIP(ctx, hipMemsetAsync(S.cnt.p, 0, 16, ctx->stream));
+    for (int o = 0; o < nOct; ++o) {
+      const Oct& q = P.o[o];
+      if (q.w <= 2 * kBorder || q.h <= 2 * kBorder) continue;
+      dim3 g((unsigned)((q.w - 2 * kBorder + 255) / 256), (unsigned)(q.h - 2 * kBorder), (unsigned)L);
+      hipLaunchKernelGGL(extrema_kernel, g, dim3(256), 0, ctx->stream, S.dogs.p, P, o, thr, S.cand.p,
+                         S.cnt.p, S.cap);
+    }
+    hipLaunchKernelGGL(refine_kernel, dim3((unsigned)((S.cap + 127) / 128)), dim3(128), 0, ctx->stream,
+                       S.gauss.p, S.dogs.p, P, S.cand.p, S.cnt.p, S.cap, (float)S.contrast,
+                       (float)S.edge, (float)S.sigma, S.kps.p, S.cnt.p + 1, S.cap);
+    unsigned c[2];
+    SOD_HIP(ctx, hipMemcpyAsync(c, S.cnt.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (c[0] > (unsigned)S.cap || c[1] > (unsigned)S.cap) {   // grow and redo (order-free)
+      S.cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)std::max(c[0], c[1]));
+      continue;
+    }
+    const int nk = (int)c[1];
+    if (nk > 0) {
+      const unsigned blocks = (unsigned)((nk + kRankTile - 1) / kRankTile);
+      hipLaunchKernelGGL(rank_kernel, dim3(blocks), dim3(kRankTile), 0, ctx->stream, S.kps.p,
+                         S.cnt.p + 1, S.cap, 0, S.dup.p, S.pos.p, S.cnt.p + 2);
+      hipLaunchKernelGGL(rank_kernel, dim3(blocks), dim3(kRankTile), 0, ctx->stream, S.kps.p,
+                         S.cnt.p + 1, S.cap, 1, S.dup.p, S.pos.p, S.cnt.p + 2);
+      hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0,
+                         ctx->stream, S.kps.p, S.cnt.p + 1, S.cap, S.pos.p, S.sorted.p);
+    }
+    unsigned nf = 0;
+    SOD_HIP(ctx, hipMemcpyAsync(&nf, S.cnt.p + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    S.n = nf;
+    if (nf > 0) {
+      SOD_TRY(sod_reserve(ctx, S.desc, (size_t)nf * 128));
+      hipLaunchKernelGGL(descriptor_kernel, dim3((nf + 63) / 64), dim3(64), 0, ctx->stream, S.gauss.p,
+                         P, S.sorted.p, S.cnt.p + 2, S.desc.p);
+    }
+    SOD_HIP(ctx, hipGetLastError());
+    S.valid = true;
+    return SOD_OK;
+  }
+  return sod_fail(ctx, SOD_ENOMEM, "SIFT: candidate list did not fit after growing");
+}
+
+}  // namespace
+
+// ---- C ABI ----------------------------------------------------------------------------
+extern "C" {
+
+int sod_sift_set_params(sod_ctx* ctx, int32_t n_octave_layers, double contrast_threshold,
+                        double edge_threshold, double sigma) {
+  if (!ctx) return SOD_EINVAL;
+  if (n_octave_layers < 1 || n_octave_layers + 3 > kMaxLayers || !(sigma > 0) ||
+      !(contrast_threshold >= 0) || !(edge_threshold > 0))
+    return sod_fail(ctx, SOD_EINVAL, "SIFT parameters out of range");
+  SiftWork& S = *work(ctx);
+  if (S.L == n_octave_layers && S.contrast == contrast_threshold && S.edge == edge_threshold &&
+      S.sigma == sigma)
+    return SOD_OK;
+  S.L = n_octave_layers;
+  S.contrast = contrast_threshold;
+  S.edge = edge_threshold;
+  S.sigma = sigma;
+  S.kern_ok = false;
+  S.valid = false;
+  return SOD_OK;
+}
+
+int sod_sift_detect(sod_ctx* ctx, const uint8_t* gray, int32_t width, int32_t height,
+                    int32_t* n_keypoints) {
+  if (!ctx) return SOD_EINVAL;
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  if (!gray || !n_keypoints || width < 1 || height < 1 || (int64_t)width * height > (1LL << 28))
+    return sod_fail(ctx, SOD_EINVAL, "bad image arguments");
+  SiftWork& S = *work(ctx);
+  S.valid = false;
+  SOD_TRY(sod_reserve(ctx, S.gray, (size_t)width * height));
+  SOD_HIP(ctx, hipMemcpyAsync(S.gray.p, gray, (size_t)width * height, hipMemcpyHostToDevice, ctx->stream));
+  SOD_TRY(run_image(ctx, S, width, height));
+  *n_keypoints = (int32_t)S.n;
+  return SOD_OK;
+}
+
+int sod_sift_detect_bgr(sod_ctx* ctx, const uint8_t* bgr, int32_t width, int32_t height,
+                        int32_t* n_keypoints) {
+  if (!ctx) return SOD_EINVAL;
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  if (!bgr || !n_keypoints || width < 1 || height < 1 || (int64_t)width * height > (1LL << 28))
+    return sod_fail(ctx, SOD_EINVAL, "bad image arguments");
+  SiftWork& S = *work(ctx);
+  S.valid = false;
+  const int64_t npix = (int64_t)width * height;
+  SOD_TRY(sod_reserve(ctx, S.gray, (size_t)npix));
+  SOD_TRY(sod_reserve(ctx, ctx->stage_u8, (size_t)npix * 3));
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->stage_u8.p, bgr, (size_t)npix * 3, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(bgr2gray_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, ctx->stream,
+                     ctx->stage_u8.p, npix, S.gray.p);
+  SOD_TRY(run_image(ctx, S, width, height));
+  *n_keypoints = (int32_t)S.n;
+  return SOD_OK;
+}
+
+int sod_sift_get(sod_ctx* ctx, int32_t cap, float* x, float* y, float* size, float* angle,
+                 float* response, int32_t* octave, float* descriptors) {
+  if (!ctx) return SOD_EINVAL;
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  SiftWork* S = ctx->sift;
+  if (!S || !S->valid) return sod_fail(ctx, SOD_ESTATE, "no SIFT result: call sod_sift_detect first");
+  const int64_t n = std::min<int64_t>(S->n, std::max(cap, 0));
+  if (n > 0) {
+    std::vector<Kp> h((size_t)n);
+    SOD_HIP(ctx, hipMemcpyAsync(h.data(), S->sorted.p, (size_t)n * sizeof(Kp), hipMemcpyDeviceToHost,
+                                ctx->stream));
+    if (descriptors)
+      SOD_HIP(ctx, hipMemcpyAsync(descriptors, S->desc.p, (size_t)n * 128 * 4, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int64_t i = 0; i < n; ++i) {
+      const Kp& k = h[(size_t)i];
+      if (x) x[i] = k.x;
+      if (y) y[i] = k.y;
+      if (size) size[i] = k.size;
+      if (angle) angle[i] = k.angle;
+      if (response) response[i] = k.response;
+      if (octave) octave[i] = k.octave;
+    }
+  }
+  return SOD_OK;
+}
+
+// the detected keypoints become the query set of the matcher / Hough stages, without a
+// host round trip (descriptors are packed from device memory)
+int sod_sift_to_queries(sod_ctx* ctx) {
+  if (!ctx) return SOD_EINVAL;
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  SiftWork* S = ctx->sift;
+  if (!S || !S->valid) return sod_fail(ctx, SOD_ESTATE, "no SIFT result: call sod_sift_detect first");
+  if (S->n < 1) return sod_fail(ctx, SOD_ESTATE, "the image has no SIFT keypoints");
+  const int32_t nq = (int32_t)S->n;
+  SOD_TRY(sod_reserve(ctx, ctx->flags, 4));
+  SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p, 0, 12, ctx->stream));
+  SOD_TRY(ctx->impl != 0 ? launch_pack_i8(ctx, S->desc.p, SOD_DTYPE_F32, nq, false)
+                         : launch_pack_queries(ctx, S->desc.p, SOD_DTYPE_F32, nq));
+  SOD_TRY(sod_reserve(ctx, ctx->qx, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->qy, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->qang, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->qoct, (size_t)nq));
+  hipLaunchKernelGGL(unpack_kp_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ctx->stream,
+                     S->sorted.p, S->cnt.p + 2, ctx->qx.p, ctx->qy.p, ctx->qang.p, ctx->qoct.p);
+  SOD_HIP(ctx, hipGetLastError());
+  ctx->nq = nq;
+  ctx->win0 = 0;
+  ctx->winn = -1;
+  ctx->n_qimg = 0;
+  ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+}  // extern "C"

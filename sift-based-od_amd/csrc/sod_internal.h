@@ -28,6 +28,8 @@ struct DevBuf {
   bool own = true;   // false: a view of another context's buffer (sod_db_share)
 };
 
+struct SiftWork;   // sift.hip: SIFT detect + describe workspace
+
 struct sod_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -125,6 +127,9 @@ struct sod_ctx {
   DevBuf<uint64_t> post_pos, post_ori;   // [n * ceil(n/64)] relation bitmasks
   DevBuf<int32_t> post_img;     // [n] query image of each bin (image batches)
 
+  // ---- SIFT on the device (sift.hip) ----
+  SiftWork* sift = nullptr;
+
   // ---- comm ----
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -217,3 +222,4 @@ int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
                       const float* qa, const int32_t* qo, const double* cx, const double* cy,
                       double* pose, int32_t* idx);
 int sod_build_sigma_lut(sod_ctx* ctx, int32_t bins_sigma);
+void sod_sift_free(sod_ctx* ctx);

@@ -152,3 +152,33 @@ def make_queries(n_queries, seed=1, db_seed=0, kp_per_image=1000, planted_frac=0
         row[s] = j * kp_per_image + m
         objid[s] = j
     return QuerySet(des, Keypoints(x, y, ang, octave), tuple(shape), row, objid)
+
+
+def textured_image(h, w, seed=0, n_blobs=None, n_rects=None):
+    """Seeded 8-bit gray test image with SIFT structure at several scales: a smooth
+    gradient, random rectangles (corners, edges), Gaussian blobs of radii 1.5-24 px and
+    mild noise.  For the SIFT row: no image files are needed."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    img = 60.0 + 40.0 * (xx / max(w, 1)) + 30.0 * (yy / max(h, 1))
+    n_rects = n_rects if n_rects is not None else max(4, (h * w) // 6000)
+    for _ in range(n_rects):
+        x0, y0 = rng.integers(0, w), rng.integers(0, h)
+        rw, rh = rng.integers(4, max(5, w // 6)), rng.integers(4, max(5, h // 6))
+        img[y0:y0 + rh, x0:x0 + rw] += rng.uniform(-50, 50)
+    n_blobs = n_blobs if n_blobs is not None else max(8, (h * w) // 300)
+    cx = rng.uniform(0, w, n_blobs)
+    cy = rng.uniform(0, h, n_blobs)
+    rad = np.exp(rng.uniform(np.log(1.5), np.log(24.0), n_blobs))
+    amp = rng.uniform(-90, 90, n_blobs)
+    for x0, y0, r, a in zip(cx, cy, rad, amp):
+        k = int(3 * r) + 1
+        xa, xb = max(0, int(x0) - k), min(w, int(x0) + k + 1)
+        ya, yb = max(0, int(y0) - k), min(h, int(y0) + k + 1)
+        if xa >= xb or ya >= yb:
+            continue
+        gx = np.exp(-((np.arange(xa, xb) - x0) ** 2) / (2 * r * r))
+        gy = np.exp(-((np.arange(ya, yb) - y0) ** 2) / (2 * r * r))
+        img[ya:yb, xa:xb] += a * np.outer(gy, gx)
+    img += rng.normal(0, 2.0, img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
