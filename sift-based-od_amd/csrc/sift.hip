@@ -235,6 +235,49 @@ __global__ void blur_cols_kernel(const float* __restrict__ src, float* __restric
   if (dog) dog[o] = s - prev[o];
 }
 
+// fused separable blur of one TW x TH output tile: the source tile with an r-pixel halo
+// (rows and columns reflected, BORDER_REFLECT_101) is staged in LDS, the row pass writes
+// an LDS intermediate, the column pass the output (and the DoG = output - source).  The
+// arithmetic is exactly blur_rows_kernel followed by blur_cols_kernel.
+constexpr int kTW = 64, kTH = 16, kMaxR = 16;
+__global__ __launch_bounds__(256) void blur_tile_kernel(const float* __restrict__ src,
+                                                        float* __restrict__ dst, int w, int h,
+                                                        const float* __restrict__ kern, int r,
+                                                        float* __restrict__ dog) {
+  __shared__ float in[(kTH + 2 * kMaxR) * (kTW + 2 * kMaxR)];
+  __shared__ float mid[(kTH + 2 * kMaxR) * kTW];
+  __shared__ float k[kMaxR + 1];
+  const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
+  const int iw = kTW + 2 * r, ih = kTH + 2 * r;
+  const int tid = threadIdx.x;
+  if (tid <= r) k[tid] = kern[tid];
+  for (int t = tid; t < iw * ih; t += 256) {
+    const int u = t % iw, v = t / iw;
+    const int gx = reflect101(x0 - r + u, w), gy = reflect101(y0 - r + v, h);
+    in[v * iw + u] = src[(size_t)gy * w + gx];
+  }
+  __syncthreads();
+  for (int t = tid; t < ih * kTW; t += 256) {   // row pass over all staged rows
+    const int u = t % kTW, v = t / kTW;
+    const float* row = in + v * iw + r + u;
+    float s = k[0] * row[0];
+    for (int i = 1; i <= r; ++i) s += k[i] * (row[-i] + row[i]);
+    mid[v * kTW + u] = s;
+  }
+  __syncthreads();
+  for (int t = tid; t < kTH * kTW; t += 256) {
+    const int u = t % kTW, v = t / kTW;
+    const int x = x0 + u, y = y0 + v;
+    if (x >= w || y >= h) continue;
+    const float* col = mid + (v + r) * kTW + u;
+    float s = k[0] * col[0];
+    for (int i = 1; i <= r; ++i) s += k[i] * (col[-i * kTW] + col[i * kTW]);
+    const size_t o = (size_t)y * w + x;
+    dst[o] = s;
+    if (dog) dog[o] = s - in[(v + r) * iw + r + u];
+  }
+}
+
 __global__ void down2_kernel(const float* __restrict__ src, int sw, float* __restrict__ dst, int dw) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
   if (x >= dw) return;
@@ -366,11 +409,18 @@ __device__ bool adjust_local_extrema(const float* dogs, const Pyr& P, int octv, 
   return true;
 }
 
-__global__ void refine_kernel(const float* __restrict__ gauss, const float* __restrict__ dogs,
-                              Pyr P, const int4* __restrict__ cand,
+// a candidate that passed adjustLocalExtrema: its keypoint (pyramid coordinates) and
+// the Gaussian layer / pixel its orientation histogram is taken at
+struct Surv {
+  Kp k;
+  int o, layer, r, c;
+};
+
+// one thread per candidate: adjustLocalExtrema
+__global__ void refine_kernel(const float* __restrict__ dogs, Pyr P, const int4* __restrict__ cand,
                               const unsigned* __restrict__ ncand, int cap, float contrastThreshold,
-                              float edgeThreshold, float sigma, Kp* __restrict__ kps,
-                              unsigned* __restrict__ nkp, int kcap) {
+                              float edgeThreshold, float sigma, Surv* __restrict__ surv,
+                              unsigned* __restrict__ nsurv) {
   const unsigned id = blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= min(*ncand, (unsigned)cap)) return;
   const int4 cd = cand[id];
@@ -379,33 +429,61 @@ __global__ void refine_kernel(const float* __restrict__ gauss, const float* __re
   Kp kpt;
   if (!adjust_local_extrema(dogs, P, o, layer, r, c, contrastThreshold, edgeThreshold, sigma, kpt))
     return;
-  // calcOrientationHist on Gaussian layer `layer` of octave o at (c, r)
+  const unsigned k = atomicAdd(nsurv, 1u);   // at most one survivor per candidate
+  surv[k] = Surv{kpt, o, layer, r, c};
+}
+
+// one wave per survivor: calcOrientationHist + one keypoint per histogram peak.  The
+// window's samples are computed 64 at a time (one per lane, in OpenCV's row-major order)
+// and added to the LDS histogram lane by lane, so every bin sums in OpenCV's order.
+__global__ __launch_bounds__(64) void orient_kernel(const float* __restrict__ gauss, Pyr P,
+                                                    const Surv* __restrict__ surv,
+                                                    const unsigned* __restrict__ nsurv, int cap,
+                                                    Kp* __restrict__ kps, unsigned* __restrict__ nkp,
+                                                    int kcap) {
+  __shared__ float tmp[kOriBins + 4];
+  if (blockIdx.x >= min(*nsurv, (unsigned)cap)) return;
+  const int lane = threadIdx.x;
+  const Surv sv = surv[blockIdx.x];
+  const Kp& kpt = sv.k;
+  const int o = sv.o, r = sv.r, c = sv.c;
   const Oct& q = P.o[o];
-  const float* img = gauss + q.g + (size_t)q.w * q.h * layer;
+  const float* img = gauss + q.g + (size_t)q.w * q.h * sv.layer;
   const float scl_octv = kpt.size * 0.5f / (1 << o);
   const int radius = rnd(kOriRadius * scl_octv);
   const float osig = kOriSigFctr * scl_octv;
   const float expf_scale = -1.f / (2.f * osig * osig);
-  float tmp[kOriBins + 4];
+  if (lane < kOriBins + 4) tmp[lane] = 0.f;
+  __syncthreads();
   float* temphist = tmp + 2;
-  for (int i = 0; i < kOriBins; i++) temphist[i] = 0.f;
-  for (int i = -radius; i <= radius; i++) {
-    const int y = r + i;
-    if (y <= 0 || y >= q.h - 1) continue;
-    for (int j = -radius; j <= radius; j++) {
-      const int x = c + j;
-      if (x <= 0 || x >= q.w - 1) continue;
+  const int side = 2 * radius + 1, total = side * side;
+  for (int p0 = 0; p0 < total; p0 += 64) {
+    const int p = p0 + lane;
+    const int i = p / side - radius, j = p % side - radius;
+    const int y = r + i, x = c + j;
+    const bool ok = p < total && y > 0 && y < q.h - 1 && x > 0 && x < q.w - 1;
+    int bin = 0;
+    float val = 0.f;
+    if (ok) {
       const float dx = at(img, q.w, y, x + 1) - at(img, q.w, y, x - 1);
       const float dy = at(img, q.w, y - 1, x) - at(img, q.w, y + 1, x);
       const float wgt = fexp((i * i + j * j) * expf_scale);
       const float ori = fast_atan2(dy, dx);
       const float mag = fmag(dx, dy);
-      int bin = rnd((kOriBins / 360.f) * ori);
+      bin = rnd((kOriBins / 360.f) * ori);
       if (bin >= kOriBins) bin -= kOriBins;
       if (bin < 0) bin += kOriBins;
-      temphist[bin] += wgt * mag;
+      val = wgt * mag;
+    }
+    uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+    while (m) {   // ordered: lowest lane first (LDS operations of a wave retire in order)
+      const int t = __builtin_ctzll(m);
+      m &= m - 1;
+      if (lane == t) atomicAdd(&temphist[bin], val);
     }
   }
+  __syncthreads();
+  if (lane != 0) return;
   temphist[-1] = temphist[kOriBins - 1];
   temphist[-2] = temphist[kOriBins - 2];
   temphist[kOriBins] = temphist[0];
@@ -454,65 +532,67 @@ __device__ inline bool kp_same(const Kp& a, const Kp& b) {
   return a.x == b.x && a.y == b.y && a.size == b.size && a.angle == b.angle;
 }
 
-constexpr int kRankTile = 256;
-// pass 0: dup[i] = an equal (x, y, size, angle) keypoint precedes i;
-// pass 1: pos[i] = number of kept keypoints before i (sorted position), -1 when dropped
-__global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ kps,
-                                                         const unsigned* __restrict__ nkp, int kcap,
-                                                         int pass, uint8_t* __restrict__ dup,
-                                                         int* __restrict__ pos,
-                                                         unsigned* __restrict__ nfinal) {
+constexpr int kRankTile = 64;
+// (i tile, j tile) blocks.  pass 0: dup[i] |= an equal (x, y, size, angle) keypoint
+// precedes i; pass 1: before[i] += kept keypoints preceding i (the sorted position)
+__global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ kps, int n, int pass,
+                                                         unsigned* __restrict__ dup,
+                                                         unsigned* __restrict__ before) {
   __shared__ Kp tile[kRankTile];
-  __shared__ uint8_t tdup[kRankTile];
-  const int n = (int)min(*nkp, (unsigned)kcap);
+  __shared__ unsigned tdup[kRankTile];
   const int i = blockIdx.x * kRankTile + threadIdx.x;
-  if (blockIdx.x * kRankTile >= n) return;
-  Kp me{};
-  if (i < n) me = kps[i];
-  int cnt = 0;
-  bool d = false;
-  for (int t0 = 0; t0 < n; t0 += kRankTile) {
-    __syncthreads();
-    if (t0 + (int)threadIdx.x < n) {
-      tile[threadIdx.x] = kps[t0 + threadIdx.x];
-      tdup[threadIdx.x] = pass ? dup[t0 + threadIdx.x] : 0;
-    }
-    __syncthreads();
-    const int m = min(kRankTile, n - t0);
-    if (i < n) {
-      for (int j = 0; j < m; ++j) {
-        const Kp& o = tile[j];
-        const bool lt = kp_less(o, t0 + j, me, i);
-        if (pass == 0)
-          d = d || (lt && kp_same(o, me));
-        else
-          cnt += (lt && !tdup[j]) ? 1 : 0;
-      }
-    }
+  const int j0 = blockIdx.y * kRankTile;
+  if (j0 + (int)threadIdx.x < n) {
+    tile[threadIdx.x] = kps[j0 + threadIdx.x];
+    tdup[threadIdx.x] = pass ? dup[j0 + threadIdx.x] : 0u;
   }
+  __syncthreads();
   if (i >= n) return;
+  const Kp me = kps[i];
+  const int m = min(kRankTile, n - j0);
+  unsigned cnt = 0;
+  bool d = false;
+  for (int j = 0; j < m; ++j) {
+    const bool lt = kp_less(tile[j], j0 + j, me, i);
+    if (pass == 0)
+      d = d || (lt && kp_same(tile[j], me));
+    else
+      cnt += (lt && !tdup[j]) ? 1u : 0u;
+  }
   if (pass == 0) {
-    dup[i] = d ? 1 : 0;
-    if (!d) atomicAdd(nfinal, 1u);
-  } else {
-    pos[i] = dup[i] ? -1 : cnt;
+    if (d) atomicOr(&dup[i], 1u);
+  } else if (cnt) {
+    atomicAdd(&before[i], cnt);
   }
 }
 
-__global__ void scatter_kernel(const Kp* __restrict__ kps, const unsigned* __restrict__ nkp,
-                               int kcap, const int* __restrict__ pos, Kp* __restrict__ sorted) {
+__global__ void scatter_kernel(const Kp* __restrict__ kps, int n, const unsigned* __restrict__ dup,
+                               const unsigned* __restrict__ before, Kp* __restrict__ sorted,
+                               unsigned* __restrict__ nfinal) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int)min(*nkp, (unsigned)kcap)) return;
-  const int p = pos[i];
-  if (p >= 0) sorted[p] = kps[i];
+  if (i >= n || dup[i]) return;
+  sorted[before[i]] = kps[i];
+  atomicAdd(nfinal, 1u);
 }
 
-// ---- descriptors: calcSIFTDescriptor, one thread per keypoint -------------------------
-__global__ void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
-                                  const Kp* __restrict__ sorted, const unsigned* __restrict__ nfinal,
-                                  float* __restrict__ desc) {
-  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+// ---- descriptors: calcSIFTDescriptor, one wave per keypoint ---------------------------
+// The window's samples are computed 64 at a time (one per lane, OpenCV's row-major
+// order), compacted, and their eight trilinear contributions added to the LDS histogram
+// sample by sample (lanes 0-7, one contribution each: the eight bins of a sample are
+// distinct), so every bin sums in OpenCV's order.
+constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);
+__global__ __launch_bounds__(64) void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
+                                                        const Kp* __restrict__ sorted,
+                                                        const unsigned* __restrict__ nfinal,
+                                                        float* __restrict__ desc) {
+  __shared__ float hist[kHistLen];
+  __shared__ int sidx[64];
+  __shared__ float sval[64][8];
+  __shared__ float raw[kD * kD * kN];
+  __shared__ float scal[2];
+  const int id = blockIdx.x;
   if (id >= (int)*nfinal) return;
+  const int lane = threadIdx.x;
   const Kp k = sorted[id];
   int octave = k.octave & 255;
   const int layer = (k.octave >> 8) & 255;
@@ -539,18 +619,26 @@ __global__ void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
   cos_t /= hist_width;
   sin_t /= hist_width;
   const int rows = q.h, cols = q.w;
-  float hist[(kD + 2) * (kD + 2) * (kN + 2)];
-  for (int i = 0; i < (kD + 2) * (kD + 2) * (kN + 2); i++) hist[i] = 0.f;
-  for (int i = -radius; i <= radius; i++)
-    for (int j = -radius; j <= radius; j++) {
-      const float c_rot = j * cos_t - i * sin_t;
-      const float r_rot = j * sin_t + i * cos_t;
-      float rbin = r_rot + kD / 2 - 0.5f;
-      float cbin = c_rot + kD / 2 - 0.5f;
-      const int r = py + i, c = px + j;
-      if (!(rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 &&
-            c < cols - 1))
-        continue;
+  for (int t = lane; t < kHistLen; t += 64) hist[t] = 0.f;
+  // the eight bins of a sample relative to its first
+  const int off = lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? kN + 2 : lane == 3 ? kN + 3
+                : lane == 4 ? (kD + 2) * (kN + 2) : lane == 5 ? (kD + 2) * (kN + 2) + 1
+                : lane == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
+  __syncthreads();
+  const int side = 2 * radius + 1;
+  const int64_t total = (int64_t)side * side;
+  for (int64_t p0 = 0; p0 < total; p0 += 64) {
+    const int64_t p = p0 + lane;
+    const int i = (int)(p / side) - radius, j = (int)(p % side) - radius;
+    const float c_rot = j * cos_t - i * sin_t;
+    const float r_rot = j * sin_t + i * cos_t;
+    float rbin = r_rot + kD / 2 - 0.5f;
+    float cbin = c_rot + kD / 2 - 0.5f;
+    const int r = py + i, c = px + j;
+    const bool ok = p < total && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 &&
+                    r < rows - 1 && c > 0 && c < cols - 1;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+    if (ok) {
       const float dx = at(img, cols, r, c + 1) - at(img, cols, r, c - 1);
       const float dy = at(img, cols, r - 1, c) - at(img, cols, r + 1, c);
       const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
@@ -573,38 +661,50 @@ __global__ void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
       const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
       const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
       const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-      const int idx = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
-      hist[idx] += v_rco000;
-      hist[idx + 1] += v_rco001;
-      hist[idx + (kN + 2)] += v_rco010;
-      hist[idx + (kN + 3)] += v_rco011;
-      hist[idx + (kD + 2) * (kN + 2)] += v_rco100;
-      hist[idx + (kD + 2) * (kN + 2) + 1] += v_rco101;
-      hist[idx + (kD + 3) * (kN + 2)] += v_rco110;
-      hist[idx + (kD + 3) * (kN + 2) + 1] += v_rco111;
+      const int slot = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      sidx[slot] = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
+      sval[slot][0] = v_rco000;
+      sval[slot][1] = v_rco001;
+      sval[slot][2] = v_rco010;
+      sval[slot][3] = v_rco011;
+      sval[slot][4] = v_rco100;
+      sval[slot][5] = v_rco101;
+      sval[slot][6] = v_rco110;
+      sval[slot][7] = v_rco111;
     }
-  float raw[kD * kD * kN];
-  for (int i = 0; i < kD; i++)
-    for (int j = 0; j < kD; j++) {
-      const int idx = ((i + 1) * (kD + 2) + (j + 1)) * (kN + 2);
-      hist[idx] += hist[idx + kN];
-      hist[idx + 1] += hist[idx + kN + 1];
-      for (int k2 = 0; k2 < kN; k2++) raw[(i * kD + j) * kN + k2] = hist[idx + k2];
-    }
-  constexpr int len = kD * kD * kN;
-  float nrm2 = 0;
-  for (int k2 = 0; k2 < len; k2++) nrm2 += raw[k2] * raw[k2];
-  const float thr = sqrt_rn(nrm2) * kDescrMagThr;
-  nrm2 = 0;
-  for (int i = 0; i < len; i++) {
-    const float val = fminf(raw[i], thr);
-    raw[i] = val;
-    nrm2 += val * val;
+    __syncthreads();
+    const int nv = __builtin_popcountll(m);
+    if (lane < 8)
+      for (int t = 0; t < nv; ++t) atomicAdd(&hist[sidx[t] + off], sval[t][lane]);
+    __syncthreads();
   }
-  nrm2 = kIntDescrFctr / fmaxf(sqrt_rn(nrm2), 1.1920928955078125e-07f);
+  // finalize: fold the circular orientation bins, then OpenCV's sequential norms
+  if (lane < kD * kD) {
+    const int i = lane / kD, j = lane % kD;
+    const int idx = ((i + 1) * (kD + 2) + (j + 1)) * (kN + 2);
+    hist[idx] += hist[idx + kN];
+    hist[idx + 1] += hist[idx + kN + 1];
+    for (int k2 = 0; k2 < kN; k2++) raw[(i * kD + j) * kN + k2] = hist[idx + k2];
+  }
+  __syncthreads();
+  constexpr int len = kD * kD * kN;
+  if (lane == 0) {
+    float nrm2 = 0;
+    for (int k2 = 0; k2 < len; k2++) nrm2 += raw[k2] * raw[k2];
+    const float thr = sqrt_rn(nrm2) * kDescrMagThr;
+    nrm2 = 0;
+    for (int i = 0; i < len; i++) {
+      const float val = fminf(raw[i], thr);
+      raw[i] = val;
+      nrm2 += val * val;
+    }
+    scal[0] = kIntDescrFctr / fmaxf(sqrt_rn(nrm2), 1.1920928955078125e-07f);
+  }
+  __syncthreads();
+  const float nrm = scal[0];
   float* dst = desc + (size_t)id * 128;
-  for (int k2 = 0; k2 < len; k2++) {
-    const int v = rnd(raw[k2] * nrm2);
+  for (int k2 = lane; k2 < len; k2 += 64) {
+    const int v = rnd(raw[k2] * nrm);
     dst[k2] = (float)(v < 0 ? 0 : v > 255 ? 255 : v);
   }
 }
@@ -659,10 +759,10 @@ struct SiftWork {
   DevBuf<uint8_t> gray;
   DevBuf<float> gauss, dogs, tmp, up;
   DevBuf<int4> cand;
+  DevBuf<Surv> surv;
   DevBuf<Kp> kps, sorted;
-  DevBuf<uint8_t> dup;
-  DevBuf<int32_t> pos;
-  DevBuf<unsigned> cnt;        // [0] candidates, [1] raw keypoints, [2] final keypoints
+  DevBuf<unsigned> dup, before;
+  DevBuf<unsigned> cnt;        // [0] candidates, [1] raw keypoints, [2] final, [3] survivors
   DevBuf<float> desc;          // [n * 128]
   int cap = 1 << 16;
   int64_t n = 0;               // final keypoints of the last image
@@ -681,8 +781,9 @@ void sod_sift_free(sod_ctx* ctx) {
   sod_release(S->cand);
   sod_release(S->kps);
   sod_release(S->sorted);
+  sod_release(S->surv);
   sod_release(S->dup);
-  sod_release(S->pos);
+  sod_release(S->before);
   sod_release(S->cnt);
   sod_release(S->desc);
   delete S;
@@ -725,6 +826,11 @@ int blur(sod_ctx* ctx, SiftWork& S, const float* src, float* dst, int w, int h, 
          const float* prev, float* dog) {
   const float* k = S.kern.p + (size_t)layer * kMaxTaps;
   const int r = S.radius[layer];
+  if (r <= kMaxR) {
+    dim3 gt((unsigned)((w + kTW - 1) / kTW), (unsigned)((h + kTH - 1) / kTH));
+    hipLaunchKernelGGL(blur_tile_kernel, gt, dim3(256), 0, ctx->stream, src, dst, w, h, k, r, dog);
+    return SOD_OK;
+  }
   dim3 g((unsigned)((w + 255) / 256), (unsigned)h);
   hipLaunchKernelGGL(blur_rows_kernel, g, dim3(256), 0, ctx->stream, src, S.tmp.p, w, k, r);
   hipLaunchKernelGGL(blur_cols_kernel, g, dim3(256), 0, ctx->stream, S.tmp.p, dst, w, h, k, r,
@@ -781,10 +887,8 @@ int run_image(sod_ctx* ctx, SiftWork& S, int w, int h) {
   const float thr = (float)(int)std::floor(0.5 * S.contrast / L * 255 * 1);
   for (int attempt = 0; attempt < 3; ++attempt) {
     SOD_TRY(sod_reserve(ctx, S.cand, (size_t)S.cap));
+    SOD_TRY(sod_reserve(ctx, S.surv, (size_t)S.cap));
     SOD_TRY(sod_reserve(ctx, S.kps, (size_t)S.cap));
-    SOD_TRY(sod_reserve(ctx, S.sorted, (size_t)S.cap));
-    SOD_TRY(sod_reserve(ctx, S.dup, (size_t)S.cap));
-    SOD_TRY(sod_reserve(ctx, S.pos, (size_t)S.cap));
     SOD_HIP(ctx, hipMemsetAsync(S.cnt.p, 0, 16, ctx->stream));
     for (int o = 0; o < nOct; ++o) {
       const Oct& q = P.o[o];
@@ -793,34 +897,50 @@ int run_image(sod_ctx* ctx, SiftWork& S, int w, int h) {
       hipLaunchKernelGGL(extrema_kernel, g, dim3(256), 0, ctx->stream, S.dogs.p, P, o, thr, S.cand.p,
                          S.cnt.p, S.cap);
     }
-    hipLaunchKernelGGL(refine_kernel, dim3((unsigned)((S.cap + 127) / 128)), dim3(128), 0, ctx->stream,
-                       S.gauss.p, S.dogs.p, P, S.cand.p, S.cnt.p, S.cap, (float)S.contrast,
-                       (float)S.edge, (float)S.sigma, S.kps.p, S.cnt.p + 1, S.cap);
-    unsigned c[2];
-    SOD_HIP(ctx, hipMemcpyAsync(c, S.cnt.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned c[4];
+    SOD_HIP(ctx, hipMemcpyAsync(c, S.cnt.p, 16, hipMemcpyDeviceToHost, ctx->stream));
     SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (c[0] > (unsigned)S.cap || c[1] > (unsigned)S.cap) {   // grow and redo (order-free)
-      S.cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)std::max(c[0], c[1]));
+    if (c[0] > (unsigned)S.cap) {   // grow and redo (the result does not depend on order)
+      S.cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)c[0]);
+      continue;
+    }
+    const unsigned ncand = c[0];
+    if (ncand > 0) {
+      hipLaunchKernelGGL(refine_kernel, dim3((ncand + 127) / 128), dim3(128), 0, ctx->stream, S.dogs.p,
+                         P, S.cand.p, S.cnt.p, S.cap, (float)S.contrast, (float)S.edge,
+                         (float)S.sigma, S.surv.p, S.cnt.p + 3);
+      // survivors <= candidates <= cap: one block per candidate slot, idle ones exit
+      hipLaunchKernelGGL(orient_kernel, dim3(ncand), dim3(64), 0, ctx->stream, S.gauss.p, P, S.surv.p,
+                         S.cnt.p + 3, S.cap, S.kps.p, S.cnt.p + 1, S.cap);
+    }
+    SOD_HIP(ctx, hipMemcpyAsync(c, S.cnt.p, 16, hipMemcpyDeviceToHost, ctx->stream));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (c[1] > (unsigned)S.cap) {
+      S.cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)c[1]);
       continue;
     }
     const int nk = (int)c[1];
-    if (nk > 0) {
-      const unsigned blocks = (unsigned)((nk + kRankTile - 1) / kRankTile);
-      hipLaunchKernelGGL(rank_kernel, dim3(blocks), dim3(kRankTile), 0, ctx->stream, S.kps.p,
-                         S.cnt.p + 1, S.cap, 0, S.dup.p, S.pos.p, S.cnt.p + 2);
-      hipLaunchKernelGGL(rank_kernel, dim3(blocks), dim3(kRankTile), 0, ctx->stream, S.kps.p,
-                         S.cnt.p + 1, S.cap, 1, S.dup.p, S.pos.p, S.cnt.p + 2);
-      hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0,
-                         ctx->stream, S.kps.p, S.cnt.p + 1, S.cap, S.pos.p, S.sorted.p);
-    }
     unsigned nf = 0;
-    SOD_HIP(ctx, hipMemcpyAsync(&nf, S.cnt.p + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (nk > 0) {
+      SOD_TRY(sod_reserve(ctx, S.sorted, (size_t)nk));
+      SOD_TRY(sod_reserve(ctx, S.dup, (size_t)nk));
+      SOD_TRY(sod_reserve(ctx, S.before, (size_t)nk));
+      SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)nk * 4, ctx->stream));
+      SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)nk * 4, ctx->stream));
+      const unsigned tiles = (unsigned)((nk + kRankTile - 1) / kRankTile);
+      for (int pass = 0; pass < 2; ++pass)
+        hipLaunchKernelGGL(rank_kernel, dim3(tiles, tiles), dim3(kRankTile), 0, ctx->stream, S.kps.p,
+                           nk, pass, S.dup.p, S.before.p);
+      hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0,
+                         ctx->stream, S.kps.p, nk, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2);
+      SOD_HIP(ctx, hipMemcpyAsync(&nf, S.cnt.p + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
+      SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     S.n = nf;
     if (nf > 0) {
       SOD_TRY(sod_reserve(ctx, S.desc, (size_t)nf * 128));
-      hipLaunchKernelGGL(descriptor_kernel, dim3((nf + 63) / 64), dim3(64), 0, ctx->stream, S.gauss.p,
-                         P, S.sorted.p, S.cnt.p + 2, S.desc.p);
+      hipLaunchKernelGGL(descriptor_kernel, dim3(nf), dim3(64), 0, ctx->stream, S.gauss.p, P,
+                         S.sorted.p, S.cnt.p + 2, S.desc.p);
     }
     SOD_HIP(ctx, hipGetLastError());
     S.valid = true;

@@ -170,6 +170,32 @@ class SiftDatabase:
         return cls(np.concatenate(dess, axis=0), kp, np.concatenate(imgs),
                    np.array(cents, np.float64), np.array(sizes, np.int32))
 
+    @classmethod
+    def from_images(cls, images, sift=None):
+        """``GenerateDatabaseInfo.py:19-37`` on the device: SIFT of every training image
+        (8-bit gray or BGR, already resized as the script's ``cv2.resize`` to width 1500
+        does), its keypoints, ``get_centroid`` and ``img_size = (w, h)``."""
+        from .sift import SIFT_create
+        sift = sift or SIFT_create()
+        xs, ys, angs, octs, imgs, dess, cents, sizes = [], [], [], [], [], [], [], []
+        for i, img in enumerate(images):
+            r = sift.detect_arrays(np.asarray(img))
+            n = len(r["x"])
+            if n == 0:
+                raise ValueError("training image %d has no SIFT keypoints" % i)
+            xs.append(r["x"])
+            ys.append(r["y"])
+            angs.append(r["angle"])
+            octs.append(r["octave"])
+            imgs.append(np.full(n, i, np.int32))
+            dess.append(r["descriptors"])
+            cents.append(centroid_of(r["x"], r["y"]))
+            sizes.append((int(np.shape(img)[1]), int(np.shape(img)[0])))
+        kp = Keypoints(np.concatenate(xs), np.concatenate(ys), np.concatenate(angs),
+                       np.concatenate(octs))
+        return cls(np.concatenate(dess, axis=0), kp, np.concatenate(imgs),
+                   np.array(cents, np.float64), np.array(sizes, np.int32))
+
     def shard(self, rank, world):
         """Rows ``[rank*N/world, (rank+1)*N/world)`` -- the DB-row split of
         SURVEY.md §8(e).  Returns (row_offset, descriptors) for the shard;

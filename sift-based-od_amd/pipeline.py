@@ -5,6 +5,7 @@ Same stage names, order and thresholds as the reference::
     m = Main()
     m.set_database(db)                                   # main.py:48-66 (pickle -> SoA)
     m.get_query_features(des_query, kp_query, shape)     # main.py:36-45 (SIFT output given)
+    m.get_query_image(bgr_image)                         # main.py:36-45 (SIFT on the device)
     m.run_matcher()                                      # main.py:68-87
     m.apply_hough_transform(15)                          # main.py:89-119
     m.get_valid_bins(5)                                  # main.py:121-132
@@ -13,9 +14,9 @@ Same stage names, order and thresholds as the reference::
 Every stage runs on the device and leaves its result there; the reference's Python
 objects (``matching_keypoints`` tuples, the ``hough_transform`` dict of PoseBins,
 ``valid_bins``, ``keypoint_pairs``) are materialised lazily, only when read.  ``run()``
-enqueues the whole path on one stream (the bench path).  SIFT detection
-(``main.py:43``) and the post-processing / plotting stages are outside this path
-(SURVEY.md §8(f)).
+enqueues the whole path on one stream (the bench path).  ``get_query_image`` runs SIFT
+detection (``main.py:43``) on the device as well; plotting stays
+outside.
 """
 from __future__ import annotations
 
@@ -82,6 +83,26 @@ class Main:
         self.image_query_size = (int(image_shape[1]), int(image_shape[0]))   # (w, h)
         self.kp_query = _LazyKeypoints(self, "query")
         self.ctx.upload_queries(self.des_query, kp_query)
+        self._reset_after_match()
+
+    def get_query_image(self, image, database=None):
+        """``main.py:36-45`` from the image itself: ``image`` as ``cv2.imread`` returns it
+        (8-bit BGR [h, w, 3]) or already gray [h, w].  BGR2GRAY and
+        ``SIFT_create().detectAndCompute`` run on the device and the
+        features become the query set without leaving it."""
+        if database is not None:
+            self.set_database(database)
+        img = np.asarray(image)
+        r = self.ctx.sift_detect(img)
+        if len(r["x"]) == 0:
+            raise ValueError("the query image has no SIFT keypoints")
+        self.ctx.sift_to_queries()
+        self._qkp = Keypoints(r["x"], r["y"], r["angle"], r["octave"])
+        self.des_query = r["descriptors"]
+        self.sift_query = r
+        self.rgb_query = _Shape(img.shape if img.ndim == 3 else img.shape + (3,))
+        self.image_query_size = (int(img.shape[1]), int(img.shape[0]))   # (w, h)
+        self.kp_query = _LazyKeypoints(self, "query")
         self._reset_after_match()
 
     def _reset_after_match(self):

@@ -209,3 +209,34 @@ def test_sift_to_queries_equals_host_upload(ctx):
     assert np.array_equal(d2_a, d2_b) and np.array_equal(good_a, good_b)
     e1, f1, f2 = orc.knn2_match(r["descriptors"], db.des)
     assert np.array_equal(idx_a, e1) and np.array_equal(d1_a, f1) and np.array_equal(d2_a, f2)
+
+
+@pytest.mark.gpu
+def test_image_to_pose_end_to_end(ctx):
+    """GenerateDatabaseInfo (SIFT of the training images) -> main.py on a query IMAGE:
+    SIFT, matcher, Hough, affine and post-processing all on the device.  The result
+    equals the same driver fed the oracle's SIFT features, and the object is found where
+    it was pasted."""
+    from sift_based_od_amd import Main, SiftDatabase
+    objs = [synthetic.textured_image(240, 300, seed=30 + i) for i in range(3)]
+    db = SiftDatabase.from_images(objs, dsift.SIFT_create(ctx=ctx))
+    canvas = synthetic.textured_image(480, 640, seed=40, n_blobs=60)
+    canvas[100:340, 200:500] = objs[1]                       # object 1 at (200, 100)
+    m = Main(ctx)
+    m.set_database(db)
+    m.get_query_image(canvas)
+    r_dev = m.run(bins=15)
+    ref = osift.detect_and_compute(canvas)
+    kp = synthetic.Keypoints(ref["x"], ref["y"], ref["angle"], ref["octave"])
+    m2 = Main(ctx)
+    m2.set_database(db)
+    m2.get_query_features(ref["descriptors"], kp, canvas.shape + (3,))
+    r_ref = m2.run(bins=15)
+    for k in ("idx1", "d1", "d2", "good"):
+        assert np.array_equal(r_dev[k], r_ref[k]), k
+    assert np.array_equal(r_dev["valid"]["keys"], r_ref["valid"]["keys"])
+    fp = r_dev["post"]["final_pose"]
+    assert len(fp) >= 1
+    # the pose centroid of the best cluster lies inside the pasted object
+    xs, ys = fp[:, 0], fp[:, 1]
+    assert np.any((xs > 200) & (xs < 500) & (ys > 100) & (ys < 340))
