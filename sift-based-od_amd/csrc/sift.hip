@@ -29,6 +29,9 @@
 
 namespace {
 
+#ifndef SOD_SIFT_EXP
+#define SOD_SIFT_EXP 0   // timing experiments only (wrong results): 1 no descriptor adds,
+#endif                   // 2 no orientation adds, 4 no small-octave extrema
 constexpr int kBorder = 5;              // SIFT_IMG_BORDER
 constexpr int kMaxInterp = 5;           // SIFT_MAX_INTERP_STEPS
 constexpr int kOriBins = 36;            // SIFT_ORI_HIST_BINS
@@ -235,46 +238,287 @@ __global__ void blur_cols_kernel(const float* __restrict__ src, float* __restric
   if (dog) dog[o] = s - prev[o];
 }
 
-// fused separable blur of one TW x TH output tile: the source tile with an r-pixel halo
-// (rows and columns reflected, BORDER_REFLECT_101) is staged in LDS, the row pass writes
-// an LDS intermediate, the column pass the output (and the DoG = output - source).  The
-// arithmetic is exactly blur_rows_kernel followed by blur_cols_kernel.
-constexpr int kTW = 64, kTH = 16, kMaxR = 16;
+// fused separable blur of one kTW x kTH output tile, radius R a template parameter: the
+// source tile with an R-pixel halo (rows and columns reflected, BORDER_REFLECT_101) is
+// staged in LDS; the row pass (each thread a run of kSeg outputs from a register window)
+// writes an LDS intermediate, the column pass (runs of kSeg down a column) the output and
+// the DoG = output - source.  Per output the arithmetic is exactly blur_rows_kernel's
+// then blur_cols_kernel's: k0*x + sum_{i=1..R} k_i*(x[-i] + x[+i]) in increasing i.
+constexpr int kTW = 64, kTH = 32, kSeg = 8, kMaxR = 16;
+template <int R>
 __global__ __launch_bounds__(256) void blur_tile_kernel(const float* __restrict__ src,
                                                         float* __restrict__ dst, int w, int h,
-                                                        const float* __restrict__ kern, int r,
+                                                        const float* __restrict__ kern,
                                                         float* __restrict__ dog) {
-  __shared__ float in[(kTH + 2 * kMaxR) * (kTW + 2 * kMaxR)];
-  __shared__ float mid[(kTH + 2 * kMaxR) * kTW];
-  __shared__ float k[kMaxR + 1];
+  constexpr int IW = kTW + 2 * R, IH = kTH + 2 * R;
+  __shared__ float in[IH * IW];
+  __shared__ float mid[IH * kTW];
   const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
-  const int iw = kTW + 2 * r, ih = kTH + 2 * r;
   const int tid = threadIdx.x;
-  if (tid <= r) k[tid] = kern[tid];
-  for (int t = tid; t < iw * ih; t += 256) {
-    const int u = t % iw, v = t / iw;
-    const int gx = reflect101(x0 - r + u, w), gy = reflect101(y0 - r + v, h);
-    in[v * iw + u] = src[(size_t)gy * w + gx];
+  float k[R + 1];
+#pragma unroll
+  for (int i = 0; i <= R; ++i) k[i] = kern[i];
+  const bool interior = x0 >= R && x0 + kTW + R <= w && y0 >= R && y0 + kTH + R <= h;
+  for (int t = tid; t < IW * IH; t += 256) {
+    const int u = t % IW, v = t / IW;
+    int gx = x0 - R + u, gy = y0 - R + v;
+    if (!interior) {
+      gx = reflect101(gx, w);
+      gy = reflect101(gy, h);
+    }
+    in[t] = src[(size_t)gy * w + gx];
   }
   __syncthreads();
-  for (int t = tid; t < ih * kTW; t += 256) {   // row pass over all staged rows
-    const int u = t % kTW, v = t / kTW;
-    const float* row = in + v * iw + r + u;
-    float s = k[0] * row[0];
-    for (int i = 1; i <= r; ++i) s += k[i] * (row[-i] + row[i]);
-    mid[v * kTW + u] = s;
+  // row pass: IH rows x (kTW / kSeg) runs
+  for (int t = tid; t < IH * (kTW / kSeg); t += 256) {
+    const int run = t % (kTW / kSeg), v = t / (kTW / kSeg);
+    const float* row = in + v * IW + run * kSeg;   // window starts R left of the first output
+    float win[kSeg + 2 * R];
+#pragma unroll
+    for (int j = 0; j < kSeg + 2 * R; ++j) win[j] = row[j];
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) {
+      float s = k[0] * win[o + R];
+#pragma unroll
+      for (int i = 1; i <= R; ++i) s += k[i] * (win[o + R - i] + win[o + R + i]);
+      mid[v * kTW + run * kSeg + o] = s;
+    }
   }
   __syncthreads();
-  for (int t = tid; t < kTH * kTW; t += 256) {
-    const int u = t % kTW, v = t / kTW;
-    const int x = x0 + u, y = y0 + v;
-    if (x >= w || y >= h) continue;
-    const float* col = mid + (v + r) * kTW + u;
-    float s = k[0] * col[0];
-    for (int i = 1; i <= r; ++i) s += k[i] * (col[-i * kTW] + col[i * kTW]);
-    const size_t o = (size_t)y * w + x;
-    dst[o] = s;
-    if (dog) dog[o] = s - in[(v + r) * iw + r + u];
+  // column pass: kTW columns x (kTH / kSeg) runs
+  for (int t = tid; t < kTW * (kTH / kSeg); t += 256) {
+    const int u = t % kTW, run = t / kTW;
+    const float* col = mid + run * kSeg * kTW + u;
+    float win[kSeg + 2 * R];
+#pragma unroll
+    for (int j = 0; j < kSeg + 2 * R; ++j) win[j] = col[j * kTW];
+    const int x = x0 + u;
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) {
+      const int y = y0 + run * kSeg + o;
+      float s = k[0] * win[o + R];
+#pragma unroll
+      for (int i = 1; i <= R; ++i) s += k[i] * (win[o + R - i] + win[o + R + i]);
+      if (x < w && y < h) {
+        const size_t oo = (size_t)y * w + x;
+        dst[oo] = s;
+        if (dog) dog[oo] = s - in[(run * kSeg + o + R) * IW + R + u];
+      }
+    }
+  }
+}
+
+using BlurFn = void (*)(const float*, float*, int, int, const float*, float*);
+constexpr BlurFn kBlurFns[kMaxR + 1] = {
+    nullptr, blur_tile_kernel<1>, blur_tile_kernel<2>, blur_tile_kernel<3>, blur_tile_kernel<4>,
+    blur_tile_kernel<5>, blur_tile_kernel<6>, blur_tile_kernel<7>, blur_tile_kernel<8>,
+    blur_tile_kernel<9>, blur_tile_kernel<10>, blur_tile_kernel<11>, blur_tile_kernel<12>,
+    blur_tile_kernel<13>, blur_tile_kernel<14>, blur_tile_kernel<15>, blur_tile_kernel<16>};
+
+// OpenCV's test: val >= all 26 neighbours (val > 0) or <= all (val < 0); the 26 loads
+// are issued together (max / min of the neighbours, no short-circuit chain of loads)
+__device__ inline bool is_extremum(const float* cur, size_t plane, size_t c, int step, float val) {
+  float mx = -3.4e38f, mn = 3.4e38f;
+#pragma unroll
+  for (int dl = -1; dl <= 1; ++dl)
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!dl && !dy && !dx) continue;
+        const float v = cur[(ptrdiff_t)plane * dl + (ptrdiff_t)c + (ptrdiff_t)dy * step + dx];
+        mx = fmaxf(mx, v);
+        mn = fminf(mn, v);
+      }
+  return val > 0 ? val >= mx : val <= mn;
+}
+
+// ---- the small octaves in ONE work-group: from octave o0 (<= kChainPixels pixels) to
+// the last, the /2 base, the incremental blurs (row pass, column pass + DoG; the same
+// arithmetic as above) on LDS copies of the current layer, each layer also written to the
+// pyramid, then the extrema of those octaves.  Replaces ~6 launches per small octave.
+constexpr int kChainPixels = 4096;
+constexpr int kChainDog = 5;     // DoG layers held in LDS: the chain runs for nOctaveLayers <= 3
+constexpr int kTabMax = 64;   // dimensions up to this use an LDS reflection table
+// BORDER_REFLECT_101 index for the chain: a table for small dimensions (several
+// reflections when the kernel is wider than the image), one reflection otherwise
+__device__ inline int refl(int p, int len, const int* tab) {
+  if (len <= kTabMax) return tab[p + kMaxR];
+  return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
+}
+// one blur pass (rows: along x; else along y) of a w x h LDS image, taps unrolled (R a
+// template parameter); the arithmetic of blur_rows_kernel / blur_cols_kernel
+template <int R>
+__device__ inline float blur_px_r(const float* img, int w, int h, int x, int y, bool row,
+                                  const float* k, const int* tabx, const int* taby) {
+  float s;
+  if (row) {
+    const float* p = img + y * w;
+    s = k[0] * p[x];
+    if (x >= R && x + R < w) {
+#pragma unroll
+      for (int j = 1; j <= R; ++j) s += k[j] * (p[x - j] + p[x + j]);
+    } else {
+#pragma unroll
+      for (int j = 1; j <= R; ++j) s += k[j] * (p[refl(x - j, w, tabx)] + p[refl(x + j, w, tabx)]);
+    }
+  } else {
+    const float* p = img + x;
+    s = k[0] * p[y * w];
+    if (y >= R && y + R < h) {
+#pragma unroll
+      for (int j = 1; j <= R; ++j) s += k[j] * (p[(y - j) * w] + p[(y + j) * w]);
+    } else {
+#pragma unroll
+      for (int j = 1; j <= R; ++j)
+        s += k[j] * (p[refl(y - j, h, taby) * w] + p[refl(y + j, h, taby) * w]);
+    }
+  }
+  return s;
+}
+template <int R>
+__device__ void chain_rows(const float* cur, float* T, int w, int h, const float* k, const int* tabx,
+                           const int* taby, int tid) {
+  for (int t = tid; t < w * h; t += 1024) {
+    const int y = t / w, x = t - y * w;
+    T[t] = blur_px_r<R>(cur, w, h, x, y, true, k, tabx, taby);
+  }
+}
+template <int R>
+__device__ void chain_cols(const float* T, const float* cur, float* nxt, float* dst, float* dg,
+                           float* dgl, float* keep, int w, int h, const float* k, const int* tabx,
+                           const int* taby, int tid) {
+  for (int t = tid; t < w * h; t += 1024) {
+    const int y = t / w, x = t - y * w;
+    const float s = blur_px_r<R>(T, w, h, x, y, false, k, tabx, taby);
+    const float d = s - cur[t];
+    nxt[t] = s;
+    dst[t] = s;
+    dg[t] = d;
+    dgl[t] = d;
+    if (keep) keep[t] = s;
+  }
+}
+#define SOD_CHAIN_CASES(F, ...)                                                         \
+  switch (r) {                                                                          \
+    case 1: F<1>(__VA_ARGS__); break;   case 2: F<2>(__VA_ARGS__); break;               \
+    case 3: F<3>(__VA_ARGS__); break;   case 4: F<4>(__VA_ARGS__); break;               \
+    case 5: F<5>(__VA_ARGS__); break;   case 6: F<6>(__VA_ARGS__); break;               \
+    case 7: F<7>(__VA_ARGS__); break;   case 8: F<8>(__VA_ARGS__); break;               \
+    case 9: F<9>(__VA_ARGS__); break;   case 10: F<10>(__VA_ARGS__); break;             \
+    case 11: F<11>(__VA_ARGS__); break; case 12: F<12>(__VA_ARGS__); break;             \
+    case 13: F<13>(__VA_ARGS__); break; case 14: F<14>(__VA_ARGS__); break;             \
+    case 15: F<15>(__VA_ARGS__); break; default: F<16>(__VA_ARGS__); break;             \
+  }
+
+#ifdef SOD_SIFT_STAMP
+// diagnostic build only: s_memrealtime (100 MHz) at each phase of the small-octave chain
+__device__ unsigned long long g_sift_stamps[256];
+#define SIFT_STAMP(i)                                                              \
+  {                                                                                \
+    const int i_ = (i);                                                            \
+    if (threadIdx.x == 0 && i_ < 256) g_sift_stamps[i_] = __builtin_amdgcn_s_memrealtime(); \
+  }
+#else
+#define SIFT_STAMP(i)
+#endif
+
+// barrier for LDS traffic only: the pyramid's global stores drain in the background (no
+// pass of the chain reads them back)
+__device__ inline void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ---- the small octaves (<= kChainPixels pixels each) in ONE work-group, entirely in LDS:
+// the /2 base (from the pyramid for the first, from the LDS copy of layer L after that),
+// the incremental blurs (row pass, column pass + DoG), every layer also written to the
+// pyramid, and the extrema of each octave from its LDS DoG layers.  Replaces ~7 launches
+// per small octave.
+__global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__ gauss,
+                                                             float* __restrict__ dogs, Pyr P, int o0,
+                                                             const float* __restrict__ kern,
+                                                             const int* __restrict__ radius,
+                                                             float thr, int4* __restrict__ cand,
+                                                             unsigned* __restrict__ ncand, int cap) {
+  __shared__ float A[kChainPixels], T[kChainPixels], C[kChainPixels], Bl[kChainPixels];
+  __shared__ float Dg[kChainDog][kChainPixels];
+  __shared__ float kk[kMaxLayers][kMaxTaps];
+  __shared__ int tabx[kTabMax + 2 * kMaxR], taby[kTabMax + 2 * kMaxR];
+  const int L = P.L, tid = threadIdx.x;
+  int stamp = 0;
+  (void)stamp;
+  SIFT_STAMP(stamp++)
+  for (int t = tid; t < kMaxLayers * kMaxTaps; t += 1024) kk[t / kMaxTaps][t % kMaxTaps] = kern[t];
+  for (int o = o0; o < P.n; ++o) {
+    const Oct& q = P.o[o];
+    const int w = q.w, h = q.h, np = w * h;
+    float* g0 = gauss + q.g;
+    const Oct& pq = P.o[o - 1];
+    if (o == o0) {
+      const float* base = gauss + pq.g + (size_t)pq.w * pq.h * L;   // written by earlier launches
+      for (int t = tid; t < np; t += 1024) {
+        const int y = t / w, x = t - y * w;
+        A[t] = base[(size_t)(2 * y) * pq.w + 2 * x];
+      }
+    } else {
+      for (int t = tid; t < np; t += 1024) {
+        const int y = t / w, x = t - y * w;
+        A[t] = Bl[(2 * y) * pq.w + 2 * x];
+      }
+    }
+    for (int t = tid; t < kTabMax + 2 * kMaxR; t += 1024) {
+      if (w <= kTabMax) tabx[t] = reflect101(t - kMaxR, w);
+      if (h <= kTabMax) taby[t] = reflect101(t - kMaxR, h);
+    }
+    lds_barrier();
+    for (int t = tid; t < np; t += 1024) g0[t] = A[t];
+    float* cur = A;
+    float* nxt = C;
+    for (int i = 1; i < L + 3; ++i) {
+      const int r = radius[i];
+      SOD_CHAIN_CASES(chain_rows, cur, T, w, h, kk[i], tabx, taby, tid)
+      lds_barrier();
+      SIFT_STAMP(stamp++)
+      float* dst = g0 + (size_t)np * i;
+      float* dg = dogs + q.d + (size_t)np * (i - 1);
+      SOD_CHAIN_CASES(chain_cols, T, cur, nxt, dst, dg, Dg[i - 1], i == L ? Bl : nullptr, w, h,
+                      kk[i], tabx, taby, tid)
+      lds_barrier();
+      SIFT_STAMP(stamp++)
+      float* t2 = cur;
+      cur = nxt;
+      nxt = t2;
+    }
+    if (SOD_SIFT_EXP & 4) continue;
+    // extrema of this octave (extrema_kernel's test) on the LDS DoG layers
+    const int iw = w - 2 * kBorder, ih = h - 2 * kBorder;
+    if (iw > 0 && ih > 0) {
+      for (int t = tid; t < iw * ih * L; t += 1024) {
+        const int layer = t / (iw * ih) + 1, rem = t - (layer - 1) * (iw * ih);
+        const int y = rem / iw + kBorder, x = rem - (y - kBorder) * iw + kBorder;
+        const float* cur2 = Dg[layer];
+        const int c = y * w + x;
+        const float val = cur2[c];
+        if (!(fabsf(val) > thr)) continue;
+        float mx = -3.4e38f, mn = 3.4e38f;
+#pragma unroll
+        for (int dl = -1; dl <= 1; ++dl)
+#pragma unroll
+          for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+              if (!dl && !dy && !dx) continue;
+              const float v = Dg[layer + dl][c + dy * w + dx];
+              mx = fmaxf(mx, v);
+              mn = fminf(mn, v);
+            }
+        if (!(val > 0 ? val >= mx : val <= mn)) continue;
+        const unsigned i = atomicAdd(ncand, 1u);
+        if (i < (unsigned)cap) cand[i] = make_int4(o, layer, y, x);
+      }
+    }
+    lds_barrier();
+    SIFT_STAMP(stamp++)
   }
 }
 
@@ -284,7 +528,7 @@ __global__ void down2_kernel(const float* __restrict__ src, int sw, float* __res
   dst[(size_t)y * dw + x] = src[(size_t)(2 * y) * sw + 2 * x];
 }
 
-// ---- extrema --------------------------------------------------------------------------
+// ---- extrema ------------------------------------------------------------------------
 __global__ void extrema_kernel(const float* __restrict__ dogs, Pyr P, int o, float thr,
                                int4* __restrict__ cand, unsigned* __restrict__ ncand, int cap) {
   const Oct& q = P.o[o];
@@ -296,20 +540,7 @@ __global__ void extrema_kernel(const float* __restrict__ dogs, Pyr P, int o, flo
   const size_t c = (size_t)y * q.w + x;
   const float val = cur[c];
   if (!(fabsf(val) > thr)) return;
-  const int step = q.w;
-  bool ext = true;
-#pragma unroll
-  for (int dl = -1; dl <= 1; ++dl) {
-    const float* m = cur + (ptrdiff_t)plane * dl;
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        if (!dl && !dy && !dx) continue;
-        const float v = m[c + (ptrdiff_t)dy * step + dx];
-        ext = ext && (val > 0 ? val >= v : val <= v);
-      }
-  }
+  const bool ext = is_extremum(cur, plane, c, q.w, val);
   if (!ext) return;
   const unsigned i = atomicAdd(ncand, 1u);
   if (i < (unsigned)cap) cand[i] = make_int4(o, layer, y, x);
@@ -433,87 +664,134 @@ __global__ void refine_kernel(const float* __restrict__ dogs, Pyr P, const int4*
   surv[k] = Surv{kpt, o, layer, r, c};
 }
 
-// one wave per survivor: calcOrientationHist + one keypoint per histogram peak.  The
-// window's samples are computed 64 at a time (one per lane, in OpenCV's row-major order)
-// and added to the LDS histogram lane by lane, so every bin sums in OpenCV's order.
-__global__ __launch_bounds__(64) void orient_kernel(const float* __restrict__ gauss, Pyr P,
-                                                    const Surv* __restrict__ surv,
-                                                    const unsigned* __restrict__ nsurv, int cap,
-                                                    Kp* __restrict__ kps, unsigned* __restrict__ nkp,
-                                                    int kcap) {
-  __shared__ float tmp[kOriBins + 4];
-  if (blockIdx.x >= min(*nsurv, (unsigned)cap)) return;
-  const int lane = threadIdx.x;
-  const Surv sv = surv[blockIdx.x];
-  const Kp& kpt = sv.k;
-  const int o = sv.o, r = sv.r, c = sv.c;
-  const Oct& q = P.o[o];
-  const float* img = gauss + q.g + (size_t)q.w * q.h * sv.layer;
-  const float scl_octv = kpt.size * 0.5f / (1 << o);
-  const int radius = rnd(kOriRadius * scl_octv);
-  const float osig = kOriSigFctr * scl_octv;
-  const float expf_scale = -1.f / (2.f * osig * osig);
-  if (lane < kOriBins + 4) tmp[lane] = 0.f;
+// one 256-thread block per survivor: calcOrientationHist + one keypoint per histogram
+// peak.  The window's samples are computed 256 at a time (one per thread, in OpenCV's
+// row-major order), compacted in that order, and added to the LDS histogram by one lane
+// in order (LDS operations of a wave retire in order), so every bin sums in OpenCV's order.
+constexpr int kOT = 256;
+__device__ inline int block_compact_slot(bool ok, int* wcnt, int& total) {
+  // position of this thread's item among the block's valid items (thread order)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+  if (lane == 0) wcnt[wave] = __builtin_popcountll(m);
   __syncthreads();
-  float* temphist = tmp + 2;
-  const int side = 2 * radius + 1, total = side * side;
-  for (int p0 = 0; p0 < total; p0 += 64) {
-    const int p = p0 + lane;
-    const int i = p / side - radius, j = p % side - radius;
-    const int y = r + i, x = c + j;
-    const bool ok = p < total && y > 0 && y < q.h - 1 && x > 0 && x < q.w - 1;
-    int bin = 0;
-    float val = 0.f;
-    if (ok) {
-      const float dx = at(img, q.w, y, x + 1) - at(img, q.w, y, x - 1);
-      const float dy = at(img, q.w, y - 1, x) - at(img, q.w, y + 1, x);
-      const float wgt = fexp((i * i + j * j) * expf_scale);
-      const float ori = fast_atan2(dy, dx);
-      const float mag = fmag(dx, dy);
-      bin = rnd((kOriBins / 360.f) * ori);
-      if (bin >= kOriBins) bin -= kOriBins;
-      if (bin < 0) bin += kOriBins;
-      val = wgt * mag;
-    }
-    uint64_t m = __builtin_amdgcn_ballot_w64(ok);
-    while (m) {   // ordered: lowest lane first (LDS operations of a wave retire in order)
-      const int t = __builtin_ctzll(m);
-      m &= m - 1;
-      if (lane == t) atomicAdd(&temphist[bin], val);
-    }
+  int base = 0;
+  total = 0;
+  for (int w2 = 0; w2 < (int)(blockDim.x >> 6); ++w2) {
+    base += w2 < wave ? wcnt[w2] : 0;
+    total += wcnt[w2];
   }
-  __syncthreads();
-  if (lane != 0) return;
-  temphist[-1] = temphist[kOriBins - 1];
-  temphist[-2] = temphist[kOriBins - 2];
-  temphist[kOriBins] = temphist[0];
-  temphist[kOriBins + 1] = temphist[1];
-  float hist[kOriBins];
-  for (int i = 0; i < kOriBins; i++)
-    hist[i] = (temphist[i - 2] + temphist[i + 2]) * (1.f / 16.f) +
-              (temphist[i - 1] + temphist[i + 1]) * (4.f / 16.f) + temphist[i] * (6.f / 16.f);
-  float omax = hist[0];
-  for (int i = 1; i < kOriBins; i++) omax = fmaxf(omax, hist[i]);
-  const float mag_thr = omax * kOriPeakRatio;
-  // firstOctave = -1 rescale (exact, so it commutes with OpenCV's later sort / dedup)
-  const float scale = 1.f / (float)(1 << -kFirstOctave);
-  Kp out = kpt;
-  out.octave = (kpt.octave & ~255) | ((kpt.octave + kFirstOctave) & 255);
-  out.x = kpt.x * scale;
-  out.y = kpt.y * scale;
-  out.size = kpt.size * scale;
-  out.pad0 = out.pad1 = 0;
-  for (int j = 0; j < kOriBins; j++) {
-    const int l = j > 0 ? j - 1 : kOriBins - 1;
-    const int r2 = j < kOriBins - 1 ? j + 1 : 0;
-    if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
-      float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
-      bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
-      out.angle = 360.f - (float)((360.f / kOriBins) * bin);
-      if (fabsf(out.angle - 360.f) < 1.1920928955078125e-07f) out.angle = 0.f;
-      const unsigned k = atomicAdd(nkp, 1u);
-      if (k < (unsigned)kcap) kps[k] = out;
+  return base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+__global__ __launch_bounds__(kOT) void orient_kernel(const float* __restrict__ gauss, Pyr P,
+                                                     const Surv* __restrict__ surv,
+                                                     const unsigned* __restrict__ nsurv, int cap,
+                                                     Kp* __restrict__ kps, unsigned* __restrict__ nkp,
+                                                     int kcap) {
+  __shared__ float tmp[kOriBins + 4 + 1];   // + a dummy bin for the padding samples
+  __shared__ __attribute__((aligned(16))) int sbin[kOT + 16];
+  __shared__ __attribute__((aligned(16))) float sval[kOT + 16];
+  __shared__ int wcnt[kOT / 64];
+  const int nsv = (int)min(*nsurv, (unsigned)cap);
+  const int tid = threadIdx.x;
+  for (int sid = blockIdx.x; sid < nsv; sid += gridDim.x) {
+    const Surv sv = surv[sid];
+    const Kp& kpt = sv.k;
+    const int o = sv.o, r = sv.r, c = sv.c;
+    const Oct& q = P.o[o];
+    const float* img = gauss + q.g + (size_t)q.w * q.h * sv.layer;
+    const float scl_octv = kpt.size * 0.5f / (1 << o);
+    const int radius = rnd(kOriRadius * scl_octv);
+    const float osig = kOriSigFctr * scl_octv;
+    const float expf_scale = -1.f / (2.f * osig * osig);
+    if (tid < kOriBins + 5) tmp[tid] = 0.f;
+    float* temphist = tmp + 2;
+    const int side = 2 * radius + 1, total = side * side;
+    for (int p0 = 0; p0 < total; p0 += kOT) {
+      const int p = p0 + tid;
+      const int i = p / side - radius, j = p % side - radius;
+      const int y = r + i, x = c + j;
+      const bool ok = p < total && y > 0 && y < q.h - 1 && x > 0 && x < q.w - 1;
+      int bin = 0;
+      float val = 0.f;
+      if (ok) {
+        const float dx = at(img, q.w, y, x + 1) - at(img, q.w, y, x - 1);
+        const float dy = at(img, q.w, y - 1, x) - at(img, q.w, y + 1, x);
+        const float wgt = fexp((i * i + j * j) * expf_scale);
+        const float ori = fast_atan2(dy, dx);
+        const float mag = fmag(dx, dy);
+        bin = rnd((kOriBins / 360.f) * ori);
+        if (bin >= kOriBins) bin -= kOriBins;
+        if (bin < 0) bin += kOriBins;
+        val = wgt * mag;
+      }
+      int nv;
+      const int slot = block_compact_slot(ok, wcnt, nv);
+      if (ok) {
+        sbin[slot] = bin;
+        sval[slot] = val;
+      }
+      if (tid < 16) {   // pad to a multiple of 16 with zero adds to the dummy bin
+        sbin[nv + tid] = kOriBins + 2;
+        sval[nv + tid] = 0.f;
+      }
+      __syncthreads();
+      if (tid == 0 && !(SOD_SIFT_EXP & 2)) {
+        for (int t0 = 0; t0 < nv; t0 += 16) {
+          int4 b4[4];
+          float4 v4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            b4[u] = *reinterpret_cast<const int4*>(&sbin[t0 + 4 * u]);
+            v4[u] = *reinterpret_cast<const float4*>(&sval[t0 + 4 * u]);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            atomicAdd(&temphist[b4[u].x], v4[u].x);
+            atomicAdd(&temphist[b4[u].y], v4[u].y);
+            atomicAdd(&temphist[b4[u].z], v4[u].z);
+            atomicAdd(&temphist[b4[u].w], v4[u].w);
+          }
+        }
+      }
+      __syncthreads();
     }
+    if (tid == 0) {
+      temphist[-1] = temphist[kOriBins - 1];
+      temphist[-2] = temphist[kOriBins - 2];
+      temphist[kOriBins] = temphist[0];
+      temphist[kOriBins + 1] = temphist[1];
+      float hist[kOriBins];
+      for (int i = 0; i < kOriBins; i++)
+        hist[i] = (temphist[i - 2] + temphist[i + 2]) * (1.f / 16.f) +
+                  (temphist[i - 1] + temphist[i + 1]) * (4.f / 16.f) + temphist[i] * (6.f / 16.f);
+      float omax = hist[0];
+      for (int i = 1; i < kOriBins; i++) omax = fmaxf(omax, hist[i]);
+      const float mag_thr = omax * kOriPeakRatio;
+      // firstOctave = -1 rescale (exact, so it commutes with OpenCV's later sort / dedup)
+      const float scale = 1.f / (float)(1 << -kFirstOctave);
+      Kp out = kpt;
+      out.octave = (kpt.octave & ~255) | ((kpt.octave + kFirstOctave) & 255);
+      out.x = kpt.x * scale;
+      out.y = kpt.y * scale;
+      out.size = kpt.size * scale;
+      out.pad0 = out.pad1 = 0;
+      for (int j = 0; j < kOriBins; j++) {
+        const int l = j > 0 ? j - 1 : kOriBins - 1;
+        const int r2 = j < kOriBins - 1 ? j + 1 : 0;
+        if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+          float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
+          bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
+          out.angle = 360.f - (float)((360.f / kOriBins) * bin);
+          if (fabsf(out.angle - 360.f) < 1.1920928955078125e-07f) out.angle = 0.f;
+          const unsigned k = atomicAdd(nkp, 1u);
+          if (k < (unsigned)kcap) kps[k] = out;
+        }
+      }
+    }
+    __syncthreads();   // tmp is reused by the next survivor
   }
 }
 
@@ -533,179 +811,213 @@ __device__ inline bool kp_same(const Kp& a, const Kp& b) {
 }
 
 constexpr int kRankTile = 64;
-// (i tile, j tile) blocks.  pass 0: dup[i] |= an equal (x, y, size, angle) keypoint
-// precedes i; pass 1: before[i] += kept keypoints preceding i (the sorted position)
-__global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ kps, int n, int pass,
-                                                         unsigned* __restrict__ dup,
+// (i tile, j tile) pairs, strided over the grid.  pass 0: dup[i] |= an equal (x, y, size,
+// angle) keypoint precedes i; pass 1: before[i] += kept keypoints preceding i (the sorted
+// position)
+__global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ kps,
+                                                         const unsigned* __restrict__ nkp, int kcap,
+                                                         int pass, unsigned* __restrict__ dup,
                                                          unsigned* __restrict__ before) {
   __shared__ Kp tile[kRankTile];
   __shared__ unsigned tdup[kRankTile];
-  const int i = blockIdx.x * kRankTile + threadIdx.x;
-  const int j0 = blockIdx.y * kRankTile;
-  if (j0 + (int)threadIdx.x < n) {
-    tile[threadIdx.x] = kps[j0 + threadIdx.x];
-    tdup[threadIdx.x] = pass ? dup[j0 + threadIdx.x] : 0u;
-  }
-  __syncthreads();
-  if (i >= n) return;
-  const Kp me = kps[i];
-  const int m = min(kRankTile, n - j0);
-  unsigned cnt = 0;
-  bool d = false;
-  for (int j = 0; j < m; ++j) {
-    const bool lt = kp_less(tile[j], j0 + j, me, i);
-    if (pass == 0)
-      d = d || (lt && kp_same(tile[j], me));
-    else
-      cnt += (lt && !tdup[j]) ? 1u : 0u;
-  }
-  if (pass == 0) {
-    if (d) atomicOr(&dup[i], 1u);
-  } else if (cnt) {
-    atomicAdd(&before[i], cnt);
+  const int n = (int)min(*nkp, (unsigned)kcap);
+  const int tiles = (n + kRankTile - 1) / kRankTile;
+  for (int tp = blockIdx.x; tp < tiles * tiles; tp += gridDim.x) {
+    const int i = (tp % tiles) * kRankTile + threadIdx.x;
+    const int j0 = (tp / tiles) * kRankTile;
+    __syncthreads();
+    if (j0 + (int)threadIdx.x < n) {
+      tile[threadIdx.x] = kps[j0 + threadIdx.x];
+      tdup[threadIdx.x] = pass ? dup[j0 + threadIdx.x] : 0u;
+    }
+    __syncthreads();
+    if (i >= n) continue;
+    const Kp me = kps[i];
+    const int m = min(kRankTile, n - j0);
+    unsigned cnt = 0;
+    bool d = false;
+    for (int j = 0; j < m; ++j) {
+      const bool lt = kp_less(tile[j], j0 + j, me, i);
+      if (pass == 0)
+        d = d || (lt && kp_same(tile[j], me));
+      else
+        cnt += (lt && !tdup[j]) ? 1u : 0u;
+    }
+    if (pass == 0) {
+      if (d) atomicOr(&dup[i], 1u);
+    } else if (cnt) {
+      atomicAdd(&before[i], cnt);
+    }
   }
 }
 
-__global__ void scatter_kernel(const Kp* __restrict__ kps, int n, const unsigned* __restrict__ dup,
-                               const unsigned* __restrict__ before, Kp* __restrict__ sorted,
-                               unsigned* __restrict__ nfinal) {
+__global__ void scatter_kernel(const Kp* __restrict__ kps, const unsigned* __restrict__ nkp, int kcap,
+                               const unsigned* __restrict__ dup, const unsigned* __restrict__ before,
+                               Kp* __restrict__ sorted, unsigned* __restrict__ nfinal) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || dup[i]) return;
+  if (i >= (int)min(*nkp, (unsigned)kcap) || dup[i]) return;
   sorted[before[i]] = kps[i];
   atomicAdd(nfinal, 1u);
 }
 
-// ---- descriptors: calcSIFTDescriptor, one wave per keypoint ---------------------------
-// The window's samples are computed 64 at a time (one per lane, OpenCV's row-major
-// order), compacted, and their eight trilinear contributions added to the LDS histogram
-// sample by sample (lanes 0-7, one contribution each: the eight bins of a sample are
-// distinct), so every bin sums in OpenCV's order.
+// ---- descriptors: calcSIFTDescriptor, one 256-thread block per keypoint ---------------
+// The window's samples are computed 256 at a time (one per thread, OpenCV's row-major
+// order), compacted in that order, and their eight trilinear contributions added to the
+// LDS histogram sample by sample (lanes 0-7 of wave 0, one contribution each: the eight
+// bins of a sample are distinct), so every bin sums in OpenCV's order.
 constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);
-__global__ __launch_bounds__(64) void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
-                                                        const Kp* __restrict__ sorted,
-                                                        const unsigned* __restrict__ nfinal,
-                                                        float* __restrict__ desc) {
-  __shared__ float hist[kHistLen];
-  __shared__ int sidx[64];
-  __shared__ float sval[64][8];
+constexpr int kDT = 256;
+__global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
+                                                         const Kp* __restrict__ sorted,
+                                                         const unsigned* __restrict__ nfinal,
+                                                         float* __restrict__ desc) {
+  __shared__ float hist[kHistLen + 72];   // + a dummy region for the padding samples
+  __shared__ __attribute__((aligned(16))) int sidx[kDT + 16];
+  __shared__ __attribute__((aligned(16))) float svalT[8][kDT + 16];
   __shared__ float raw[kD * kD * kN];
   __shared__ float scal[2];
-  const int id = blockIdx.x;
-  if (id >= (int)*nfinal) return;
-  const int lane = threadIdx.x;
-  const Kp k = sorted[id];
-  int octave = k.octave & 255;
-  const int layer = (k.octave >> 8) & 255;
-  octave = octave < 128 ? octave : (-128 | octave);
-  const float sc = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
-  const float size = k.size * sc;
-  const Oct& q = P.o[octave - kFirstOctave];
-  const float* img = gauss + q.g + (size_t)q.w * q.h * layer;
-  float ori = 360.f - k.angle;
-  if (fabsf(ori - 360.f) < 1.1920928955078125e-07f) ori = 0.f;
-  const float scl = size * 0.5f;
-  const float ptx = k.x * sc, pty = k.y * sc;
-
-  const int px = rnd(ptx), py = rnd(pty);
-  double sd, cd;
-  s_sincos((double)(ori * (float)(3.14159265358979323846 / 180)), &sd, &cd);
-  float cos_t = (float)cd, sin_t = (float)sd;
-  const float bins_per_rad = kN / 360.f;
-  const float exp_scale = -1.f / (kD * kD * 0.5f);
-  const float hist_width = kDescrSclFctr * scl;
-  int radius = rnd(hist_width * 1.4142135623730951f * (kD + 1) * 0.5f);
-  const int diag = isqrt64((int64_t)q.w * q.w + (int64_t)q.h * q.h);
-  radius = min(radius, diag);
-  cos_t /= hist_width;
-  sin_t /= hist_width;
-  const int rows = q.h, cols = q.w;
-  for (int t = lane; t < kHistLen; t += 64) hist[t] = 0.f;
-  // the eight bins of a sample relative to its first
-  const int off = lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? kN + 2 : lane == 3 ? kN + 3
-                : lane == 4 ? (kD + 2) * (kN + 2) : lane == 5 ? (kD + 2) * (kN + 2) + 1
-                : lane == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
-  __syncthreads();
-  const int side = 2 * radius + 1;
-  const int64_t total = (int64_t)side * side;
-  for (int64_t p0 = 0; p0 < total; p0 += 64) {
-    const int64_t p = p0 + lane;
-    const int i = (int)(p / side) - radius, j = (int)(p % side) - radius;
-    const float c_rot = j * cos_t - i * sin_t;
-    const float r_rot = j * sin_t + i * cos_t;
-    float rbin = r_rot + kD / 2 - 0.5f;
-    float cbin = c_rot + kD / 2 - 0.5f;
-    const int r = py + i, c = px + j;
-    const bool ok = p < total && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 &&
-                    r < rows - 1 && c > 0 && c < cols - 1;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
-    if (ok) {
-      const float dx = at(img, cols, r, c + 1) - at(img, cols, r, c - 1);
-      const float dy = at(img, cols, r - 1, c) - at(img, cols, r + 1, c);
-      const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
-      const float o_k = fast_atan2(dy, dx);
-      const float mag_k = fmag(dx, dy);
-      const float w_k = fexp(wexp);
-      float obin = (o_k - ori) * bins_per_rad;
-      const float mag = mag_k * w_k;
-      const int r0 = flo(rbin), c0 = flo(cbin);
-      int o0 = flo(obin);
-      rbin -= r0;
-      cbin -= c0;
-      obin -= o0;
-      if (o0 < 0) o0 += kN;
-      if (o0 >= kN) o0 -= kN;
-      const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-      const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-      const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-      const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-      const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-      const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-      const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-      const int slot = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-      sidx[slot] = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
-      sval[slot][0] = v_rco000;
-      sval[slot][1] = v_rco001;
-      sval[slot][2] = v_rco010;
-      sval[slot][3] = v_rco011;
-      sval[slot][4] = v_rco100;
-      sval[slot][5] = v_rco101;
-      sval[slot][6] = v_rco110;
-      sval[slot][7] = v_rco111;
+  __shared__ int wcnt[kDT / 64];
+  const int tid = threadIdx.x;
+  const int nf = (int)*nfinal;
+  // the eight bins of a sample relative to its first (lanes 0-7)
+  const int off = tid == 0 ? 0 : tid == 1 ? 1 : tid == 2 ? kN + 2 : tid == 3 ? kN + 3
+                : tid == 4 ? (kD + 2) * (kN + 2) : tid == 5 ? (kD + 2) * (kN + 2) + 1
+                : tid == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
+  for (int id = blockIdx.x; id < nf; id += gridDim.x) {
+    const Kp k = sorted[id];
+    int octave = k.octave & 255;
+    const int layer = (k.octave >> 8) & 255;
+    octave = octave < 128 ? octave : (-128 | octave);
+    const float sc = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
+    const float size = k.size * sc;
+    const Oct& q = P.o[octave - kFirstOctave];
+    const float* img = gauss + q.g + (size_t)q.w * q.h * layer;
+    float ori = 360.f - k.angle;
+    if (fabsf(ori - 360.f) < 1.1920928955078125e-07f) ori = 0.f;
+    const float scl = size * 0.5f;
+    const float ptx = k.x * sc, pty = k.y * sc;
+    const int px = rnd(ptx), py = rnd(pty);
+    double sd, cd;
+    s_sincos((double)(ori * (float)(3.14159265358979323846 / 180)), &sd, &cd);
+    float cos_t = (float)cd, sin_t = (float)sd;
+    const float bins_per_rad = kN / 360.f;
+    const float exp_scale = -1.f / (kD * kD * 0.5f);
+    const float hist_width = kDescrSclFctr * scl;
+    int radius = rnd(hist_width * 1.4142135623730951f * (kD + 1) * 0.5f);
+    const int diag = isqrt64((int64_t)q.w * q.w + (int64_t)q.h * q.h);
+    radius = min(radius, diag);
+    cos_t /= hist_width;
+    sin_t /= hist_width;
+    const int rows = q.h, cols = q.w;
+    for (int t = tid; t < kHistLen; t += kDT) hist[t] = 0.f;
+    const int side = 2 * radius + 1;
+    const int64_t total = (int64_t)side * side;
+    for (int64_t p0 = 0; p0 < total; p0 += kDT) {
+      const int64_t p = p0 + tid;
+      const int i = (int)(p / side) - radius, j = (int)(p % side) - radius;
+      const float c_rot = j * cos_t - i * sin_t;
+      const float r_rot = j * sin_t + i * cos_t;
+      float rbin = r_rot + kD / 2 - 0.5f;
+      float cbin = c_rot + kD / 2 - 0.5f;
+      const int r = py + i, c = px + j;
+      const bool ok = p < total && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 &&
+                      r < rows - 1 && c > 0 && c < cols - 1;
+      int idx = 0;
+      float v8[8];
+      if (ok) {
+        const float dx = at(img, cols, r, c + 1) - at(img, cols, r, c - 1);
+        const float dy = at(img, cols, r - 1, c) - at(img, cols, r + 1, c);
+        const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
+        const float o_k = fast_atan2(dy, dx);
+        const float mag_k = fmag(dx, dy);
+        const float w_k = fexp(wexp);
+        float obin = (o_k - ori) * bins_per_rad;
+        const float mag = mag_k * w_k;
+        const int r0 = flo(rbin), c0 = flo(cbin);
+        int o0 = flo(obin);
+        rbin -= r0;
+        cbin -= c0;
+        obin -= o0;
+        if (o0 < 0) o0 += kN;
+        if (o0 >= kN) o0 -= kN;
+        const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+        const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+        const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+        v8[7] = v_rc11 * obin;            // v_rco111
+        v8[6] = v_rc11 - v8[7];           // v_rco110
+        v8[5] = v_rc10 * obin;            // v_rco101
+        v8[4] = v_rc10 - v8[5];           // v_rco100
+        v8[3] = v_rc01 * obin;            // v_rco011
+        v8[2] = v_rc01 - v8[3];           // v_rco010
+        v8[1] = v_rc00 * obin;            // v_rco001
+        v8[0] = v_rc00 - v8[1];           // v_rco000
+        idx = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
+      }
+      int nv;
+      const int slot = block_compact_slot(ok, wcnt, nv);
+      if (ok) {
+        sidx[slot] = idx;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) svalT[e][slot] = v8[e];
+      }
+      if (tid < 16) {   // pad to a multiple of 16 with zero adds to the dummy bins
+        sidx[nv + tid] = kHistLen;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) svalT[e][nv + tid] = 0.f;
+      }
+      __syncthreads();
+      if (tid < 8 && !(SOD_SIFT_EXP & 1)) {
+        // 16 samples' indices and this lane's values read as 128-bit vectors, then the
+        // 16 adds (in order, fire-and-forget)
+        for (int t0 = 0; t0 < nv; t0 += 16) {
+          int4 i4[4];
+          float4 v4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            i4[u] = *reinterpret_cast<const int4*>(&sidx[t0 + 4 * u]);
+            v4[u] = *reinterpret_cast<const float4*>(&svalT[tid][t0 + 4 * u]);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            atomicAdd(&hist[i4[u].x + off], v4[u].x);
+            atomicAdd(&hist[i4[u].y + off], v4[u].y);
+            atomicAdd(&hist[i4[u].z + off], v4[u].z);
+            atomicAdd(&hist[i4[u].w + off], v4[u].w);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // finalize: fold the circular orientation bins, then OpenCV's sequential norms
+    if (tid < kD * kD) {
+      const int i = tid / kD, j = tid % kD;
+      const int idx = ((i + 1) * (kD + 2) + (j + 1)) * (kN + 2);
+      hist[idx] += hist[idx + kN];
+      hist[idx + 1] += hist[idx + kN + 1];
+      for (int k2 = 0; k2 < kN; k2++) raw[(i * kD + j) * kN + k2] = hist[idx + k2];
     }
     __syncthreads();
-    const int nv = __builtin_popcountll(m);
-    if (lane < 8)
-      for (int t = 0; t < nv; ++t) atomicAdd(&hist[sidx[t] + off], sval[t][lane]);
-    __syncthreads();
-  }
-  // finalize: fold the circular orientation bins, then OpenCV's sequential norms
-  if (lane < kD * kD) {
-    const int i = lane / kD, j = lane % kD;
-    const int idx = ((i + 1) * (kD + 2) + (j + 1)) * (kN + 2);
-    hist[idx] += hist[idx + kN];
-    hist[idx + 1] += hist[idx + kN + 1];
-    for (int k2 = 0; k2 < kN; k2++) raw[(i * kD + j) * kN + k2] = hist[idx + k2];
-  }
-  __syncthreads();
-  constexpr int len = kD * kD * kN;
-  if (lane == 0) {
-    float nrm2 = 0;
-    for (int k2 = 0; k2 < len; k2++) nrm2 += raw[k2] * raw[k2];
-    const float thr = sqrt_rn(nrm2) * kDescrMagThr;
-    nrm2 = 0;
-    for (int i = 0; i < len; i++) {
-      const float val = fminf(raw[i], thr);
-      raw[i] = val;
-      nrm2 += val * val;
+    constexpr int len = kD * kD * kN;
+    if (tid == 0) {
+      float nrm2 = 0;
+      for (int k2 = 0; k2 < len; k2++) nrm2 += raw[k2] * raw[k2];
+      const float thr = sqrt_rn(nrm2) * kDescrMagThr;
+      nrm2 = 0;
+      for (int i = 0; i < len; i++) {
+        const float val = fminf(raw[i], thr);
+        raw[i] = val;
+        nrm2 += val * val;
+      }
+      scal[0] = kIntDescrFctr / fmaxf(sqrt_rn(nrm2), 1.1920928955078125e-07f);
     }
-    scal[0] = kIntDescrFctr / fmaxf(sqrt_rn(nrm2), 1.1920928955078125e-07f);
-  }
-  __syncthreads();
-  const float nrm = scal[0];
-  float* dst = desc + (size_t)id * 128;
-  for (int k2 = lane; k2 < len; k2 += 64) {
-    const int v = rnd(raw[k2] * nrm);
-    dst[k2] = (float)(v < 0 ? 0 : v > 255 ? 255 : v);
+    __syncthreads();
+    const float nrm = scal[0];
+    float* dst = desc + (size_t)id * 128;
+    if (tid < len) {
+      const int v = rnd(raw[tid] * nrm);
+      dst[tid] = (float)(v < 0 ? 0 : v > 255 ? 255 : v);
+    }
+    __syncthreads();   // LDS reused by the next keypoint
   }
 }
 
@@ -754,6 +1066,7 @@ struct SiftWork {
   double contrast = 0.04, edge = 10.0, sigma = 1.6;
   int radius[kMaxLayers] = {};
   DevBuf<float> kern;          // [kMaxLayers][kMaxTaps]
+  DevBuf<int> rad;             // [kMaxLayers]
   bool kern_ok = false;
   Pyr P{};
   DevBuf<uint8_t> gray;
@@ -773,6 +1086,7 @@ void sod_sift_free(sod_ctx* ctx) {
   SiftWork* S = ctx->sift;
   if (!S) return;
   sod_release(S->kern);
+  sod_release(S->rad);
   sod_release(S->gray);
   sod_release(S->gauss);
   sod_release(S->dogs);
@@ -816,7 +1130,9 @@ int set_kernels(sod_ctx* ctx, SiftWork& S) {
     if (S.radius[i] < 0) return sod_fail(ctx, SOD_EINVAL, "sigma too large for the blur kernel");
   }
   SOD_TRY(sod_reserve(ctx, S.kern, h.size()));
+  SOD_TRY(sod_reserve(ctx, S.rad, (size_t)kMaxLayers));
   SOD_HIP(ctx, hipMemcpyAsync(S.kern.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(S.rad.p, S.radius, sizeof(S.radius), hipMemcpyHostToDevice, ctx->stream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   S.kern_ok = true;
   return SOD_OK;
@@ -826,9 +1142,9 @@ int blur(sod_ctx* ctx, SiftWork& S, const float* src, float* dst, int w, int h, 
          const float* prev, float* dog) {
   const float* k = S.kern.p + (size_t)layer * kMaxTaps;
   const int r = S.radius[layer];
-  if (r <= kMaxR) {
+  if (r >= 1 && r <= kMaxR) {
     dim3 gt((unsigned)((w + kTW - 1) / kTW), (unsigned)((h + kTH - 1) / kTH));
-    hipLaunchKernelGGL(blur_tile_kernel, gt, dim3(256), 0, ctx->stream, src, dst, w, h, k, r, dog);
+    hipLaunchKernelGGL(kBlurFns[r], gt, dim3(256), 0, ctx->stream, src, dst, w, h, k, dog);
     return SOD_OK;
   }
   dim3 g((unsigned)((w + 255) / 256), (unsigned)h);
@@ -838,7 +1154,12 @@ int blur(sod_ctx* ctx, SiftWork& S, const float* src, float* dst, int w, int h, 
   return SOD_OK;
 }
 
-// detect + describe one image already in S.gray; leaves the results on the device
+constexpr int kOrientGrid = 4096, kRankGrid = 2048, kDescGrid = 4096;
+
+// detect + describe one image already in S.gray: every stage is enqueued back to back
+// (grids sized by capacity, counts read on the device); one host sync at the end reads
+// the counts.  An overflow of the candidate / keypoint lists grows them and re-runs
+// (the result does not depend on discovery order).
 int run_image(sod_ctx* ctx, SiftWork& S, int w, int h) {
   SOD_TRY(set_kernels(ctx, S));
   const int L = S.L;
@@ -861,88 +1182,82 @@ int run_image(sod_ctx* ctx, SiftWork& S, int w, int h) {
       break;
     }
   }
+  int o_small = nOct;   // first octave handled by small_octaves_kernel
+  for (int o = 1; o < nOct && L + 2 <= kChainDog; ++o)
+    if ((int64_t)P.o[o].w * P.o[o].h <= kChainPixels) {
+      o_small = o;
+      break;
+    }
   SOD_TRY(sod_reserve(ctx, S.gauss, (size_t)go));
   SOD_TRY(sod_reserve(ctx, S.dogs, (size_t)dof));
   SOD_TRY(sod_reserve(ctx, S.tmp, (size_t)bw * bh));
   SOD_TRY(sod_reserve(ctx, S.up, (size_t)bw * bh));
   SOD_TRY(sod_reserve(ctx, S.cnt, 4));
-
-  hipLaunchKernelGGL(upscale_kernel, dim3((unsigned)((bw + 255) / 256), (unsigned)bh), dim3(256), 0,
-                     ctx->stream, S.gray.p, w, h, S.up.p);
-  for (int o = 0; o < nOct; ++o) {
-    const Oct& q = P.o[o];
-    const size_t plane = (size_t)q.w * q.h;
-    float* g0 = S.gauss.p + q.g;
-    if (o == 0) {
-      SOD_TRY(blur(ctx, S, S.up.p, g0, q.w, q.h, 0, nullptr, nullptr));
-    } else {
-      const Oct& pq = P.o[o - 1];
-      hipLaunchKernelGGL(down2_kernel, dim3((unsigned)((q.w + 255) / 256), (unsigned)q.h), dim3(256),
-                         0, ctx->stream, S.gauss.p + pq.g + (size_t)pq.w * pq.h * L, pq.w, g0, q.w);
-    }
-    for (int i = 1; i < L + 3; ++i)
-      SOD_TRY(blur(ctx, S, g0 + plane * (i - 1), g0 + plane * i, q.w, q.h, i, g0 + plane * (i - 1),
-                   S.dogs.p + q.d + plane * (i - 1)));
-  }
   const float thr = (float)(int)std::floor(0.5 * S.contrast / L * 255 * 1);
-  for (int attempt = 0; attempt < 3; ++attempt) {
-    SOD_TRY(sod_reserve(ctx, S.cand, (size_t)S.cap));
-    SOD_TRY(sod_reserve(ctx, S.surv, (size_t)S.cap));
-    SOD_TRY(sod_reserve(ctx, S.kps, (size_t)S.cap));
+
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    const int cap = S.cap;
+    SOD_TRY(sod_reserve(ctx, S.cand, (size_t)cap));
+    SOD_TRY(sod_reserve(ctx, S.surv, (size_t)cap));
+    SOD_TRY(sod_reserve(ctx, S.kps, (size_t)cap));
+    SOD_TRY(sod_reserve(ctx, S.sorted, (size_t)cap));
+    SOD_TRY(sod_reserve(ctx, S.dup, (size_t)cap));
+    SOD_TRY(sod_reserve(ctx, S.before, (size_t)cap));
     SOD_HIP(ctx, hipMemsetAsync(S.cnt.p, 0, 16, ctx->stream));
-    for (int o = 0; o < nOct; ++o) {
+    if (attempt == 0) {   // the pyramid (and the small octaves' extrema)
+      hipLaunchKernelGGL(upscale_kernel, dim3((unsigned)((bw + 255) / 256), (unsigned)bh), dim3(256),
+                         0, ctx->stream, S.gray.p, w, h, S.up.p);
+      for (int o = 0; o < o_small; ++o) {
+        const Oct& q = P.o[o];
+        const size_t plane = (size_t)q.w * q.h;
+        float* g0 = S.gauss.p + q.g;
+        if (o == 0) {
+          SOD_TRY(blur(ctx, S, S.up.p, g0, q.w, q.h, 0, nullptr, nullptr));
+        } else {
+          const Oct& pq = P.o[o - 1];
+          hipLaunchKernelGGL(down2_kernel, dim3((unsigned)((q.w + 255) / 256), (unsigned)q.h),
+                             dim3(256), 0, ctx->stream, S.gauss.p + pq.g + (size_t)pq.w * pq.h * L,
+                             pq.w, g0, q.w);
+        }
+        for (int i = 1; i < L + 3; ++i)
+          SOD_TRY(blur(ctx, S, g0 + plane * (i - 1), g0 + plane * i, q.w, q.h, i,
+                       g0 + plane * (i - 1), S.dogs.p + q.d + plane * (i - 1)));
+      }
+    }
+    for (int o = 0; o < o_small; ++o) {
       const Oct& q = P.o[o];
       if (q.w <= 2 * kBorder || q.h <= 2 * kBorder) continue;
       dim3 g((unsigned)((q.w - 2 * kBorder + 255) / 256), (unsigned)(q.h - 2 * kBorder), (unsigned)L);
       hipLaunchKernelGGL(extrema_kernel, g, dim3(256), 0, ctx->stream, S.dogs.p, P, o, thr, S.cand.p,
-                         S.cnt.p, S.cap);
+                         S.cnt.p, cap);
     }
+    if (o_small < nOct)   // re-running it re-blurs the small octaves identically
+      hipLaunchKernelGGL(small_octaves_kernel, dim3(1), dim3(1024), 0, ctx->stream, S.gauss.p,
+                         S.dogs.p, P, o_small, S.kern.p, S.rad.p, thr, S.cand.p, S.cnt.p, cap);
+    hipLaunchKernelGGL(refine_kernel, dim3((unsigned)((cap + 127) / 128)), dim3(128), 0, ctx->stream,
+                       S.dogs.p, P, S.cand.p, S.cnt.p, cap, (float)S.contrast, (float)S.edge,
+                       (float)S.sigma, S.surv.p, S.cnt.p + 3);
+    hipLaunchKernelGGL(orient_kernel, dim3(kOrientGrid), dim3(kOT), 0, ctx->stream, S.gauss.p, P,
+                       S.surv.p, S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap);
+    SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)cap * 4, ctx->stream));
+    SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)cap * 4, ctx->stream));
+    for (int pass = 0; pass < 2; ++pass)
+      hipLaunchKernelGGL(rank_kernel, dim3(kRankGrid), dim3(kRankTile), 0, ctx->stream, S.kps.p,
+                         S.cnt.p + 1, cap, pass, S.dup.p, S.before.p);
+    hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, ctx->stream,
+                       S.kps.p, S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2);
+    SOD_TRY(sod_reserve(ctx, S.desc, (size_t)cap * 128));
+    hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, ctx->stream, S.gauss.p, P,
+                       S.sorted.p, S.cnt.p + 2, S.desc.p);
+    SOD_HIP(ctx, hipGetLastError());
     unsigned c[4];
     SOD_HIP(ctx, hipMemcpyAsync(c, S.cnt.p, 16, hipMemcpyDeviceToHost, ctx->stream));
     SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (c[0] > (unsigned)S.cap) {   // grow and redo (the result does not depend on order)
-      S.cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)c[0]);
+    if (c[0] > (unsigned)cap || c[1] > (unsigned)cap) {
+      S.cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)std::max(c[0], c[1]));
       continue;
     }
-    const unsigned ncand = c[0];
-    if (ncand > 0) {
-      hipLaunchKernelGGL(refine_kernel, dim3((ncand + 127) / 128), dim3(128), 0, ctx->stream, S.dogs.p,
-                         P, S.cand.p, S.cnt.p, S.cap, (float)S.contrast, (float)S.edge,
-                         (float)S.sigma, S.surv.p, S.cnt.p + 3);
-      // survivors <= candidates <= cap: one block per candidate slot, idle ones exit
-      hipLaunchKernelGGL(orient_kernel, dim3(ncand), dim3(64), 0, ctx->stream, S.gauss.p, P, S.surv.p,
-                         S.cnt.p + 3, S.cap, S.kps.p, S.cnt.p + 1, S.cap);
-    }
-    SOD_HIP(ctx, hipMemcpyAsync(c, S.cnt.p, 16, hipMemcpyDeviceToHost, ctx->stream));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (c[1] > (unsigned)S.cap) {
-      S.cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)c[1]);
-      continue;
-    }
-    const int nk = (int)c[1];
-    unsigned nf = 0;
-    if (nk > 0) {
-      SOD_TRY(sod_reserve(ctx, S.sorted, (size_t)nk));
-      SOD_TRY(sod_reserve(ctx, S.dup, (size_t)nk));
-      SOD_TRY(sod_reserve(ctx, S.before, (size_t)nk));
-      SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)nk * 4, ctx->stream));
-      SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)nk * 4, ctx->stream));
-      const unsigned tiles = (unsigned)((nk + kRankTile - 1) / kRankTile);
-      for (int pass = 0; pass < 2; ++pass)
-        hipLaunchKernelGGL(rank_kernel, dim3(tiles, tiles), dim3(kRankTile), 0, ctx->stream, S.kps.p,
-                           nk, pass, S.dup.p, S.before.p);
-      hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0,
-                         ctx->stream, S.kps.p, nk, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2);
-      SOD_HIP(ctx, hipMemcpyAsync(&nf, S.cnt.p + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
-      SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    }
-    S.n = nf;
-    if (nf > 0) {
-      SOD_TRY(sod_reserve(ctx, S.desc, (size_t)nf * 128));
-      hipLaunchKernelGGL(descriptor_kernel, dim3(nf), dim3(64), 0, ctx->stream, S.gauss.p, P,
-                         S.sorted.p, S.cnt.p + 2, S.desc.p);
-    }
-    SOD_HIP(ctx, hipGetLastError());
+    S.n = c[2];
     S.valid = true;
     return SOD_OK;
   }
@@ -1064,3 +1379,9 @@ int sod_sift_to_queries(sod_ctx* ctx) {
 }
 
 }  // extern "C"
+
+#ifdef SOD_SIFT_STAMP
+extern "C" int sod_debug_sift_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sift_stamps), 256 * 8) == hipSuccess ? 0 : 1;
+}
+#endif
