@@ -228,12 +228,58 @@ def extras(c, ctx, shard, bins, n_images=64, per_image=500):
     t_packed = timed(lambda: c.import_packed(packed))
     if c is not ctx:
         c.share_db(ctx)     # back to the shared resident DB
-    return {"query_batch": {"images": n_images, "queries_per_image": per_image,
+    sift = sift_extras(c, bins)
+    return {"sift": sift,
+            "query_batch": {"images": n_images, "queries_per_image": per_image,
                             "per_image_pipeline_ms": t_single, "fused_batch_ms": t_fused,
                             "images_per_s": n_images / (t_fused / 1000.0),
                             "speedup": t_single / t_fused},
             "db_upload_ms": {"raw_descriptors": t_raw, "packed_image": t_packed,
                              "rows": len(shard)}}
+
+
+def sift_extras(c, bins, n_batch=16, h=800, w=1000):
+    """SURVEY 8(f) row 4 (outside the timed region): SIFT detect + describe on the device
+    for 1000 x 800 query images (the C3 query shape) -- one image (latency, keypoints and
+    descriptors back on the host), a batch of 16 (four in flight, features left on the
+    device), and 16 query images end to end (SIFT -> one matcher pass over the resident
+    DB -> fused Hough / affine / post-processing)."""
+    from sift_based_od_amd import sift_query_batch
+    imgs = [synthetic.textured_image(h, w, seed=2000 + k) for k in range(n_batch)]
+
+    def timed(fn, reps=5):
+        fn()
+        c.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        c.synchronize()
+        return (time.perf_counter() - t0) / reps * 1000.0
+
+    n_kp = len(c.sift_detect(imgs[0])["x"])
+    t_one = timed(lambda: c.sift_detect(imgs[0]), reps=10)
+    counts = c.sift_detect_batch(imgs, results=False)
+    t_batch = timed(lambda: c.sift_detect_batch(imgs, results=False))
+    t_e2e = timed(lambda: sift_query_batch(c, imgs, bins=bins, results=False), reps=3)
+    return {"image": [h, w], "keypoints_per_image": n_kp,
+            "single_image_ms": t_one,
+            "batch_images": n_batch, "batch_ms": t_batch,
+            "batch_images_per_s": n_batch / (t_batch / 1000.0),
+            "batch_keypoints": int(counts.sum()),
+            "image_to_pose_batch_ms": t_e2e,
+            "image_to_pose_images_per_s": n_batch / (t_e2e / 1000.0)}
+
+
+def cpu_sift_baseline(h=800, w=1000):
+    """oracle/sift_oracle.c (C, one thread) on the same 1000 x 800 image."""
+    from oracle import sift as osift
+    img = synthetic.textured_image(h, w, seed=2000)
+    t0 = time.perf_counter()
+    r = osift.detect_and_compute(img)
+    dt = time.perf_counter() - t0
+    return {"value": dt * 1000.0, "unit": "ms/image", "cores": 1, "kind": "port",
+            "sample": "oracle SIFT detect+describe (C restatement of OpenCV's algorithm, "
+                      "1 thread) of one %dx%d image, %d keypoints, %.2f s" % (w, h, len(r["x"]), dt)}
 
 
 def pmc_traffic(kernel, config):
@@ -426,6 +472,8 @@ def main():
                                                        idx1, good, bins)
         if post is not None:
             out["cpu_baseline_post"] = cpu_post_baseline(ctx, post)
+        if not a.no_extras:
+            out["cpu_baseline_sift"] = cpu_sift_baseline()
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -228,11 +228,20 @@ int sod_sift_detect(sod_ctx* ctx, const uint8_t* gray /* [h*w] */, int32_t width
                     int32_t height, int32_t* n_keypoints);
 int sod_sift_detect_bgr(sod_ctx* ctx, const uint8_t* bgr /* [h*w*3] */, int32_t width,
                         int32_t height, int32_t* n_keypoints);
-/* copies min(n, cap) keypoints out; every pointer may be NULL */
-int sod_sift_get(sod_ctx* ctx, int32_t cap, float* x, float* y, float* size, float* angle,
+/* several images (GenerateDatabaseInfo.py:19-37's loop, or a batch of query images):
+ * images[i] is [h_i*w_i*channels_i] 8-bit (channels 1 = gray, 3 = BGR; channels may be
+ * NULL = all gray); counts[i] = keypoints of image i.  Four images are in flight at once,
+ * each on its own stream; the results are concatenated in image order. */
+int sod_sift_detect_batch(sod_ctx* ctx, int32_t n_images, const uint8_t* const* images,
+                          const int32_t* widths, const int32_t* heights, const int32_t* channels,
+                          int32_t* counts);
+/* copies the first min(total, cap) keypoints of the last detect / batch out (image order);
+ * every pointer may be NULL */
+int sod_sift_get(sod_ctx* ctx, int64_t cap, float* x, float* y, float* size, float* angle,
                  float* response, int32_t* octave, float* descriptors /* [cap*128] */);
 /* the last detection becomes the query set (descriptors + keypoints, device to device):
- * main.py's get_query_features followed by run_matcher without a host round trip */
+ * main.py's get_query_features followed by run_matcher without a host round trip; a batch
+ * is also declared as query images (sod_query_images) for the fused per-image stages */
 int sod_sift_to_queries(sod_ctx* ctx);
 
 /* ---- host-side exchange (multi-rank over a host communicator, e.g. gloo) ------------

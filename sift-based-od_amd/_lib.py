@@ -96,7 +96,9 @@ SIGNATURES = {
     "sod_sift_set_params": (C.c_int, [c_ctx, C.c_int32, C.c_double, C.c_double, C.c_double]),
     "sod_sift_detect": (C.c_int, [c_ctx, c_u8p, C.c_int32, C.c_int32, c_i32p]),
     "sod_sift_detect_bgr": (C.c_int, [c_ctx, c_u8p, C.c_int32, C.c_int32, c_i32p]),
-    "sod_sift_get": (C.c_int, [c_ctx, C.c_int32, c_f32p, c_f32p, c_f32p, c_f32p, c_f32p, c_i32p,
+    "sod_sift_detect_batch": (C.c_int, [c_ctx, C.c_int32, C.POINTER(c_u8p), c_i32p, c_i32p,
+                                        c_i32p, c_i32p]),
+    "sod_sift_get": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_f32p, c_f32p, c_i32p,
                                c_f32p]),
     "sod_sift_to_queries": (C.c_int, [c_ctx]),
     "sod_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
@@ -479,7 +481,10 @@ class Context:
                                                   b.shape[0], C.byref(n)))
         else:
             raise ValueError("SIFT input must be [h, w] or [h, w, 3|4]")
-        n = n.value
+        self._sift_n = n.value
+        return self._sift_get(n.value, descriptors)
+
+    def _sift_get(self, n, descriptors):
         out = {k: np.zeros(n, np.float32) for k in ("x", "y", "size", "angle", "response")}
         out["octave"] = np.zeros(n, np.int32)
         desc = np.zeros((n, 128), np.float32) if descriptors else None
@@ -490,8 +495,34 @@ class Context:
             ptr(desc, C.c_float)))
         if descriptors:
             out["descriptors"] = desc
-        self._sift_n = n
         return out
+
+    def sift_detect_batch(self, images, descriptors=True, results=True):
+        """detectAndCompute on several 8-bit images (gray [h, w] or BGR [h, w, 3|4]), four
+        in flight at once.  Returns one SoA dict per image (``results=False``: only the
+        counts; the features stay on the device for ``sift_to_queries``)."""
+        imgs = []
+        for im in images:
+            a = np.asarray(im)
+            if a.dtype != np.uint8 or a.ndim not in (2, 3) or (a.ndim == 3 and a.shape[2] not in (3, 4)):
+                raise ValueError("SIFT inputs must be 8-bit [h, w] or [h, w, 3|4] images")
+            imgs.append(_c(a if a.ndim == 2 else a[:, :, :3], np.uint8))
+        n = len(imgs)
+        ptrs = (c_u8p * n)(*[ptr(a, C.c_uint8) for a in imgs])
+        w = np.array([a.shape[1] for a in imgs], np.int32)
+        h = np.array([a.shape[0] for a in imgs], np.int32)
+        ch = np.array([1 if a.ndim == 2 else 3 for a in imgs], np.int32)
+        counts = np.zeros(n, np.int32)
+        self._chk(self._L.sod_sift_detect_batch(self._h, n, ptrs, ptr(w, C.c_int32),
+                                                ptr(h, C.c_int32), ptr(ch, C.c_int32),
+                                                ptr(counts, C.c_int32)))
+        self._sift_n = int(counts.sum())
+        self._sift_counts = counts
+        if not results:
+            return counts
+        allr = self._sift_get(self._sift_n, descriptors)
+        off = np.concatenate([[0], np.cumsum(counts)])
+        return [{k: v[off[i]:off[i + 1]] for k, v in allr.items()} for i in range(n)]
 
     def sift_to_queries(self):
         """The last SIFT detection becomes the query set (device to device)."""

@@ -55,10 +55,36 @@ def run_query_batch(ctx, images, bins=15, ratio=0.75, vote_threshold=5, affine_t
     return out
 
 
+def sift_query_batch(ctx, images, bins=15, ratio=0.75, vote_threshold=5, affine_threshold=4,
+                     post_process=True, results=True):
+    """Query IMAGES end to end on the device (SURVEY 8(f) rows 3 + 4): SIFT of every image
+    (``main.py:36-45``, four in flight), ONE matcher pass over the DB for all their
+    features, then the fused per-image Hough / valid-bin / affine / post-processing stages.
+    ``images``: 8-bit gray [h, w] or BGR [h, w, 3] arrays (``cv2.imread`` output).  Returns
+    the per-image dicts of :func:`run_query_batch` plus each image's keypoint count."""
+    counts = ctx.sift_detect_batch(images, results=False)
+    if int(np.sum(counts)) == 0:
+        raise ValueError("no SIFT keypoints in the batch")
+    ctx.sift_to_queries()          # also declares the images (offsets, shapes) when > 1
+    ctx.match()
+    ctx.ratio(ratio)
+    shapes = [tuple(np.shape(im)[:2]) + (3,) for im in images]
+    out = _fused_sizes(ctx, [int(c) for c in counts], shapes, bins, vote_threshold,
+                       affine_threshold, post_process, results)
+    for r, c in zip(out, counts):
+        r["n_keypoints"] = int(c)
+    return out
+
+
 def _fused(ctx, images, bins, vote_threshold, affine_threshold, post_process, results):
-    sizes = [len(d) for d, _, _ in images]
+    return _fused_sizes(ctx, [len(d) for d, _, _ in images], [s for _, _, s in images], bins,
+                        vote_threshold, affine_threshold, post_process, results)
+
+
+def _fused_sizes(ctx, sizes, shapes, bins, vote_threshold, affine_threshold, post_process,
+                 results):
     off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
-    ctx.query_images(off, [s for _, _, s in images])
+    ctx.query_images(off, shapes)
     ctx.hough((1, 1), bins)
     ctx.select(vote_threshold)
     ctx.affine((1, 1), POS_FACTOR * 4.0, POS_FACTOR * 4.0, affine_threshold)
@@ -69,7 +95,7 @@ def _fused(ctx, images, bins, vote_threshold, affine_threshold, post_process, re
         img = ctx.valid_images()
         post = ctx.postprocess() if post_process else None
         idx1, d1, d2, good = ctx.match_result()
-        for b in range(len(images)):
+        for b in range(len(sizes)):
             lo, hi = int(off[b]), int(off[b + 1])
             sel = np.nonzero(img == b)[0]
             vo = v["offsets"]

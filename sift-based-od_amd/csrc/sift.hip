@@ -1061,6 +1061,23 @@ int gauss_kernel(double sigma, float* k) {
 
 }  // namespace
 
+// one in-flight image: its pyramid, candidate / keypoint lists and descriptors, on its
+// own stream (a batch keeps several images in flight)
+struct SiftSlot {
+  hipStream_t stream = nullptr;
+  Pyr P{};
+  DevBuf<uint8_t> gray, bgr;
+  DevBuf<float> gauss, dogs, tmp, up;
+  DevBuf<int4> cand;
+  DevBuf<Surv> surv;
+  DevBuf<Kp> kps, sorted;
+  DevBuf<unsigned> dup, before;
+  DevBuf<unsigned> cnt;        // [0] candidates, [1] raw keypoints, [2] final, [3] survivors
+  DevBuf<float> desc;          // [cap * 128]
+  unsigned* hcnt = nullptr;    // pinned copy of cnt
+  int cap = 1 << 16;
+};
+
 struct SiftWork {
   int L = 3;
   double contrast = 0.04, edge = 10.0, sigma = 1.6;
@@ -1068,108 +1085,122 @@ struct SiftWork {
   DevBuf<float> kern;          // [kMaxLayers][kMaxTaps]
   DevBuf<int> rad;             // [kMaxLayers]
   bool kern_ok = false;
-  Pyr P{};
-  DevBuf<uint8_t> gray;
-  DevBuf<float> gauss, dogs, tmp, up;
-  DevBuf<int4> cand;
-  DevBuf<Surv> surv;
-  DevBuf<Kp> kps, sorted;
-  DevBuf<unsigned> dup, before;
-  DevBuf<unsigned> cnt;        // [0] candidates, [1] raw keypoints, [2] final, [3] survivors
-  DevBuf<float> desc;          // [n * 128]
-  int cap = 1 << 16;
-  int64_t n = 0;               // final keypoints of the last image
+  std::vector<SiftSlot*> slots;
+  // results of the last detect / batch, concatenated in image order
+  DevBuf<Kp> all_kp;
+  DevBuf<float> all_desc;
+  std::vector<int64_t> off{0};
+  std::vector<int32_t> shapes;   // (h, w) per image
   bool valid = false;
 };
 
-void sod_sift_free(sod_ctx* ctx) {
-  SiftWork* S = ctx->sift;
-  if (!S) return;
-  sod_release(S->kern);
-  sod_release(S->rad);
+static void free_slot(SiftSlot* S) {
+  if (S->stream) (void)hipStreamSynchronize(S->stream);
   sod_release(S->gray);
+  sod_release(S->bgr);
   sod_release(S->gauss);
   sod_release(S->dogs);
   sod_release(S->tmp);
   sod_release(S->up);
   sod_release(S->cand);
+  sod_release(S->surv);
   sod_release(S->kps);
   sod_release(S->sorted);
-  sod_release(S->surv);
   sod_release(S->dup);
   sod_release(S->before);
   sod_release(S->cnt);
   sod_release(S->desc);
+  if (S->hcnt) (void)hipHostFree(S->hcnt);
+  if (S->stream) (void)hipStreamDestroy(S->stream);
   delete S;
+}
+
+void sod_sift_free(sod_ctx* ctx) {
+  SiftWork* W = ctx->sift;
+  if (!W) return;
+  for (SiftSlot* S : W->slots) free_slot(S);
+  sod_release(W->kern);
+  sod_release(W->rad);
+  sod_release(W->all_kp);
+  sod_release(W->all_desc);
+  delete W;
   ctx->sift = nullptr;
 }
 
 namespace {
+
+constexpr int kSlots = 4;   // images in flight in a batch
 
 SiftWork* work(sod_ctx* ctx) {
   if (!ctx->sift) ctx->sift = new SiftWork();
   return ctx->sift;
 }
 
-int set_kernels(sod_ctx* ctx, SiftWork& S) {
-  if (S.kern_ok) return SOD_OK;
+int get_slot(sod_ctx* ctx, SiftWork& W, int i, SiftSlot** out) {
+  while ((int)W.slots.size() <= i) {
+    SiftSlot* S = new SiftSlot();
+    W.slots.push_back(S);
+    SOD_HIP(ctx, hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking));
+    SOD_HIP(ctx, hipHostMalloc((void**)&S->hcnt, 16, hipHostMallocDefault));
+  }
+  *out = W.slots[(size_t)i];
+  return SOD_OK;
+}
+
+int set_kernels(sod_ctx* ctx, SiftWork& W) {
+  if (W.kern_ok) return SOD_OK;
   // sig[0] = the base blur sqrt(max(sigma^2 - 4 * 0.5^2, 0.01)) in float (createInitialImage);
   // sig[i] as buildGaussianPyramid (double)
   double sig[kMaxLayers];
-  const float s = (float)S.sigma;
+  const float s = (float)W.sigma;
   sig[0] = (double)std::sqrt(std::max(s * s - 0.5f * 0.5f * 4, 0.01f));
-  const double k = std::pow(2., 1. / S.L);
-  for (int i = 1; i < S.L + 3; i++) {
-    const double sig_prev = std::pow(k, (double)(i - 1)) * S.sigma;
+  const double k = std::pow(2., 1. / W.L);
+  for (int i = 1; i < W.L + 3; i++) {
+    const double sig_prev = std::pow(k, (double)(i - 1)) * W.sigma;
     const double sig_total = sig_prev * k;
     sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
   }
   std::vector<float> h((size_t)kMaxLayers * kMaxTaps, 0.f);
-  for (int i = 0; i < S.L + 3; i++) {
-    S.radius[i] = gauss_kernel(sig[i], h.data() + (size_t)i * kMaxTaps);
-    if (S.radius[i] < 0) return sod_fail(ctx, SOD_EINVAL, "sigma too large for the blur kernel");
+  for (int i = 0; i < W.L + 3; i++) {
+    W.radius[i] = gauss_kernel(sig[i], h.data() + (size_t)i * kMaxTaps);
+    if (W.radius[i] < 0) return sod_fail(ctx, SOD_EINVAL, "sigma too large for the blur kernel");
   }
-  SOD_TRY(sod_reserve(ctx, S.kern, h.size()));
-  SOD_TRY(sod_reserve(ctx, S.rad, (size_t)kMaxLayers));
-  SOD_HIP(ctx, hipMemcpyAsync(S.kern.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  SOD_HIP(ctx, hipMemcpyAsync(S.rad.p, S.radius, sizeof(S.radius), hipMemcpyHostToDevice, ctx->stream));
+  SOD_TRY(sod_reserve(ctx, W.kern, h.size()));
+  SOD_TRY(sod_reserve(ctx, W.rad, (size_t)kMaxLayers));
+  SOD_HIP(ctx, hipMemcpyAsync(W.kern.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(W.rad.p, W.radius, sizeof(W.radius), hipMemcpyHostToDevice, ctx->stream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  S.kern_ok = true;
+  W.kern_ok = true;
   return SOD_OK;
 }
 
-int blur(sod_ctx* ctx, SiftWork& S, const float* src, float* dst, int w, int h, int layer,
-         const float* prev, float* dog) {
-  const float* k = S.kern.p + (size_t)layer * kMaxTaps;
-  const int r = S.radius[layer];
+int blur(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, const float* src, float* dst, int w, int h,
+         int layer, const float* prev, float* dog) {
+  const float* k = W.kern.p + (size_t)layer * kMaxTaps;
+  const int r = W.radius[layer];
   if (r >= 1 && r <= kMaxR) {
     dim3 gt((unsigned)((w + kTW - 1) / kTW), (unsigned)((h + kTH - 1) / kTH));
-    hipLaunchKernelGGL(kBlurFns[r], gt, dim3(256), 0, ctx->stream, src, dst, w, h, k, dog);
+    hipLaunchKernelGGL(kBlurFns[r], gt, dim3(256), 0, S.stream, src, dst, w, h, k, dog);
     return SOD_OK;
   }
   dim3 g((unsigned)((w + 255) / 256), (unsigned)h);
-  hipLaunchKernelGGL(blur_rows_kernel, g, dim3(256), 0, ctx->stream, src, S.tmp.p, w, k, r);
-  hipLaunchKernelGGL(blur_cols_kernel, g, dim3(256), 0, ctx->stream, S.tmp.p, dst, w, h, k, r,
-                     prev, dog);
+  hipLaunchKernelGGL(blur_rows_kernel, g, dim3(256), 0, S.stream, src, S.tmp.p, w, k, r);
+  hipLaunchKernelGGL(blur_cols_kernel, g, dim3(256), 0, S.stream, S.tmp.p, dst, w, h, k, r, prev,
+                     dog);
   return SOD_OK;
 }
 
 constexpr int kOrientGrid = 4096, kRankGrid = 2048, kDescGrid = 4096;
 
-// detect + describe one image already in S.gray: every stage is enqueued back to back
-// (grids sized by capacity, counts read on the device); one host sync at the end reads
-// the counts.  An overflow of the candidate / keypoint lists grows them and re-runs
-// (the result does not depend on discovery order).
-int run_image(sod_ctx* ctx, SiftWork& S, int w, int h) {
-  SOD_TRY(set_kernels(ctx, S));
-  const int L = S.L;
-  Pyr& P = S.P;
+// geometry of the pyramid of a w x h image (OpenCV: nOctaves = cvRound(log2(min(2w, 2h)) - 2)
+// - firstOctave); returns the Gaussian / DoG element counts
+void plan_pyramid(int L, int w, int h, Pyr& P, int64_t& go, int64_t& dof, int& o_small) {
   P.L = L;
   const int bw = 2 * w, bh = 2 * h;
   int nOct = (int)std::lrint(std::log((double)std::min(bw, bh)) / std::log(2.) - 2) - kFirstOctave;
   nOct = std::max(1, std::min(nOct, kMaxOct));
   P.n = nOct;
-  int64_t go = 0, dof = 0;
+  go = dof = 0;
   int ow = bw, oh = bh;
   for (int o = 0; o < nOct; ++o) {
     P.o[o] = Oct{ow, oh, go, dof};
@@ -1182,86 +1213,174 @@ int run_image(sod_ctx* ctx, SiftWork& S, int w, int h) {
       break;
     }
   }
-  int o_small = nOct;   // first octave handled by small_octaves_kernel
+  o_small = nOct;   // first octave handled by small_octaves_kernel
   for (int o = 1; o < nOct && L + 2 <= kChainDog; ++o)
     if ((int64_t)P.o[o].w * P.o[o].h <= kChainPixels) {
       o_small = o;
       break;
     }
+}
+
+// enqueue detect + describe of the image in S.gray on S.stream (no host sync); the counts
+// land in S.hcnt.  `pyramid` false re-runs only the stages after it (list overflow).
+int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, bool pyramid) {
+  const int L = W.L;
+  Pyr& P = S.P;
+  int64_t go, dof;
+  int o_small;
+  plan_pyramid(L, w, h, P, go, dof, o_small);
+  const int nOct = P.n, bw = 2 * w, bh = 2 * h;
   SOD_TRY(sod_reserve(ctx, S.gauss, (size_t)go));
   SOD_TRY(sod_reserve(ctx, S.dogs, (size_t)dof));
   SOD_TRY(sod_reserve(ctx, S.tmp, (size_t)bw * bh));
   SOD_TRY(sod_reserve(ctx, S.up, (size_t)bw * bh));
   SOD_TRY(sod_reserve(ctx, S.cnt, 4));
-  const float thr = (float)(int)std::floor(0.5 * S.contrast / L * 255 * 1);
-
-  for (int attempt = 0; attempt < 4; ++attempt) {
-    const int cap = S.cap;
-    SOD_TRY(sod_reserve(ctx, S.cand, (size_t)cap));
-    SOD_TRY(sod_reserve(ctx, S.surv, (size_t)cap));
-    SOD_TRY(sod_reserve(ctx, S.kps, (size_t)cap));
-    SOD_TRY(sod_reserve(ctx, S.sorted, (size_t)cap));
-    SOD_TRY(sod_reserve(ctx, S.dup, (size_t)cap));
-    SOD_TRY(sod_reserve(ctx, S.before, (size_t)cap));
-    SOD_HIP(ctx, hipMemsetAsync(S.cnt.p, 0, 16, ctx->stream));
-    if (attempt == 0) {   // the pyramid (and the small octaves' extrema)
-      hipLaunchKernelGGL(upscale_kernel, dim3((unsigned)((bw + 255) / 256), (unsigned)bh), dim3(256),
-                         0, ctx->stream, S.gray.p, w, h, S.up.p);
-      for (int o = 0; o < o_small; ++o) {
-        const Oct& q = P.o[o];
-        const size_t plane = (size_t)q.w * q.h;
-        float* g0 = S.gauss.p + q.g;
-        if (o == 0) {
-          SOD_TRY(blur(ctx, S, S.up.p, g0, q.w, q.h, 0, nullptr, nullptr));
-        } else {
-          const Oct& pq = P.o[o - 1];
-          hipLaunchKernelGGL(down2_kernel, dim3((unsigned)((q.w + 255) / 256), (unsigned)q.h),
-                             dim3(256), 0, ctx->stream, S.gauss.p + pq.g + (size_t)pq.w * pq.h * L,
-                             pq.w, g0, q.w);
-        }
-        for (int i = 1; i < L + 3; ++i)
-          SOD_TRY(blur(ctx, S, g0 + plane * (i - 1), g0 + plane * i, q.w, q.h, i,
-                       g0 + plane * (i - 1), S.dogs.p + q.d + plane * (i - 1)));
-      }
-    }
+  const int cap = S.cap;
+  SOD_TRY(sod_reserve(ctx, S.cand, (size_t)cap));
+  SOD_TRY(sod_reserve(ctx, S.surv, (size_t)cap));
+  SOD_TRY(sod_reserve(ctx, S.kps, (size_t)cap));
+  SOD_TRY(sod_reserve(ctx, S.sorted, (size_t)cap));
+  SOD_TRY(sod_reserve(ctx, S.dup, (size_t)cap));
+  SOD_TRY(sod_reserve(ctx, S.before, (size_t)cap));
+  SOD_TRY(sod_reserve(ctx, S.desc, (size_t)cap * 128));
+  const float thr = (float)(int)std::floor(0.5 * W.contrast / L * 255 * 1);
+  hipStream_t st = S.stream;
+  SOD_HIP(ctx, hipMemsetAsync(S.cnt.p, 0, 16, st));
+  if (pyramid) {
+    hipLaunchKernelGGL(upscale_kernel, dim3((unsigned)((bw + 255) / 256), (unsigned)bh), dim3(256), 0,
+                       st, S.gray.p, w, h, S.up.p);
     for (int o = 0; o < o_small; ++o) {
       const Oct& q = P.o[o];
-      if (q.w <= 2 * kBorder || q.h <= 2 * kBorder) continue;
-      dim3 g((unsigned)((q.w - 2 * kBorder + 255) / 256), (unsigned)(q.h - 2 * kBorder), (unsigned)L);
-      hipLaunchKernelGGL(extrema_kernel, g, dim3(256), 0, ctx->stream, S.dogs.p, P, o, thr, S.cand.p,
-                         S.cnt.p, cap);
+      const size_t plane = (size_t)q.w * q.h;
+      float* g0 = S.gauss.p + q.g;
+      if (o == 0) {
+        SOD_TRY(blur(ctx, W, S, S.up.p, g0, q.w, q.h, 0, nullptr, nullptr));
+      } else {
+        const Oct& pq = P.o[o - 1];
+        hipLaunchKernelGGL(down2_kernel, dim3((unsigned)((q.w + 255) / 256), (unsigned)q.h), dim3(256),
+                           0, st, S.gauss.p + pq.g + (size_t)pq.w * pq.h * L, pq.w, g0, q.w);
+      }
+      for (int i = 1; i < L + 3; ++i)
+        SOD_TRY(blur(ctx, W, S, g0 + plane * (i - 1), g0 + plane * i, q.w, q.h, i, g0 + plane * (i - 1),
+                     S.dogs.p + q.d + plane * (i - 1)));
     }
-    if (o_small < nOct)   // re-running it re-blurs the small octaves identically
-      hipLaunchKernelGGL(small_octaves_kernel, dim3(1), dim3(1024), 0, ctx->stream, S.gauss.p,
-                         S.dogs.p, P, o_small, S.kern.p, S.rad.p, thr, S.cand.p, S.cnt.p, cap);
-    hipLaunchKernelGGL(refine_kernel, dim3((unsigned)((cap + 127) / 128)), dim3(128), 0, ctx->stream,
-                       S.dogs.p, P, S.cand.p, S.cnt.p, cap, (float)S.contrast, (float)S.edge,
-                       (float)S.sigma, S.surv.p, S.cnt.p + 3);
-    hipLaunchKernelGGL(orient_kernel, dim3(kOrientGrid), dim3(kOT), 0, ctx->stream, S.gauss.p, P,
-                       S.surv.p, S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap);
-    SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)cap * 4, ctx->stream));
-    SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)cap * 4, ctx->stream));
-    for (int pass = 0; pass < 2; ++pass)
-      hipLaunchKernelGGL(rank_kernel, dim3(kRankGrid), dim3(kRankTile), 0, ctx->stream, S.kps.p,
-                         S.cnt.p + 1, cap, pass, S.dup.p, S.before.p);
-    hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, ctx->stream,
-                       S.kps.p, S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2);
-    SOD_TRY(sod_reserve(ctx, S.desc, (size_t)cap * 128));
-    hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, ctx->stream, S.gauss.p, P,
-                       S.sorted.p, S.cnt.p + 2, S.desc.p);
-    SOD_HIP(ctx, hipGetLastError());
-    unsigned c[4];
-    SOD_HIP(ctx, hipMemcpyAsync(c, S.cnt.p, 16, hipMemcpyDeviceToHost, ctx->stream));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (c[0] > (unsigned)cap || c[1] > (unsigned)cap) {
-      S.cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)std::max(c[0], c[1]));
-      continue;
-    }
-    S.n = c[2];
-    S.valid = true;
-    return SOD_OK;
   }
-  return sod_fail(ctx, SOD_ENOMEM, "SIFT: candidate list did not fit after growing");
+  for (int o = 0; o < o_small; ++o) {
+    const Oct& q = P.o[o];
+    if (q.w <= 2 * kBorder || q.h <= 2 * kBorder) continue;
+    dim3 g((unsigned)((q.w - 2 * kBorder + 255) / 256), (unsigned)(q.h - 2 * kBorder), (unsigned)L);
+    hipLaunchKernelGGL(extrema_kernel, g, dim3(256), 0, st, S.dogs.p, P, o, thr, S.cand.p, S.cnt.p, cap);
+  }
+  if (o_small < nOct)   // re-running it re-blurs the small octaves identically
+    hipLaunchKernelGGL(small_octaves_kernel, dim3(1), dim3(1024), 0, st, S.gauss.p, S.dogs.p, P,
+                       o_small, W.kern.p, W.rad.p, thr, S.cand.p, S.cnt.p, cap);
+  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)((cap + 127) / 128)), dim3(128), 0, st, S.dogs.p, P,
+                     S.cand.p, S.cnt.p, cap, (float)W.contrast, (float)W.edge, (float)W.sigma, S.surv.p,
+                     S.cnt.p + 3);
+  hipLaunchKernelGGL(orient_kernel, dim3(kOrientGrid), dim3(kOT), 0, st, S.gauss.p, P, S.surv.p,
+                     S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap);
+  SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)cap * 4, st));
+  SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)cap * 4, st));
+  for (int pass = 0; pass < 2; ++pass)
+    hipLaunchKernelGGL(rank_kernel, dim3(kRankGrid), dim3(kRankTile), 0, st, S.kps.p, S.cnt.p + 1, cap,
+                       pass, S.dup.p, S.before.p);
+  hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, S.kps.p,
+                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2);
+  hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, P, S.sorted.p,
+                     S.cnt.p + 2, S.desc.p);
+  SOD_HIP(ctx, hipGetLastError());
+  SOD_HIP(ctx, hipMemcpyAsync(S.hcnt, S.cnt.p, 16, hipMemcpyDeviceToHost, st));
+  return SOD_OK;
+}
+
+// upload one image (8-bit gray, or BGR converted on the device) into S.gray
+int slot_upload(sod_ctx* ctx, SiftSlot& S, const uint8_t* img, int w, int h, int channels) {
+  const size_t np = (size_t)w * h;
+  SOD_TRY(sod_reserve(ctx, S.gray, np));
+  if (channels == 1) {
+    SOD_HIP(ctx, hipMemcpyAsync(S.gray.p, img, np, hipMemcpyHostToDevice, S.stream));
+  } else {
+    SOD_TRY(sod_reserve(ctx, S.bgr, np * 3));
+    SOD_HIP(ctx, hipMemcpyAsync(S.bgr.p, img, np * 3, hipMemcpyHostToDevice, S.stream));
+    hipLaunchKernelGGL(bgr2gray_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, S.stream,
+                       S.bgr.p, (int64_t)np, S.gray.p);
+  }
+  return SOD_OK;
+}
+
+int grow_results(sod_ctx* ctx, SiftWork& W, int64_t need) {
+  if ((int64_t)W.all_kp.n >= need && (int64_t)W.all_desc.n >= need * 128) return SOD_OK;
+  const int64_t have = W.off.back();
+  const int64_t n = std::max<int64_t>(need, 2 * (int64_t)W.all_kp.n);
+  DevBuf<Kp> nk;
+  DevBuf<float> nd;
+  SOD_TRY(sod_reserve(ctx, nk, (size_t)n));
+  SOD_TRY(sod_reserve(ctx, nd, (size_t)n * 128));
+  for (SiftSlot* S : W.slots) SOD_HIP(ctx, hipStreamSynchronize(S->stream));
+  if (have > 0) {
+    SOD_HIP(ctx, hipMemcpy(nk.p, W.all_kp.p, (size_t)have * sizeof(Kp), hipMemcpyDeviceToDevice));
+    SOD_HIP(ctx, hipMemcpy(nd.p, W.all_desc.p, (size_t)have * 512, hipMemcpyDeviceToDevice));
+  }
+  sod_release(W.all_kp);
+  sod_release(W.all_desc);
+  W.all_kp = nk;
+  W.all_desc = nd;
+  return SOD_OK;
+}
+
+// detect + describe n images, kSlots in flight on their own streams; the results are
+// appended to W.all_kp / W.all_desc in image order (W.off = prefix counts)
+int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws, const int32_t* hs,
+              const int32_t* chans, int32_t* counts) {
+  SiftWork& W = *work(ctx);
+  W.valid = false;
+  for (int i = 0; i < n; ++i)
+    if (!imgs[i] || ws[i] < 1 || hs[i] < 1 || (int64_t)ws[i] * hs[i] > (1LL << 28) ||
+        (chans && chans[i] != 1 && chans[i] != 3))
+      return sod_fail(ctx, SOD_EINVAL, "bad image arguments (image " + std::to_string(i) + ")");
+  SOD_TRY(set_kernels(ctx, W));
+  W.off.assign(1, 0);
+  W.shapes.clear();
+  const int K = std::min(n, kSlots);
+  for (int i0 = 0; i0 < n; i0 += K) {
+    const int m = std::min(K, n - i0);
+    for (int j = 0; j < m; ++j) {
+      SiftSlot* S;
+      SOD_TRY(get_slot(ctx, W, j, &S));
+      const int i = i0 + j;
+      SOD_TRY(slot_upload(ctx, *S, imgs[i], ws[i], hs[i], chans ? chans[i] : 1));
+      SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], true));
+    }
+    for (int j = 0; j < m; ++j) {
+      SiftSlot* S = W.slots[(size_t)j];
+      const int i = i0 + j;
+      for (int attempt = 0;; ++attempt) {
+        SOD_HIP(ctx, hipStreamSynchronize(S->stream));
+        const unsigned c0 = S->hcnt[0], c1 = S->hcnt[1];
+        if (c0 <= (unsigned)S->cap && c1 <= (unsigned)S->cap) break;
+        if (attempt >= 3) return sod_fail(ctx, SOD_ENOMEM, "SIFT: candidate list did not fit after growing");
+        // grow and redo after the pyramid (the result does not depend on discovery order)
+        S->cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)std::max(c0, c1));
+        SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], false));
+      }
+      const int64_t cnt = S->hcnt[2];
+      const int64_t at = W.off.back();
+      SOD_TRY(grow_results(ctx, W, at + cnt));
+      if (cnt > 0) {
+        SOD_HIP(ctx, hipMemcpyAsync(W.all_kp.p + at, S->sorted.p, (size_t)cnt * sizeof(Kp),
+                                    hipMemcpyDeviceToDevice, S->stream));
+        SOD_HIP(ctx, hipMemcpyAsync(W.all_desc.p + at * 128, S->desc.p, (size_t)cnt * 512,
+                                    hipMemcpyDeviceToDevice, S->stream));
+      }
+      W.off.push_back(at + cnt);
+      W.shapes.push_back(hs[i]);
+      W.shapes.push_back(ws[i]);
+      if (counts) counts[i] = (int32_t)cnt;
+    }
+  }
+  for (int j = 0; j < K; ++j) SOD_HIP(ctx, hipStreamSynchronize(W.slots[(size_t)j]->stream));
+  W.valid = true;
+  return SOD_OK;
 }
 
 }  // namespace
@@ -1275,16 +1394,16 @@ int sod_sift_set_params(sod_ctx* ctx, int32_t n_octave_layers, double contrast_t
   if (n_octave_layers < 1 || n_octave_layers + 3 > kMaxLayers || !(sigma > 0) ||
       !(contrast_threshold >= 0) || !(edge_threshold > 0))
     return sod_fail(ctx, SOD_EINVAL, "SIFT parameters out of range");
-  SiftWork& S = *work(ctx);
-  if (S.L == n_octave_layers && S.contrast == contrast_threshold && S.edge == edge_threshold &&
-      S.sigma == sigma)
+  SiftWork& W = *work(ctx);
+  if (W.L == n_octave_layers && W.contrast == contrast_threshold && W.edge == edge_threshold &&
+      W.sigma == sigma)
     return SOD_OK;
-  S.L = n_octave_layers;
-  S.contrast = contrast_threshold;
-  S.edge = edge_threshold;
-  S.sigma = sigma;
-  S.kern_ok = false;
-  S.valid = false;
+  W.L = n_octave_layers;
+  W.contrast = contrast_threshold;
+  W.edge = edge_threshold;
+  W.sigma = sigma;
+  W.kern_ok = false;
+  W.valid = false;
   return SOD_OK;
 }
 
@@ -1292,51 +1411,44 @@ int sod_sift_detect(sod_ctx* ctx, const uint8_t* gray, int32_t width, int32_t he
                     int32_t* n_keypoints) {
   if (!ctx) return SOD_EINVAL;
   SOD_HIP(ctx, hipSetDevice(ctx->device));
-  if (!gray || !n_keypoints || width < 1 || height < 1 || (int64_t)width * height > (1LL << 28))
-    return sod_fail(ctx, SOD_EINVAL, "bad image arguments");
-  SiftWork& S = *work(ctx);
-  S.valid = false;
-  SOD_TRY(sod_reserve(ctx, S.gray, (size_t)width * height));
-  SOD_HIP(ctx, hipMemcpyAsync(S.gray.p, gray, (size_t)width * height, hipMemcpyHostToDevice, ctx->stream));
-  SOD_TRY(run_image(ctx, S, width, height));
-  *n_keypoints = (int32_t)S.n;
-  return SOD_OK;
+  if (!n_keypoints) return sod_fail(ctx, SOD_EINVAL, "null output");
+  const uint8_t* imgs[1] = {gray};
+  const int32_t one = 1;
+  return run_batch(ctx, 1, imgs, &width, &height, &one, n_keypoints);
 }
 
 int sod_sift_detect_bgr(sod_ctx* ctx, const uint8_t* bgr, int32_t width, int32_t height,
                         int32_t* n_keypoints) {
   if (!ctx) return SOD_EINVAL;
   SOD_HIP(ctx, hipSetDevice(ctx->device));
-  if (!bgr || !n_keypoints || width < 1 || height < 1 || (int64_t)width * height > (1LL << 28))
-    return sod_fail(ctx, SOD_EINVAL, "bad image arguments");
-  SiftWork& S = *work(ctx);
-  S.valid = false;
-  const int64_t npix = (int64_t)width * height;
-  SOD_TRY(sod_reserve(ctx, S.gray, (size_t)npix));
-  SOD_TRY(sod_reserve(ctx, ctx->stage_u8, (size_t)npix * 3));
-  SOD_HIP(ctx, hipMemcpyAsync(ctx->stage_u8.p, bgr, (size_t)npix * 3, hipMemcpyHostToDevice, ctx->stream));
-  hipLaunchKernelGGL(bgr2gray_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, ctx->stream,
-                     ctx->stage_u8.p, npix, S.gray.p);
-  SOD_TRY(run_image(ctx, S, width, height));
-  *n_keypoints = (int32_t)S.n;
-  return SOD_OK;
+  if (!n_keypoints) return sod_fail(ctx, SOD_EINVAL, "null output");
+  const uint8_t* imgs[1] = {bgr};
+  const int32_t three = 3;
+  return run_batch(ctx, 1, imgs, &width, &height, &three, n_keypoints);
 }
 
-int sod_sift_get(sod_ctx* ctx, int32_t cap, float* x, float* y, float* size, float* angle,
+int sod_sift_detect_batch(sod_ctx* ctx, int32_t n_images, const uint8_t* const* images,
+                          const int32_t* widths, const int32_t* heights, const int32_t* channels,
+                          int32_t* counts) {
+  if (!ctx) return SOD_EINVAL;
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  if (n_images < 1 || !images || !widths || !heights)
+    return sod_fail(ctx, SOD_EINVAL, "bad batch arguments");
+  return run_batch(ctx, n_images, images, widths, heights, channels, counts);
+}
+
+int sod_sift_get(sod_ctx* ctx, int64_t cap, float* x, float* y, float* size, float* angle,
                  float* response, int32_t* octave, float* descriptors) {
   if (!ctx) return SOD_EINVAL;
   SOD_HIP(ctx, hipSetDevice(ctx->device));
-  SiftWork* S = ctx->sift;
-  if (!S || !S->valid) return sod_fail(ctx, SOD_ESTATE, "no SIFT result: call sod_sift_detect first");
-  const int64_t n = std::min<int64_t>(S->n, std::max(cap, 0));
+  SiftWork* W = ctx->sift;
+  if (!W || !W->valid) return sod_fail(ctx, SOD_ESTATE, "no SIFT result: call sod_sift_detect first");
+  const int64_t n = std::min<int64_t>(W->off.back(), std::max<int64_t>(cap, 0));
   if (n > 0) {
     std::vector<Kp> h((size_t)n);
-    SOD_HIP(ctx, hipMemcpyAsync(h.data(), S->sorted.p, (size_t)n * sizeof(Kp), hipMemcpyDeviceToHost,
-                                ctx->stream));
+    SOD_HIP(ctx, hipMemcpy(h.data(), W->all_kp.p, (size_t)n * sizeof(Kp), hipMemcpyDeviceToHost));
     if (descriptors)
-      SOD_HIP(ctx, hipMemcpyAsync(descriptors, S->desc.p, (size_t)n * 128 * 4, hipMemcpyDeviceToHost,
-                                  ctx->stream));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      SOD_HIP(ctx, hipMemcpy(descriptors, W->all_desc.p, (size_t)n * 512, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; ++i) {
       const Kp& k = h[(size_t)i];
       if (x) x[i] = k.x;
@@ -1350,31 +1462,44 @@ int sod_sift_get(sod_ctx* ctx, int32_t cap, float* x, float* y, float* size, flo
   return SOD_OK;
 }
 
-// the detected keypoints become the query set of the matcher / Hough stages, without a
-// host round trip (descriptors are packed from device memory)
+// the last detection (one image or a batch) becomes the query set of the matcher / Hough
+// stages, without a host round trip (descriptors are packed from device memory); a batch
+// is declared as query images (sod_query_images) for the fused per-image stages
 int sod_sift_to_queries(sod_ctx* ctx) {
   if (!ctx) return SOD_EINVAL;
   SOD_HIP(ctx, hipSetDevice(ctx->device));
-  SiftWork* S = ctx->sift;
-  if (!S || !S->valid) return sod_fail(ctx, SOD_ESTATE, "no SIFT result: call sod_sift_detect first");
-  if (S->n < 1) return sod_fail(ctx, SOD_ESTATE, "the image has no SIFT keypoints");
-  const int32_t nq = (int32_t)S->n;
+  SiftWork* W = ctx->sift;
+  if (!W || !W->valid) return sod_fail(ctx, SOD_ESTATE, "no SIFT result: call sod_sift_detect first");
+  const int64_t nq64 = W->off.back();
+  if (nq64 < 1) return sod_fail(ctx, SOD_ESTATE, "the image(s) have no SIFT keypoints");
+  if (nq64 > (1 << 27)) return sod_fail(ctx, SOD_EINVAL, "query count out of range");
+  const int32_t nq = (int32_t)nq64;
   SOD_TRY(sod_reserve(ctx, ctx->flags, 4));
   SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p, 0, 12, ctx->stream));
-  SOD_TRY(ctx->impl != 0 ? launch_pack_i8(ctx, S->desc.p, SOD_DTYPE_F32, nq, false)
-                         : launch_pack_queries(ctx, S->desc.p, SOD_DTYPE_F32, nq));
+  SOD_TRY(ctx->impl != 0 ? launch_pack_i8(ctx, W->all_desc.p, SOD_DTYPE_F32, nq, false)
+                         : launch_pack_queries(ctx, W->all_desc.p, SOD_DTYPE_F32, nq));
   SOD_TRY(sod_reserve(ctx, ctx->qx, (size_t)nq));
   SOD_TRY(sod_reserve(ctx, ctx->qy, (size_t)nq));
   SOD_TRY(sod_reserve(ctx, ctx->qang, (size_t)nq));
   SOD_TRY(sod_reserve(ctx, ctx->qoct, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->scal, 4));
+  // the final count as a device scalar for unpack_kp_kernel
+  const unsigned un = (unsigned)nq;
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->scal.p + 3, &un, 4, hipMemcpyHostToDevice, ctx->stream));
   hipLaunchKernelGGL(unpack_kp_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ctx->stream,
-                     S->sorted.p, S->cnt.p + 2, ctx->qx.p, ctx->qy.p, ctx->qang.p, ctx->qoct.p);
+                     W->all_kp.p, ctx->scal.p + 3, ctx->qx.p, ctx->qy.p, ctx->qang.p, ctx->qoct.p);
   SOD_HIP(ctx, hipGetLastError());
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->nq = nq;
   ctx->win0 = 0;
   ctx->winn = -1;
   ctx->n_qimg = 0;
   ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  const int nimg = (int)W->shapes.size() / 2;
+  if (nimg > 1) {
+    std::vector<int32_t> off(W->off.begin(), W->off.end());
+    SOD_TRY(sod_query_images(ctx, nimg, off.data(), W->shapes.data()));
+  }
   return SOD_OK;
 }
 

@@ -178,8 +178,8 @@ class SiftDatabase:
         from .sift import SIFT_create
         sift = sift or SIFT_create()
         xs, ys, angs, octs, imgs, dess, cents, sizes = [], [], [], [], [], [], [], []
-        for i, img in enumerate(images):
-            r = sift.detect_arrays(np.asarray(img))
+        images = [np.asarray(im) for im in images]
+        for i, (img, r) in enumerate(zip(images, sift.detect_batch(images))):
             n = len(r["x"])
             if n == 0:
                 raise ValueError("training image %d has no SIFT keypoints" % i)

@@ -59,6 +59,12 @@ class SIFT:
         r = self._ctx.sift_detect(image, descriptors=descriptors)
         return _retain_best(r, self.nfeatures)
 
+    def detect_batch(self, images, descriptors=True):
+        """detect_arrays of several images (four in flight on the device)."""
+        self._ctx.sift_params(*self._params)
+        return [_retain_best(r, self.nfeatures)
+                for r in self._ctx.sift_detect_batch(images, descriptors=descriptors)]
+
     def detectAndCompute(self, image, mask, descriptors=None,   # noqa: N802
                          useProvidedKeypoints=False):           # noqa: N803
         if mask is not None:

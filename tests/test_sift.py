@@ -240,3 +240,50 @@ def test_image_to_pose_end_to_end(ctx):
     # the pose centroid of the best cluster lies inside the pasted object
     xs, ys = fp[:, 0], fp[:, 1]
     assert np.any((xs > 200) & (xs < 500) & (ys > 100) & (ys < 340))
+
+
+@pytest.mark.gpu
+def test_sift_batch_equals_single(ctx):
+    """Six images of four shapes, gray and BGR (two rounds of four streams): each image's
+    result equals the oracle's."""
+    rng = np.random.default_rng(50)
+    imgs = [synthetic.textured_image(h, w, seed=51 + i)
+            for i, (h, w) in enumerate([(200, 260), (240, 320), (97, 131), (200, 260), (64, 64),
+                                        (300, 220)])]
+    bgr = np.stack([imgs[1], imgs[1] // 2, 255 - imgs[1]], -1).astype(np.uint8)
+    batch = [imgs[0], bgr, imgs[2], imgs[3], imgs[4], imgs[5]]
+    out = ctx.sift_detect_batch(batch)
+    for i, (img, dev) in enumerate(zip(batch, out)):
+        g = osift.bgr2gray(img) if img.ndim == 3 else img
+        _assert_same(dev, osift.detect_and_compute(g), "batch %d" % i)
+    assert rng is not None
+
+
+@pytest.mark.gpu
+def test_sift_query_batch_equals_per_image(ctx):
+    """SURVEY 8(f) rows 3 + 4: three query images -> SIFT batch -> one matcher pass ->
+    fused stages equals each image run alone through Main.get_query_image."""
+    from sift_based_od_amd import Main, SiftDatabase, sift_query_batch
+    objs = [synthetic.textured_image(200, 260, seed=60 + i) for i in range(3)]
+    db = SiftDatabase.from_images(objs, dsift.SIFT_create(ctx=ctx))
+    queries = []
+    for i, (h, w, x0, y0) in enumerate([(400, 500, 100, 60), (360, 640, 300, 120),
+                                        (300, 300, 20, 40)]):
+        c = synthetic.textured_image(h, w, seed=70 + i, n_blobs=50)
+        c[y0:y0 + 200, x0:x0 + 260] = objs[i % 3]
+        queries.append(c)
+    ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
+    ctx.upload_db(db.des)
+    batch = sift_query_batch(ctx, queries, bins=15)
+    for i, q in enumerate(queries):
+        m = Main(ctx)
+        m.set_database(db)
+        m.get_query_image(q)
+        one = m.run(bins=15)
+        b = batch[i]
+        for k in ("idx1", "d1", "d2", "good"):
+            assert np.array_equal(b[k], one[k]), (i, k)
+        assert np.array_equal(b["valid"]["keys"], one["valid"]["keys"]), i
+        assert np.array_equal(b["affine"]["survived"], one["affine"]["survived"]), i
+        assert np.allclose(b["post"]["final_pose"], one["post"]["final_pose"]), i
+        assert len(one["post"]["final_pose"]) >= 1, i
