@@ -12,5 +12,5 @@ timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
   --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --comm host --config c3 \
   > gpurun_out/bench_c3_2rank_host.log 2>&1 || exit $?
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o c3 --output-format csv -- python3 bench.py --config c3 --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/prof_c3.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o c3 --output-format csv -- python3 bench.py --config c3 --steps 30 --warmup 5 --no-cpu-baseline --no-extras --contexts 1 > gpurun_out/prof_c3.log 2>&1 || exit $?
 exit $rc

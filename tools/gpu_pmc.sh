@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 run() {  # name, counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "$K" -d "$OUT/$name" -o pmc \
-    --output-format csv -- python3 bench.py --config "$CFG" --impl "$IMPL" --steps 2 --warmup 1 --no-cpu-baseline \
+    --output-format csv -- python3 bench.py --config "$CFG" --impl "$IMPL" --steps 2 --warmup 1 --no-cpu-baseline --no-extras --contexts 1 \
     > "$OUT/$name.log" 2>&1
 }
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU || exit $?
