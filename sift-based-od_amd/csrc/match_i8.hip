@@ -59,9 +59,13 @@ constexpr int SPS = SOD_I8_SPS;   // subtiles per stage (one barrier per stage)
 constexpr int kStageRows = SPS * 16;
 constexpr int kSub = 2048;     // bytes per 16-row subtile
 constexpr int kStageBytes = SPS * kSub;          // 16 KiB
-// per stage (128 rows) and wave w (rows 32w..32w+31): [c: 32 x i32 | p: 32 x i32]
+// per stage (128 rows) and wave w (its 128/NW16 rows): [c: i32 each | p: i32 each]
 constexpr int kStageNorm = 2 * SPS * kSubRows * 4;   // c and parity words
-constexpr int kStageSlot = kStageBytes + kStageNorm;
+// the norm words live in a ring of their own, one entry deeper than the descriptor ring:
+// the parity words of a stage are read only on the slow path of its LAST subtile, which
+// runs (software pipeline) after the next stage's barrier -- when that stage's refill
+// already targets the descriptor slot
+constexpr int kNormRing = 4;
 constexpr int kPiecesPerWave = kStageBytes / 1024 / NW16;   // 1 KiB LDS-DMA pieces
 constexpr int kPadNormI = 1 << 30;                        // ||d'||^2 of padding rows (w = -2^30)
 static_assert(kStageBytes / 1024 % NW16 == 0, "pieces split evenly");
@@ -156,23 +160,23 @@ __device__ __forceinline__ void issue_norms(const int* __restrict__ dn, int64_t 
 
 __device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
                                             const int* __restrict__ dn, int64_t npad, int64_t sub0,
-                                            uint8_t* slot, int wave, int lane) {
+                                            uint8_t* slot, uint8_t* norm_slot, int wave, int lane) {
   const uint8_t* src = dbpack + sub0 * kSub;
 #pragma unroll
   for (int j = 0; j < kPiecesPerWave; ++j) {
     const int piece = wave * kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  issue_norms<NW16, kStageRows>(dn, npad, sub0 * kSubRows, slot + kStageBytes, wave, lane);
+  issue_norms<NW16, kStageRows>(dn, npad, sub0 * kSubRows, norm_slot, wave, lane);
 }
 
-// LDS offset of a 16-row subtile's c for lane group g = lane >> 4 (its 4 rows 16u+4g..);
-// the parity words follow at +kParOff
+// offset (in a norm-ring entry) of a 16-row subtile's c for lane group g = lane >> 4 (its
+// 4 rows 16u+4g..); the parity words follow at +kParOff
 constexpr int kNormRows = kStageRows / NW16;
 constexpr int kParOff = 4 * kNormRows;
 __device__ __forceinline__ int norm_off(int u, int g) {
   const int row = 16 * u + 4 * g;
-  return kStageBytes + (row / kNormRows) * (8 * kNormRows) + (row % kNormRows) * 4;
+  return (row / kNormRows) * (8 * kNormRows) + (row % kNormRows) * 4;
 }
 
 // median of three (v_med3_i32): with y1 >= y2, med3(y1, y, y2) is the new second best
@@ -211,6 +215,9 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_EXP
 #define SOD_I8_EXP 0       // timing experiments only (wrong results): 1 no refill DMA,
 #endif                     // 2 no prefilter, 4 no stage wait/barrier
+#ifndef SOD_I8_LAZYP
+#define SOD_I8_LAZYP 1     // parity words read from LDS on the slow path only
+#endif
 #ifndef SOD_SHARED_T
 #define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
 #endif
@@ -235,11 +242,17 @@ __device__ __forceinline__ void top2_xor16(int& y1, int& y2) {
   y2 = max(max(min(a, b), (int)q[0]), (int)q[1]);
 }
 
+#if SOD_I8_LAZYP
+#define PARITY_T const uint8_t*   // LDS address of the lane's 4 parity words
+#else
+#define PARITY_T i32x4            // the parity words
+#endif
+
 // prefilter + exact top-2 update of one 16x16 tile set (see the file comment).  Each lane
 // keeps the exact top-2 (with index) of ITS rows; the prefilter threshold is the query's
 // second-best value over all four lane groups (lanes l, l^16, l^32, l^48), which every
 // row of the final top-2 reaches (>=, so ties keep their lowest-index winner).
-__device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 p, int rowb,
+__device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin, int rowb,
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
                                             int (&id)[QT]) {
   uint64_t hit[QT];
@@ -264,6 +277,11 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], const i32x4 
   if (__builtin_expect(any != 0, 0)) {   // slow path laid out away from the hot loop
 #else
   if (any) {
+#endif
+#if SOD_I8_LAZYP
+    const i32x4 p = *reinterpret_cast<const i32x4*>(pin);
+#else
+    const i32x4 p = pin;
 #endif
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
@@ -303,9 +321,12 @@ __device__ __forceinline__ void match_unit(
   const int64_t nst = (s_hi - s_lo) / SPS;
   const int64_t npad = nsub * kSubRows;
 
+  uint8_t* const nring = lds + kRing * kStageBytes;
 #pragma unroll
   for (int j = 0; j < kRing - 1; ++j)
-    if (j < nst) issue_stage(dbpack, dn, npad, s_lo + j * SPS, lds + j * kStageSlot, wave, lane);
+    if (j < nst)
+      issue_stage(dbpack, dn, npad, s_lo + j * SPS, lds + j * kStageBytes, nring + j * kStageNorm,
+                  wave, lane);
 
   i32x4 bq[QT][2];
 #pragma unroll
@@ -331,7 +352,11 @@ __device__ __forceinline__ void match_unit(
   i32x4 accp[QT];
 #pragma unroll
   for (int t = 0; t < QT; ++t) accp[t] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
+#if SOD_I8_LAZYP
+  const uint8_t* pp = nring;   // never read before it is set (accp cannot pass t2)
+#else
   i32x4 pp = {0, 0, 0, 0};
+#endif
   int rowp = 0;
 #endif
 
@@ -351,21 +376,30 @@ __device__ __forceinline__ void match_unit(
     // every wave has finished stage s-1, so its slot takes stage s+kRing-1
     if (!(SOD_I8_EXP & 1) && s + kRing - 1 < nst) {
       const int ns = slot == 0 ? kRing - 1 : slot - 1;
-      issue_stage(dbpack, dn, npad, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageSlot, wave, lane);
+      issue_stage(dbpack, dn, npad, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageBytes,
+                  nring + ((s + kRing - 1) % kNormRing) * kStageNorm, wave, lane);
     }
-    const uint8_t* sb = lds + slot * kStageSlot;
+    const uint8_t* sb = lds + slot * kStageBytes;
+    const uint8_t* nb0 = nring + (s % kNormRing) * kStageNorm + norm_off(0, lane >> 4);
     slot = slot + 1 == kRing ? 0 : slot + 1;
     i32x4 fa0 = *reinterpret_cast<const i32x4*>(sb + lane * 16);
     i32x4 fa1 = *reinterpret_cast<const i32x4*>(sb + 1024 + lane * 16);
-    i32x4 fc = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4));
-    i32x4 fp = *reinterpret_cast<const i32x4*>(sb + norm_off(0, lane >> 4) + kParOff);
+    i32x4 fc = *reinterpret_cast<const i32x4*>(nb0);
+#if !SOD_I8_LAZYP
+    i32x4 fp = *reinterpret_cast<const i32x4*>(nb0 + kParOff);
+#endif
 #if SOD_I8_UNROLL
 #pragma unroll SOD_I8_UNROLL
 #else
 #pragma unroll
 #endif
     for (int u = 0; u < SPS; ++u) {
-      const i32x4 a0 = fa0, a1 = fa1, c = fc, p = fp;   // c = floor(-||d'||^2 / 2)
+      const i32x4 a0 = fa0, a1 = fa1, c = fc;   // c = floor(-||d'||^2 / 2)
+#if SOD_I8_LAZYP
+      const uint8_t* p = nb0 + norm_off(u, 0) + kParOff;   // norm_off(u, g) = norm_off(u, 0) + 16 g
+#else
+      const i32x4 p = fp;
+#endif
       i32x4 acc[QT];
 #pragma unroll
       for (int t = 0; t < QT; ++t)
@@ -374,8 +408,10 @@ __device__ __forceinline__ void match_unit(
         const uint8_t* nb = sb + (u + 1) * kSub + lane * 16;
         fa0 = *reinterpret_cast<const i32x4*>(nb);
         fa1 = *reinterpret_cast<const i32x4*>(nb + 1024);
-        fc = *reinterpret_cast<const i32x4*>(sb + norm_off(u + 1, lane >> 4));
-        fp = *reinterpret_cast<const i32x4*>(sb + norm_off(u + 1, lane >> 4) + kParOff);
+        fc = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + 1, 0));
+#if !SOD_I8_LAZYP
+        fp = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + 1, 0) + kParOff);
+#endif
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t)
@@ -436,7 +472,7 @@ __global__ __launch_bounds__(NT16, 8 / NW16) void match_i8_kernel(
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2, int nqb) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageSlot];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageBytes + kNormRing * kStageNorm];
 #ifdef SOD_I8_STAMP
   unsigned long long t0 = 0, r0 = 0;
   if (threadIdx.x == 0) {
