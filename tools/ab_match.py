@@ -73,6 +73,15 @@ if hasattr(ctx._L, "sod_debug_stamps"):   # diagnostic build: in-kernel clock
     order = np.argsort(-dur)[:8]
     print("  slowest WGs (block, us, xcc, cu-slot):", [(int(b), int(dur[b]), int(xcc[b]),
                                                      int(place[b])) for b in order], flush=True)
+if hasattr(ctx._L, "sod_debug_counts"):   # diagnostic build: slow-path statistics
+    import ctypes as C
+    cnt = np.zeros(4, np.uint64)
+    ctx._L.sod_debug_counts(cnt.ctypes.data_as(C.c_void_p), 1)
+    ctx.match()
+    ctx.synchronize()
+    ctx._L.sod_debug_counts(cnt.ctypes.data_as(C.c_void_p), 0)
+    print("slow-path entries / wave-subtile %.4f, hit tiles / wave-subtile %.4f (%d wave-subtiles)" % (
+        cnt[0] / cnt[2], cnt[1] / cnt[2], cnt[2]), flush=True)
 ctx.ratio(0.75)
 idx1, d1, d2, good = ctx.match_result()
 print("checksum", int(idx1.astype(np.int64).sum()), float(d1.astype(np.float64).sum()), flush=True)
