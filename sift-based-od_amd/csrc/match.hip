@@ -396,7 +396,8 @@ int launch_match(sod_ctx* ctx) {
   const int64_t nstages = ctx->nsub / SPS;
   // fill every CU twice (2 workgroups of 4 waves per CU); each split >= 1 stage
   int64_t target = 2LL * ctx->num_cus;
-  int64_t split = std::max<int64_t>(1, (target + qblocks / 2) / qblocks);
+  // (rounded down: one work-group more than the slots would run as a second round)
+  int64_t split = std::max<int64_t>(1, target / qblocks);
   split = std::min<int64_t>(split, nstages);
   const int64_t st_per_split = ceil_div(nstages, split);
   split = ceil_div(nstages, st_per_split);

@@ -18,8 +18,8 @@
 // A[row l&15][k 16(l>>4)..+15] and B[k ..][col l&15]; D: col l&15, rows 4(l>>4)+r.  A 16-row
 // subtile is [kstep 2][lane 64][16 B] = 2 KiB (the LDS image is the HBM image).
 // Structure (cf. match.hip): queries stationary in VGPRs (64 per lane for 128 queries per
-// wave), DB streamed through a 3-slot LDS-DMA ring of 128-row stages (prefetch distance 2,
-// one barrier per stage), c/p read per subtile.  The prefilter of subtile u runs while
+// wave), DB streamed through a 2-slot LDS-DMA ring of 512-row stages (prefetch distance 1,
+// one barrier per stage), c read per subtile (parity on the slow path).  The prefilter of subtile u runs while
 // the MFMAs of subtile u+1 are in flight (software pipeline: no MFMA->VALU stall), with
 // one ballot + scalar branch per subtile and per 16x16 tile.  Each lane keeps the exact
 // top-2 of its own rows; the threshold is the query's second best over its four lane
@@ -50,7 +50,7 @@ constexpr int QT = 8;          // 16-query tiles per wave
 constexpr int NW16 = SOD_I8_NW;
 constexpr int NT16 = NW16 * 64;
 #ifndef SOD_I8_SPS
-#define SOD_I8_SPS 16
+#define SOD_I8_SPS 32    // 512-row stages: 64 KiB, two slots (measured +1 % over 256-row x 3)
 #endif
 #ifndef SOD_I8_UNROLL
 #define SOD_I8_UNROLL 0    // subtile-loop unroll (0 = full)
@@ -58,7 +58,7 @@ constexpr int NT16 = NW16 * 64;
 constexpr int SPS = SOD_I8_SPS;   // subtiles per stage (one barrier per stage)
 constexpr int kStageRows = SPS * 16;
 constexpr int kSub = 2048;     // bytes per 16-row subtile
-constexpr int kStageBytes = SPS * kSub;          // 16 KiB
+constexpr int kStageBytes = SPS * kSub;          // 64 KiB
 // per stage (128 rows) and wave w (its 128/NW16 rows): [c: i32 each | p: i32 each]
 constexpr int kStageNorm = 2 * SPS * kSubRows * 4;   // c and parity words
 // the norm words live in a ring of their own, one entry deeper than the descriptor ring:
@@ -198,7 +198,7 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 }
 
 #ifndef SOD_I8_RING
-#define SOD_I8_RING 3      // LDS stage slots (prefetch distance = RING - 1 stages)
+#define SOD_I8_RING 2      // LDS stage slots (prefetch distance = RING - 1 stages)
 #endif
 #ifndef SOD_I8_PIPE
 #define SOD_I8_PIPE 1      // prefilter subtile u while the MFMAs of subtile u+1 run
@@ -248,13 +248,19 @@ __device__ __forceinline__ void top2_xor16(int& y1, int& y2) {
 #define PARITY_T i32x4            // the parity words
 #endif
 
+#ifdef SOD_I8_COUNT
+// diagnostic build only: [0] slow-path entries, [1] hit tiles, [2] wave-subtiles,
+// [3] entries and [4] hit tiles within the first 64 subtiles of a chunk
+__device__ unsigned long long g_counts[8];
+#endif
+
 // prefilter + exact top-2 update of one 16x16 tile set (see the file comment).  Each lane
 // keeps the exact top-2 (with index) of ITS rows; the prefilter threshold is the query's
 // second-best value over all four lane groups (lanes l, l^16, l^32, l^48), which every
 // row of the final top-2 reaches (>=, so ties keep their lowest-index winner).
 __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin, int rowb,
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
-                                            int (&id)[QT]) {
+                                            int (&id)[QT], bool early = false) {
   uint64_t hit[QT];
   uint64_t any = 0;
 #pragma unroll
@@ -275,6 +281,18 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
 #endif
 #if SOD_I8_COLD
   if (__builtin_expect(any != 0, 0)) {   // slow path laid out away from the hot loop
+#ifdef SOD_I8_COUNT
+    if ((threadIdx.x & 63) == 0) {
+      unsigned nh = 0;
+      for (int t = 0; t < QT; ++t) nh += hit[t] != 0;
+      atomicAdd(&g_counts[0], 1ull);
+      atomicAdd(&g_counts[1], (unsigned long long)nh);
+      if (early) {
+        atomicAdd(&g_counts[3], 1ull);
+        atomicAdd(&g_counts[4], (unsigned long long)nh);
+      }
+    }
+#endif
 #else
   if (any) {
 #endif
@@ -391,7 +409,7 @@ __device__ __forceinline__ void match_unit(
 #if SOD_I8_UNROLL
 #pragma unroll SOD_I8_UNROLL
 #else
-#pragma unroll
+#pragma clang loop unroll(full)
 #endif
     for (int u = 0; u < SPS; ++u) {
       const i32x4 a0 = fa0, a1 = fa1, c = fc;   // c = floor(-||d'||^2 / 2)
@@ -427,7 +445,7 @@ __device__ __forceinline__ void match_unit(
         if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
 #elif SOD_I8_PIPE
-      tile_update(accp, pp, rowp, y1, y2, t2, id);
+      tile_update(accp, pp, rowp, y1, y2, t2, id, s * SPS + u <= 64);
 #pragma unroll
       for (int t = 0; t < QT; ++t) accp[t] = acc[t];
       pp = p;
@@ -439,6 +457,9 @@ __device__ __forceinline__ void match_unit(
   }
 #if SOD_I8_PIPE
   tile_update(accp, pp, rowp, y1, y2, t2, id);
+#endif
+#ifdef SOD_I8_COUNT
+  if (lane == 0) atomicAdd(&g_counts[2], (unsigned long long)(nst * SPS));
 #endif
 
 #pragma unroll
@@ -737,6 +758,16 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   return SOD_OK;
 }
 
+#ifdef SOD_I8_COUNT
+extern "C" int sod_debug_counts(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_counts), 64) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_counts), z, 64) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
 #ifdef SOD_I8_STAMP
 extern "C" int sod_debug_stamps(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 64) == hipSuccess ? 0 : 1;
@@ -754,7 +785,8 @@ int launch_match_i8(sod_ctx* ctx) {
   // one round of work-groups (8 waves per CU): as few DB chunks as fill the chip (every chunk
   // restarts each query's running top-2, so more chunks mean more slow-path updates)
   const int64_t slots = ((wide ? w::NW : NW16) == 4 ? 2LL : 1LL) * ctx->num_cus;   // in flight
-  int64_t split = std::max<int64_t>(1, (slots + qblocks / 2) / qblocks);
+  // (rounded down: one work-group more than the slots would run as a second round)
+  int64_t split = std::max<int64_t>(1, slots / qblocks);
   split = std::min<int64_t>(split, nstages);
   const int64_t st_per_split = cdiv(nstages, split);
   split = cdiv(nstages, st_per_split);

@@ -75,13 +75,15 @@ if hasattr(ctx._L, "sod_debug_stamps"):   # diagnostic build: in-kernel clock
                                                      int(place[b])) for b in order], flush=True)
 if hasattr(ctx._L, "sod_debug_counts"):   # diagnostic build: slow-path statistics
     import ctypes as C
-    cnt = np.zeros(4, np.uint64)
+    cnt = np.zeros(8, np.uint64)
     ctx._L.sod_debug_counts(cnt.ctypes.data_as(C.c_void_p), 1)
     ctx.match()
     ctx.synchronize()
     ctx._L.sod_debug_counts(cnt.ctypes.data_as(C.c_void_p), 0)
-    print("slow-path entries / wave-subtile %.4f, hit tiles / wave-subtile %.4f (%d wave-subtiles)" % (
-        cnt[0] / cnt[2], cnt[1] / cnt[2], cnt[2]), flush=True)
+    print("slow-path entries / wave-subtile %.4f, hit tiles / wave-subtile %.4f (%d wave-subtiles); "
+          "first 64 subtiles of a chunk: %.1f %% of entries, %.1f %% of hit tiles" % (
+              cnt[0] / cnt[2], cnt[1] / cnt[2], cnt[2], 100.0 * cnt[3] / max(cnt[0], 1),
+              100.0 * cnt[4] / max(cnt[1], 1)), flush=True)
 ctx.ratio(0.75)
 idx1, d1, d2, good = ctx.match_result()
 print("checksum", int(idx1.astype(np.int64).sum()), float(d1.astype(np.float64).sum()), flush=True)
