@@ -128,13 +128,14 @@ class Dist:
         return float(t.item())
 
 
-def device_sync(world):
-    # the whole step runs on libsod's own stream (ctx.synchronize() waits for it); with
-    # several ranks torch is loaded anyway and a device-wide sync is added on top
+def device_sync(world, dev):
+    # the whole step runs on libsod's own streams (ctx.synchronize() waits for them); with
+    # several ranks torch is loaded anyway and a device-wide sync of THIS rank's GPU is added
+    # on top (torch's default device 0 would open a context on GPU 0 in every rank)
     if world > 1:
         import torch
         if torch.cuda.is_available():
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(dev)
 
 
 def cpu_baseline(queries, db_des, nq_sample):
@@ -378,12 +379,12 @@ def main():
     match_ms, stage = [], []
     D.barrier()
     sync_all()
-    device_sync(world)
+    device_sync(world, dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     sync_all()
-    device_sync(world)
+    device_sync(world, dev)
     D.barrier()
     t1 = time.perf_counter()
     el = D.max(t1 - t0)
