@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from conftest import golden
-from helpers import kp, kp_dict
+from helpers import ThreadComm, kp, kp_dict
 from oracle import oracle as orc
 from sift_based_od_amd import _lib, synthetic
 import sift_based_od_amd as sod
@@ -110,31 +110,6 @@ def test_main_stages_match_golden():
     m.post_process()                                   # main.py:186
     got = np.array([[p[0][0], p[0][1], p[1], p[2], p[3][0], p[3][1]] for p in m.final_pose])
     np.testing.assert_allclose(got.reshape(-1, 6), g["final_pose"], rtol=1e-12, atol=1e-9)
-
-
-class ThreadComm:
-    """allgather / allreduce between threads of one process (test plumbing)."""
-
-    def __init__(self, world):
-        self.world = world
-        self.bar = threading.Barrier(world)
-        self.slots = [None] * world
-
-    def for_rank(self, r):
-        from sift_based_od_amd.sharded import HostComm
-
-        def allgather(a):
-            self.slots[r] = np.array(a)
-            self.bar.wait()
-            out = list(self.slots)
-            self.bar.wait()
-            return out
-
-        def allreduce(a, op):
-            parts = allgather(a)
-            return (np.sum(parts, axis=0) if op == "sum" else np.min(parts, axis=0)).astype(a.dtype)
-
-        return HostComm(self.world, r, allgather, allreduce)
 
 
 @pytest.mark.parametrize("world", [2, 3])

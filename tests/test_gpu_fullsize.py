@@ -1,0 +1,157 @@
+"""GPU parity at BASELINE.json's full single-GPU size (configs[2] = C3: 50 000 queries x
+1 000 000 DB rows, Hough bins 32x32x8x12, affine verify), where the oracle cannot redo the
+whole matcher in seconds.  Checked instead:
+
+* the matcher on a seeded sample of 512 queries against the oracle over ALL 1M rows
+  (bit-exact trainIdx, d1, d2, ratio decisions), and the whole 50k x 1M result bit-identical
+  between the int8 and bf16 MFMA kernels (two independent exact arithmetics);
+* everything after the matcher against the oracle on the device's own good matches: the
+  full bin table in first-touch order, valid bins, member lists, PoseBin means, survivors,
+  affine parameters (1e-4, north_star) and the post-processing poses;
+* the DB sharded 8 ways (C4's decomposition) equal to one context, bit for bit.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from sift_based_od_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+BINS = (32, 32, 8, 12)
+AFFINE_ATOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def c3():
+    db = synthetic.make_database(1000, 1000, seed=0)
+    qs = synthetic.make_queries(50000, seed=1, db_seed=0, kp_per_image=1000)
+    return db, qs
+
+
+def test_c3_full_pipeline(ctx, c3):
+    db, qs = c3
+    ctx.set_impl("i8")
+    ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
+    ctx.upload_db(db.des)
+    ctx.upload_queries(qs.des, qs.kp)
+    ctx.pipeline(qs.shape, BINS, ratio=0.75, vote_threshold=5, affine_threshold=4)
+    idx1, d1, d2, good = ctx.match_result()
+    assert ctx.exact_order()
+
+    # matcher: a sample against the oracle over the full DB
+    sample = np.sort(np.random.default_rng(7).choice(len(qs.des), 512, replace=False))
+    e1, f1, f2 = orc.knn2_match(qs.des[sample], db.des, chunk=128)
+    assert np.array_equal(idx1[sample], e1)
+    assert np.array_equal(d1[sample], f1) and np.array_equal(d2[sample], f2)
+    assert np.array_equal(good[sample], orc.ratio_test(f1, f2))
+    assert np.array_equal(good, orc.ratio_test(d1, d2))
+
+    # Hough / valid bins / members / means against the oracle on the same good matches
+    matches = [(int(q), int(idx1[q])) for q in np.nonzero(good)[0]]
+    dbkp = {"x": db.kp.x, "y": db.kp.y, "angle": db.kp.angle, "octave": db.kp.octave,
+            "img": db.img}
+    qkp = {"x": qs.kp.x, "y": qs.kp.y, "angle": qs.kp.angle, "octave": qs.kp.octave}
+    images = {"centroid": db.centroid, "size": db.size}
+    table = orc.hough_vote(matches, qkp, dbkp, images, BINS, qs.shape)
+    keys, votes = ctx.all_bins()
+    assert [tuple(int(v) for v in k) for k in keys] == list(table.keys()), \
+        "bin table (first-touch order) differs"
+    assert list(votes) == [b.votes for b in table.values()]
+    vb = orc.valid_bins(table, 5)
+    v = ctx.valid_result()
+    assert [tuple(int(x) for x in k) for k in v["keys"]] == [b.pose for b in vb]
+    assert list(v["votes"]) == [b.votes for b in vb]
+    for i, b in enumerate(vb):
+        assert list(v["members"][v["offsets"][i]:v["offsets"][i + 1]]) == [q for q, _ in b.members]
+    ref_means = np.array([[b.centroid[0], b.centroid[1], b.angle, b.scale, b.img_size[0],
+                           b.img_size[1]] for b in vb])
+    np.testing.assert_allclose(v["means"], ref_means, rtol=1e-12, atol=1e-9)
+
+    # affine verification to its fixed point
+    aff = orc.affine_verify(vb, qkp, dbkp, (qs.shape[1], qs.shape[0]), 4)
+    a = ctx.affine_result()
+    assert [bool(s) for s in a["survived"]] == [r["survived"] for r in aff]
+    surv = np.nonzero(a["survived"])[0]
+    assert len(surv) > 0
+    for i in surv:
+        assert a["votes"][i] == aff[i]["votes"]
+        np.testing.assert_allclose(a["params"][i], aff[i]["params"], rtol=0, atol=AFFINE_ATOL)
+        lo, hi = v["offsets"][i], v["offsets"][i + 1]
+        kept = v["members"][lo:hi][a["alive"][lo:hi]]
+        assert list(kept) == [q for q, _ in aff[i]["members"]]
+
+    # post-processing of the survivors
+    post = ctx.postprocess()
+    ref = orc.post_process(v["means"][post["bin_index"]])
+    fp = np.array([[p[0][0], p[0][1], p[1], p[2], p[3][0], p[3][1]] for p in ref["final_pose"]])
+    np.testing.assert_allclose(post["final_pose"], fp.reshape(-1, 6), rtol=1e-12, atol=1e-9)
+
+
+def test_c3_int8_equals_bf16(ctx, c3):
+    """The whole 50k x 1M match by two different exact MFMA arithmetics (int8 with the norm
+    folded into the accumulator; bf16 with -2d and f32 norms): identical bits."""
+    db, qs = c3
+    out = {}
+    for impl in ("i8", "bf16"):
+        ctx.set_impl(impl)
+        ctx.upload_db(db.des)
+        ctx.upload_queries(qs.des, qs.kp)
+        ctx.match()
+        ctx.ratio(0.75)
+        out[impl] = ctx.match_result()
+    for a, b in zip(out["i8"], out["bf16"]):
+        assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+
+
+def test_c3_db_sharded_8_ways_equals_single(ctx, c3):
+    """SURVEY §8(e) at C4's sharding (8 shards, here 125 000 rows each of the 1M-row DB):
+    8 contexts on this GPU, one host thread each, exchanging the 12 B/query candidates and
+    the Hough partials through a host communicator -- every rank's result equals the
+    single-context run bit for bit (the exchange logic RCCL carries on a node)."""
+    import threading
+
+    from helpers import ThreadComm
+    from sift_based_od_amd import _lib
+    import sift_based_od_amd as sod
+
+    db, qs = c3
+    world = 8
+    ctx.set_impl("i8")
+    ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
+    ctx.upload_db(db.des)
+    ctx.upload_queries(qs.des, qs.kp)
+    ctx.pipeline(qs.shape, BINS)
+    ref = (ctx.match_result(), ctx.valid_result(), ctx.affine_result())
+    comm = ThreadComm(world)
+    results = [None] * world
+    errors = []
+
+    def rank_main(r):
+        try:
+            lo, hi = sod.shard_range(len(db.des), r, world)
+            with _lib.Context(0) as c:
+                c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+                c.upload_db(db.des[lo:hi], row_offset=lo)
+                c.upload_queries(qs.des, qs.kp)
+                sod.run_sharded(c, comm.for_rank(r), (lo, hi), qs.shape, BINS)
+                results[r] = (c.match_result(), c.valid_result(), c.affine_result())
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+            comm.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    (i1, d1, d2, g1), v1, a1 = ref
+    for (i2, e1, e2, g2), v2, a2 in results:
+        assert np.array_equal(i1, i2) and np.array_equal(d1, e1) and np.array_equal(d2, e2)
+        assert np.array_equal(g1, g2)
+        for k in ("keys", "votes", "offsets", "members"):
+            assert np.array_equal(v1[k], v2[k]), k
+        assert np.array_equal(v1["means"], v2["means"])
+        assert np.array_equal(a1["survived"], a2["survived"])
+        assert np.array_equal(a1["params"], a2["params"])
