@@ -218,6 +218,10 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_LAZYP
 #define SOD_I8_LAZYP 1     // parity words read from LDS on the slow path only
 #endif
+#ifndef SOD_I8_DENSE
+#define SOD_I8_DENSE 32    // leading subtiles of a chunk updated without threshold exchange (C2: +8 %)
+#endif
+constexpr int64_t kDense = SOD_I8_DENSE;
 #ifndef SOD_SHARED_T
 #define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
 #endif
@@ -258,9 +262,12 @@ __device__ unsigned long long g_counts[8];
 // keeps the exact top-2 (with index) of ITS rows; the prefilter threshold is the query's
 // second-best value over all four lane groups (lanes l, l^16, l^32, l^48), which every
 // row of the final top-2 reaches (>=, so ties keep their lowest-index winner).
+// mode (wave-uniform): 0 = prefilter; 1 = dense (the chunk's first subtiles, where
+// t2 is still -inf and every tile takes the exact update: the threshold exchange is
+// skipped); 2 = the last dense subtile (the exchange then sets every tile's t2).
 __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin, int rowb,
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
-                                            int (&id)[QT], bool early = false) {
+                                            int (&id)[QT], bool early = false, int mode = 0) {
   uint64_t hit[QT];
   uint64_t any = 0;
 #pragma unroll
@@ -312,6 +319,21 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
           id[t] = gt ? rowb + r : id[t];
           y1[t] = gt ? y : y1[t];
         }
+        if (mode == 0) {
+#if SOD_SHARED_T
+          int g1 = y1[t], g2 = y2[t];
+          top2_xor32(g1, g2);
+          top2_xor16(g1, g2);
+          t2[t] = g2 >> 1;
+#else
+          t2[t] = y2[t] >> 1;
+#endif
+        }
+      }
+    }
+    if (mode == 2) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
 #if SOD_SHARED_T
         int g1 = y1[t], g2 = y2[t];
         top2_xor32(g1, g2);
@@ -445,7 +467,12 @@ __device__ __forceinline__ void match_unit(
         if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
 #elif SOD_I8_PIPE
-      tile_update(accp, pp, rowp, y1, y2, t2, id, s * SPS + u <= 64);
+      {
+        // the pending subtile's index in the chunk decides dense / final / prefilter
+        const int64_t kp = s * SPS + u - 1;
+        const int mode = kp < kDense - 1 ? 1 : (kp == kDense - 1 ? 2 : 0);
+        tile_update(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode);
+      }
 #pragma unroll
       for (int t = 0; t < QT; ++t) accp[t] = acc[t];
       pp = p;
@@ -456,7 +483,7 @@ __device__ __forceinline__ void match_unit(
     }
   }
 #if SOD_I8_PIPE
-  tile_update(accp, pp, rowp, y1, y2, t2, id);
+  tile_update(accp, pp, rowp, y1, y2, t2, id, false, nst * SPS <= kDense ? 1 : 0);
 #endif
 #ifdef SOD_I8_COUNT
   if (lane == 0) atomicAdd(&g_counts[2], (unsigned long long)(nst * SPS));
