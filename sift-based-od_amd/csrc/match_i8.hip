@@ -27,8 +27,9 @@
 // Work-groups are ordered XCD-aware: each XCD's L2 serves one or two DB chunks.
 // Measured and rejected (C3, same device): a persistent work-queue kernel (more chunks =
 // more top-2 restarts), a seeded threshold pre-pass (gain eaten by the pass), other
-// shifts than -128 (slower), the 32x32x32 shape (impl 2: lower clock held, kept as an
-// option).
+// shifts than -128 (slower), the 32x32x32 shape (impl 2, below: 9 VALU per 1024 pairs
+// instead of 12 and half the MFMA issue holds, but the chip holds ~2.03 GHz on it vs ~2.2 on
+// 16x16x64: 4.7 vs 4.0-4.2 ms; kept as an option).
 #include <climits>
 
 #include "sod_internal.h"
@@ -558,10 +559,15 @@ __global__ __launch_bounds__(NT16, 8 / NW16) void match_i8_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// 32x32x32 variant: lane l owns query l&31 and 16 rows (reg r -> row (r&3) + 8(r>>2) +
-// 4(l>>5)) of each 32-row subtile.  An MFMA of this shape holds the SIMD's issue port for
-// 8 of its 32 cycles (vs 8 of 16 for 16x16x64), and the prefilter reduces 16 values per
-// lane per tile, so the instruction stream leaves room beside the matrix pipe.
+// 32x32x32 variant (impl 2): lane l owns query l&31 and 16 rows (reg r -> row (r&3) +
+// 8(r>>2) + 4(l>>5)) of each 32-row subtile.  An MFMA of this shape holds the SIMD's issue
+// port for 8 of its 32 cycles (vs 8 of 16 for 16x16x64), and the prefilter reduces 16
+// values per lane and tile (9 VALU per 1024 pairs instead of 12), so the instruction stream
+// leaves room beside the matrix pipe.  Tile-major order: the 4 MFMAs (K = 4 x 32) of tile t
+// are issued back to back (one accumulation chain) and tile t-1's prefilter runs beside
+// them, so only two tile accumulators are alive (the last tile of a subtile is tested
+// beside the next subtile's first tile).  DB stages of 512 rows in a 2-slot ring, norm words
+// in a ring of their own (parity read on the slow path), as match_i8_kernel.
 #ifndef SOD_I8W_NW
 #define SOD_I8W_NW 8
 #endif
@@ -569,19 +575,17 @@ namespace w {
 constexpr int NW = SOD_I8W_NW;   // waves per work-group (8: one work-group per CU)
 constexpr int NT = NW * 64;
 constexpr int QT = 4;            // 32-query tiles per wave (128 queries)
-constexpr int SPS = 4;           // 32-row subtiles per stage (128 rows)
+constexpr int SPS = 16;          // 32-row subtiles per stage (512 rows)
 constexpr int kSub = 4096;
-constexpr int kStageBytes = SPS * kSub;          // 16 KiB
-constexpr int kStageNorm = 2 * SPS * 32 * 4;     // c and p of 128 rows: 1 KiB
-constexpr int kStageSlot = kStageBytes + kStageNorm;
+constexpr int kStageBytes = SPS * kSub;          // 64 KiB
+constexpr int kStageNorm = 2 * SPS * 32 * 4;     // c and p of 512 rows: 4 KiB
 constexpr int kPiecesPerWave = kStageBytes / 1024 / NW;
-constexpr int kRing = 3;
-constexpr int kLoadsPerStage = kPiecesPerWave + 1;
-constexpr int kNormRows = 128 / NW;               // norm rows staged per wave
-// LDS offset (from the slot) of c for the 4 consecutive rows starting at stage row r;
+constexpr int kRing = 2;
+constexpr int kNormRows = SPS * 32 / NW;          // norm rows staged per wave
+// offset (in a norm-ring entry) of c for the 4 consecutive rows starting at stage row r;
 // parity at + 4 * kNormRows
 __device__ __forceinline__ int norm_off(int r) {
-  return kStageBytes + (r / kNormRows) * (8 * kNormRows) + (r % kNormRows) * 4;
+  return (r / kNormRows) * (8 * kNormRows) + (r % kNormRows) * 4;
 }
 }  // namespace w
 
@@ -589,14 +593,60 @@ typedef __attribute__((ext_vector_type(16))) int i32x16;
 
 __device__ __forceinline__ void issue_stage_w(const uint8_t* __restrict__ dbpack,
                                               const int* __restrict__ dn, int64_t npad, int64_t sub0,
-                                              uint8_t* slot, int wave, int lane) {
+                                              uint8_t* slot, uint8_t* norm_slot, int wave, int lane) {
   const uint8_t* src = dbpack + sub0 * w::kSub;
 #pragma unroll
   for (int j = 0; j < w::kPiecesPerWave; ++j) {
     const int piece = wave * w::kPiecesPerWave + j;
     glds16(src + piece * 1024 + lane * 16, slot + piece * 1024);
   }
-  issue_norms<w::NW, 128>(dn, npad, sub0 * 32, slot + w::kStageBytes, wave, lane);
+  issue_norms<w::NW, w::SPS * 32>(dn, npad, sub0 * 32, norm_slot, wave, lane);
+}
+
+// prefilter + exact update of ONE 32x32 tile: max of the lane's 16 values against the
+// query's threshold, and on a hit the exact top-2 of the lane's rows (parity words from the
+// norm ring) and the query-wide threshold over the two lane halves
+// rowb is wave-uniform (the lane half's 4 h is added at the end), so the slow path's row
+// numbers are scalar adds, not VALU
+__device__ __forceinline__ void tile_update_w(const i32x16& acc, const uint8_t* pbase, int rowb,
+                                              int& y1, int& y2, int& t2, int& id) {
+  // two max3 chains of 7 values and one combine: 8 VALU, dependence depth 4
+  const int ma = max(max(max(max(max(max(acc[0], acc[1]), acc[2]), acc[3]), acc[4]), acc[5]), acc[6]);
+  const int mb = max(max(max(max(max(max(acc[7], acc[8]), acc[9]), acc[10]), acc[11]), acc[12]), acc[13]);
+  const int m = max(max(ma, mb), max(acc[14], acc[15]));
+#if SOD_I8_SGB
+  // interleave: MFMA, MFMA, 4 VALU, MFMA, 5 VALU, MFMA (the previous tile's MFMA result
+  // is read two MFMAs after its last MFMA)
+  __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+  __builtin_amdgcn_sched_group_barrier(0x2, 4, 0);
+  __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+  __builtin_amdgcn_sched_group_barrier(0x2, 5, 0);
+  __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+#endif
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= t2) != 0, 0)) {
+    // scalar row base materialised inside the slow path (readfirstlane is convergent, so
+    // the 16 row numbers are not hoisted into the hot block as vector adds)
+    const int rs = __builtin_amdgcn_readfirstlane(rowb);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const i32x4 pv = *reinterpret_cast<const i32x4*>(pbase + w::norm_off(8 * g) + 4 * w::kNormRows);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int y = 2 * acc[4 * g + i] | pv[i];
+        const bool gt = y > y1;
+        y2 = imed3(y1, y, y2);
+        id = gt ? rs + 8 * g + i : id;
+        y1 = gt ? y : y1;
+      }
+    }
+#if SOD_SHARED_T
+    int g1 = y1, g2 = y2;
+    top2_xor32(g1, g2);
+    t2 = g2 >> 1;
+#else
+    t2 = y2 >> 1;
+#endif
+  }
 }
 
 __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
@@ -604,7 +654,7 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2, int nqb) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[w::kRing * w::kStageSlot];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[w::kRing * w::kStageBytes + kNormRing * w::kStageNorm];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // XCD-aware chunk-major order, as match_i8_kernel
   const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x8 = blockIdx.x % 8;
@@ -617,10 +667,13 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
   const int64_t nst = (s_hi - s_lo) / w::SPS;
   const int h = lane >> 5;
   const int64_t npad = nsub * 32;
+  uint8_t* const nring = lds + w::kRing * w::kStageBytes;
 
 #pragma unroll
   for (int j = 0; j < w::kRing - 1; ++j)
-    if (j < nst) issue_stage_w(dbpack, dn, npad, s_lo + j * w::SPS, lds + j * w::kStageSlot, wave, lane);
+    if (j < nst)
+      issue_stage_w(dbpack, dn, npad, s_lo + j * w::SPS, lds + j * w::kStageBytes,
+                    nring + j * w::kStageNorm, wave, lane);
 
   i32x4 bq[w::QT][4];
 #pragma unroll
@@ -639,94 +692,74 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
     t2[t] = INT_MIN >> 1;
     id[t] = 0x7fffffff;
   }
+  const int rowl = row_offset + (int)(s_lo * 32);   // + 4 h per lane half, added at the end
+  // the last tile of the previous subtile, tested beside the next subtile's first tile
+  i32x16 accp;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) accp[r] = INT_MIN;
+  const uint8_t* pp = nring;
+  int rowp = 0;
 
   int slot = 0;
   for (int64_t s = 0; s < nst; ++s) {
-    if (s + 1 < nst)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(w::kLoadsPerStage) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!(SOD_I8_EXP & 4)) __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this stage landed (2-slot ring)
+    __builtin_amdgcn_s_barrier();
     if (s + w::kRing - 1 < nst) {
       const int ns = slot == 0 ? w::kRing - 1 : slot - 1;
-      issue_stage_w(dbpack, dn, npad, s_lo + (s + w::kRing - 1) * w::SPS, lds + ns * w::kStageSlot,
-                    wave, lane);
+      issue_stage_w(dbpack, dn, npad, s_lo + (s + w::kRing - 1) * w::SPS, lds + ns * w::kStageBytes,
+                    nring + ((s + w::kRing - 1) % kNormRing) * w::kStageNorm, wave, lane);
     }
-    const uint8_t* sb = lds + slot * w::kStageSlot;
+    const uint8_t* sb = lds + slot * w::kStageBytes;
+    const uint8_t* nb = nring + (s % kNormRing) * w::kStageNorm + w::norm_off(4 * h);
     slot = slot + 1 == w::kRing ? 0 : slot + 1;
-    i32x4 fa[4];
+    i32x4 fa[4], fc[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) fa[k] = *reinterpret_cast<const i32x4*>(sb + k * 1024 + lane * 16);
-#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      fa[k] = *reinterpret_cast<const i32x4*>(sb + k * 1024 + lane * 16);
+      fc[k] = *reinterpret_cast<const i32x4*>(nb + w::norm_off(8 * k));
+    }
+#pragma clang loop unroll(full)
     for (int u = 0; u < w::SPS; ++u) {
       i32x4 a[4];
+      i32x16 c;   // c = floor(-||d'||^2 / 2) of the lane's 16 rows 8g + 4h + i
 #pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] = fa[k];
-      // c = floor(-||d'||^2 / 2) of the lane's 16 rows 8g + 4h + i (4 x 16 B)
-      i32x16 c;
+      for (int k = 0; k < 4; ++k) {
+        a[k] = fa[k];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const i32x4 wv = *reinterpret_cast<const i32x4*>(sb + w::norm_off(32 * u + 8 * g + 4 * h));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) c[4 * g + i] = wv[i];
+        for (int i = 0; i < 4; ++i) c[4 * k + i] = fc[k][i];
       }
-      i32x16 acc[w::QT];
-#pragma unroll
-      for (int t = 0; t < w::QT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], bq[t][0], c, 0, 0, 0);
-      if (u + 1 < w::SPS) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          fa[k] = *reinterpret_cast<const i32x4*>(sb + (u + 1) * w::kSub + k * 1024 + lane * 16);
-      }
-#pragma unroll
-      for (int k = 1; k < 4; ++k)
-#pragma unroll
-        for (int t = 0; t < w::QT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], bq[t][k], acc[t], 0, 0, 0);
-      uint64_t hit[w::QT];
-      uint64_t any = 0;
+      const uint8_t* pu = nb + w::norm_off(32 * u);   // this subtile's norm words (lane half h)
+      const int rowb = rowl + (int)((s * w::SPS + u) * 32);
+      i32x16 accq;   // the previous tile of this subtile
 #pragma unroll
       for (int t = 0; t < w::QT; ++t) {
-        int m = acc[t][0];
+        i32x16 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], bq[t][0], c, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[1], bq[t][1], acc, 0, 0, 0);
+        if (t == 0 && u + 1 < w::SPS) {   // next subtile's fragments in flight
 #pragma unroll
-        for (int r = 1; r < 16; ++r) m = max(m, acc[t][r]);
-        hit[t] = __builtin_amdgcn_ballot_w64(m >= t2[t]);
-        any |= hit[t];
-      }
-      if (any) {
-        const int rowb = row_offset + (int)((s_lo + s * w::SPS + u) * 32) + 4 * h;
-#pragma unroll
-        for (int t = 0; t < w::QT; ++t) {
-          if (hit[t]) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const i32x4 pv = *reinterpret_cast<const i32x4*>(
-                  sb + w::norm_off(32 * u + 8 * g + 4 * h) + 4 * w::kNormRows);
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int y = 2 * acc[t][4 * g + i] | pv[i];
-                const bool gt = y > y1[t];
-                y2[t] = imed3(y1[t], y, y2[t]);
-                id[t] = gt ? rowb + 8 * g + i : id[t];
-                y1[t] = gt ? y : y1[t];
-              }
-            }
-#if SOD_SHARED_T
-            int g1 = y1[t], g2 = y2[t];
-            top2_xor32(g1, g2);
-            t2[t] = g2 >> 1;
-#else
-            t2[t] = y2[t] >> 1;
-#endif
+          for (int k = 0; k < 4; ++k) {
+            fa[k] = *reinterpret_cast<const i32x4*>(sb + (u + 1) * w::kSub + k * 1024 + lane * 16);
+            fc[k] = *reinterpret_cast<const i32x4*>(nb + w::norm_off(32 * (u + 1) + 8 * k));
           }
         }
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[2], bq[t][2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[3], bq[t][3], acc, 0, 0, 0);
+        if (t == 0)
+          tile_update_w(accp, pp, rowp, y1[w::QT - 1], y2[w::QT - 1], t2[w::QT - 1], id[w::QT - 1]);
+        else
+          tile_update_w(accq, pu, rowb, y1[t - 1], y2[t - 1], t2[t - 1], id[t - 1]);
+        accq = acc;
       }
+      accp = accq;
+      pp = pu;
+      rowp = rowb;
     }
   }
+  tile_update_w(accp, pp, rowp, y1[w::QT - 1], y2[w::QT - 1], t2[w::QT - 1], id[w::QT - 1]);
 
 #pragma unroll
   for (int t = 0; t < w::QT; ++t) {
+    if (y1[t] != INT_MIN) id[t] += 4 * h;   // the lane half's row offset
     const int o1 = __shfl_xor(y1[t], 32), oi = __shfl_xor(id[t], 32), o2 = __shfl_xor(y2[t], 32);
     merge2i(y1[t], id[t], y2[t], o1, oi, o2);
     const int qt = qt0 + t;
