@@ -70,6 +70,10 @@ def parse():
                         "query images alternate between them, so one image's Hough/select/"
                         "affine tail overlaps the next image's matcher.  Default: 2 on one "
                         "GPU, 1 with several ranks")
+    p.add_argument("--overlap", type=int, default=-1, choices=[-1, 0, 1],
+                   help="matcher kernel on a stream of its own, overlapping the previous query "
+                        "image's Hough/select/affine stages inside ONE context (collectives "
+                        "stay on the context stream).  Default: on with several ranks")
     p.add_argument("--impl", default="i8", choices=sorted(IMPLS),
                    help="matcher kernel: int8 MFMA 16x16x64 (default, fastest), int8 32x32x32 "
                         "or bf16 MFMA; all bit-exact")
@@ -347,7 +351,9 @@ def main():
     elif world > 1:
         comm = TorchHostComm()
     own = (rank * n_shard, (rank + 1) * n_shard)
-    ncontexts = a.contexts if a.contexts > 0 else (2 if world == 1 else 1)
+    overlap = a.overlap if a.overlap >= 0 else (1 if world > 1 else 0)
+    ctx.set_overlap(bool(overlap))
+    ncontexts = a.contexts if a.contexts > 0 else (2 if world == 1 and not overlap else 1)
     ctxs = [ctx]
     for _ in range(ncontexts - 1):
         c = _lib.Context(dev)
@@ -442,7 +448,7 @@ def main():
             " + affine verify" if run_affine else ""),
             "queries": nq, "db_rows_per_gpu": n_shard, "db_rows_total": world * n_shard,
             "bins": list(bins), "parallelism": "db-shard%d" % world,
-            "query_streams": ncontexts,
+            "query_streams": ncontexts, "matcher_overlap": bool(overlap),
             "comm": a.comm if world > 1 else None},
         "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
         "hough_stage_votes_per_s": n_votes / ((float(stage[2]) + float(stage[3])) / 1000.0),

@@ -110,6 +110,12 @@ int sod_match_enqueue(sod_ctx* ctx);
  * bf16 MFMA rate.  All are bit-exact; call before the descriptor uploads (the packed
  * layouts differ; switching drops uploaded descriptors). */
 int sod_match_set_impl(sod_ctx* ctx, int impl);
+/* Matcher on a stream of its own (1) or on the context stream (0, default).  With 1 the
+ * matcher kernel of the next sod_match_enqueue / sod_pipeline_enqueue only waits for the
+ * previous merge of its partial results (and for the last descriptor upload), so it overlaps
+ * the previous query's Hough / select / affine stages, which stay on the context stream in
+ * order (RCCL collectives included).  Results are unchanged. */
+int sod_match_set_overlap(sod_ctx* ctx, int on);
 /* multi-GPU: RCCL all-gather of every rank's per-query (d1^2, idx1, d2^2) and the
  * global merge.  No-op on a single rank. */
 int sod_match_allgather_enqueue(sod_ctx* ctx);

@@ -61,6 +61,7 @@ SIGNATURES = {
     "sod_valid_images_get": (C.c_int, [c_ctx, c_i32p]),
     "sod_match_enqueue": (C.c_int, [c_ctx]),
     "sod_match_set_impl": (C.c_int, [c_ctx, C.c_int]),
+    "sod_match_set_overlap": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
     "sod_ratio_enqueue": (C.c_int, [c_ctx, C.c_double]),
     "sod_match_get": (C.c_int, [c_ctx, c_i32p, c_f32p, c_f32p, c_u8p]),
@@ -252,6 +253,11 @@ class Context:
         32x32x32); call before uploads."""
         self._chk(self._L.sod_match_set_impl(self._h, self.IMPLS[impl] if isinstance(impl, str)
                                              else int(impl)))
+
+    def set_overlap(self, on=True):
+        """Matcher kernel on a stream of its own: the next query's matcher overlaps this
+        one's Hough / select / affine stages (sod_match_set_overlap); results unchanged."""
+        self._chk(self._L.sod_match_set_overlap(self._h, 1 if on else 0))
 
     # -- stages --
     def match(self):

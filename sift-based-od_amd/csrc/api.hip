@@ -58,6 +58,53 @@ int flags_reset(sod_ctx* ctx) {
 }
 }  // namespace
 
+// ---- matcher stream protocol (sod_match_set_overlap) -----------------------------------
+// Writers of the matcher's inputs (packed DB / queries and their norm words) first wait for
+// the last matcher kernel, then mark the inputs ready; the matcher kernel waits for the
+// inputs and for the previous merge of its partial results, and the context stream waits
+// for the kernel before merging.
+int sod_inputs_begin(sod_ctx* ctx) {
+  SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0));
+  return SOD_OK;
+}
+int sod_inputs_end(sod_ctx* ctx) {
+  SOD_HIP(ctx, hipEventRecord(ctx->ev_inputs, ctx->stream));
+  return SOD_OK;
+}
+int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1, int32_t** idx,
+                           float** d2) {
+  const int nslot = ctx->overlap ? 2 : 1;
+  SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(nslot * n)));   // (a reallocation syncs the device)
+  SOD_TRY(sod_reserve(ctx, ctx->pd2, (size_t)(nslot * n)));
+  SOD_TRY(sod_reserve(ctx, ctx->pidx, (size_t)(nslot * n)));
+  const bool resized = n != ctx->pslot_n;
+  ctx->pslot = ctx->overlap ? ctx->pslot ^ 1 : 0;
+  ctx->pslot_n = n;
+  *d1 = ctx->pd1.p + ctx->pslot * n;
+  *d2 = ctx->pd2.p + ctx->pslot * n;
+  *idx = ctx->pidx.p + ctx->pslot * n;
+  if (!ctx->overlap) {
+    *ks = ctx->stream;
+    return SOD_OK;
+  }
+  *ks = ctx->mstream;
+  SOD_HIP(ctx, hipStreamWaitEvent(ctx->mstream, ctx->ev_inputs, 0));
+  SOD_HIP(ctx, hipStreamWaitEvent(ctx->mstream, ctx->ev_merged[ctx->pslot], 0));
+  // a new slot size moves the slots' boundaries: the other slot's last merge must be done too
+  if (resized) SOD_HIP(ctx, hipStreamWaitEvent(ctx->mstream, ctx->ev_merged[ctx->pslot ^ 1], 0));
+  return SOD_OK;
+}
+int sod_partials_merged(sod_ctx* ctx) {
+  SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[ctx->pslot], ctx->stream));
+  return SOD_OK;
+}
+int sod_match_stream_end(sod_ctx* ctx) {
+  const hipStream_t ks = ctx->overlap ? ctx->mstream : ctx->stream;
+  SOD_HIP(ctx, hipEventRecord(ctx->ev_matched, ks));
+  if (ctx->overlap) SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0));
+  return SOD_OK;
+}
+
 extern "C" {
 
 int sod_abi_version(void) { return 1; }
@@ -78,6 +125,11 @@ int sod_create(int device, sod_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->mstream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_inputs, hipEventDisableTiming);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i)
+    e = hipEventCreateWithFlags(&ctx->ev_merged[i], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_matched, hipEventDisableTiming);
   if (e != hipSuccess) {
     g_err = std::string("sod_create: ") + hipGetErrorString(e);
     delete ctx;
@@ -97,6 +149,7 @@ void sod_destroy(sod_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+  if (ctx->mstream) (void)hipStreamSynchronize(ctx->mstream);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   sod_sift_free(ctx);
@@ -126,6 +179,11 @@ void sod_destroy(sod_ctx* ctx) {
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->ev_inputs) (void)hipEventDestroy(ctx->ev_inputs);
+  for (auto& ev : ctx->ev_merged)
+    if (ev) (void)hipEventDestroy(ev);
+  if (ctx->ev_matched) (void)hipEventDestroy(ctx->ev_matched);
+  if (ctx->mstream) (void)hipStreamDestroy(ctx->mstream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -136,6 +194,7 @@ const char* sod_last_error(const sod_ctx* ctx) {
 
 int sod_synchronize(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return SOD_OK;
 }
@@ -201,12 +260,14 @@ static int upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
     dsrc = ctx->stage_f32.p;
   }
   SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p, 0, 4, ctx->stream));  // invalid count
+  SOD_TRY(sod_inputs_begin(ctx));
   if (ctx->impl != 0)
     SOD_TRY(launch_pack_i8(ctx, dsrc, dtype, n, db));
   else if (db)
     SOD_TRY(launch_pack_db(ctx, dsrc, dtype, n));
   else
     SOD_TRY(launch_pack_queries(ctx, dsrc, dtype, (int32_t)n));
+  SOD_TRY(sod_inputs_end(ctx));
   uint32_t bad = 0;
   SOD_HIP(ctx, hipMemcpyAsync(&bad, ctx->flags.p, 4, hipMemcpyDeviceToHost, ctx->stream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -343,6 +404,7 @@ int sod_db_import_packed(sod_ctx* ctx, const void* in, int64_t bytes) {
       bytes < (int64_t)sizeof(h) + h.nsub * h.sub_bytes + h.norm_bytes)
     return sod_fail(ctx, SOD_EINVAL, "inconsistent packed DB image");
   const uint8_t* src = static_cast<const uint8_t*>(in) + sizeof(h);
+  SOD_TRY(sod_inputs_begin(ctx));
   SOD_TRY(sod_reserve(ctx, ctx->dbpack, (size_t)(h.nsub * h.sub_bytes)));
   SOD_TRY(sod_reserve(ctx, ctx->dn, (size_t)(h.norm_bytes / 4)));
   SOD_HIP(ctx, hipMemcpyAsync(ctx->dbpack.p, src, (size_t)(h.nsub * h.sub_bytes),
@@ -350,6 +412,7 @@ int sod_db_import_packed(sod_ctx* ctx, const void* in, int64_t bytes) {
   SOD_HIP(ctx, hipMemcpyAsync(ctx->dn.p, src + h.nsub * h.sub_bytes, (size_t)h.norm_bytes,
                               hipMemcpyHostToDevice, ctx->stream));
   SOD_HIP(ctx, hipMemcpyAsync(ctx->flags.p + 1, &h.max_norm, 4, hipMemcpyHostToDevice, ctx->stream));
+  SOD_TRY(sod_inputs_end(ctx));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->nsub = h.nsub;
   ctx->n_shard = h.n_rows;
@@ -445,6 +508,16 @@ int sod_match_enqueue(sod_ctx* ctx) {
   SOD_TRY(ctx->impl != 0 ? launch_match_i8(ctx) : launch_match(ctx));
   ctx->matched = true;
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  return SOD_OK;
+}
+
+int sod_match_set_overlap(sod_ctx* ctx, int on) {
+  SOD_TRY(set_dev(ctx));
+  if (on != 0 && on != 1) return sod_fail(ctx, SOD_EINVAL, "overlap must be 0 or 1");
+  // everything enqueued so far, on either stream, is ordered before the switch
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->overlap = on != 0;
   return SOD_OK;
 }
 

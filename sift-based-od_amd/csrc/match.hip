@@ -402,21 +402,23 @@ int launch_match(sod_ctx* ctx) {
   const int64_t st_per_split = ceil_div(nstages, split);
   split = ceil_div(nstages, st_per_split);
   ctx->split = (int)split;
-  SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(split * nq_pad)));
-  SOD_TRY(sod_reserve(ctx, ctx->pd2, (size_t)(split * nq_pad)));
-  SOD_TRY(sod_reserve(ctx, ctx->pidx, (size_t)(split * nq_pad)));
   SOD_TRY(sod_reserve(ctx, ctx->cd1, (size_t)nq_pad));
   SOD_TRY(sod_reserve(ctx, ctx->cd2, (size_t)nq_pad));
   SOD_TRY(sod_reserve(ctx, ctx->cidx, (size_t)nq_pad));
   const int64_t grid = qblocks * split;
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
-  hipLaunchKernelGGL(match_kernel, dim3((unsigned)grid), dim3(NT), 0, ctx->stream,
+  hipStream_t ks;   // context stream, or the matcher's (sod_match_set_overlap)
+  float *pd1, *pd2;
+  int32_t* pidx;
+  SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ks));
+  hipLaunchKernelGGL(match_kernel, dim3((unsigned)grid), dim3(NT), 0, ks,
                      ctx->dbpack.p, ctx->dn.p, ctx->nsub, ctx->qpack.p, ctx->qn.p, ctx->nqt,
-                     nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset, ctx->pd1.p,
-                     ctx->pidx.p, ctx->pd2.p);
+                     nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset, pd1, pidx, pd2);
   SOD_HIP(ctx, hipGetLastError());
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
-  return launch_merge(ctx, ctx->pd1.p, ctx->pidx.p, ctx->pd2.p, (int)split, nq_pad);
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ks));
+  SOD_TRY(sod_match_stream_end(ctx));
+  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad));
+  return sod_partials_merged(ctx);   // the slot is free again
 }
 
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2, int nparts,

@@ -851,26 +851,29 @@ int launch_match_i8(sod_ctx* ctx) {
   const int64_t st_per_split = cdiv(nstages, split);
   split = cdiv(nstages, st_per_split);
   ctx->split = (int)split;
-  SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(split * nq_pad)));
-  SOD_TRY(sod_reserve(ctx, ctx->pd2, (size_t)(split * nq_pad)));
-  SOD_TRY(sod_reserve(ctx, ctx->pidx, (size_t)(split * nq_pad)));
   SOD_TRY(sod_reserve(ctx, ctx->cd1, (size_t)nq_pad));
   SOD_TRY(sod_reserve(ctx, ctx->cd2, (size_t)nq_pad));
   SOD_TRY(sod_reserve(ctx, ctx->cidx, (size_t)nq_pad));
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+  hipStream_t ks;   // context stream, or the matcher's (sod_match_set_overlap)
+  float *pd1, *pd2;
+  int32_t* pidx;
+  SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ks));
   if (wide)
     hipLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0,
-                       ctx->stream, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
+                       ks, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
                        ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt,
-                       nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, ctx->pd1.p,
-                       ctx->pidx.p, ctx->pd2.p, (int)qblocks);
+                       nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, pd1,
+                       pidx, pd2, (int)qblocks);
   else
-    hipLaunchKernelGGL(match_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(NT16), 0, ctx->stream,
+    hipLaunchKernelGGL(match_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(NT16), 0, ks,
                        ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,
                        ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,
-                       (int)split, st_per_split * sps, (int)ctx->row_offset, ctx->pd1.p,
-                       ctx->pidx.p, ctx->pd2.p, (int)qblocks);
+                       (int)split, st_per_split * sps, (int)ctx->row_offset, pd1,
+                       pidx, pd2, (int)qblocks);
   SOD_HIP(ctx, hipGetLastError());
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
-  return launch_merge(ctx, ctx->pd1.p, ctx->pidx.p, ctx->pd2.p, (int)split, nq_pad);
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ks));
+  SOD_TRY(sod_match_stream_end(ctx));
+  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad));
+  return sod_partials_merged(ctx);   // the slot is free again
 }

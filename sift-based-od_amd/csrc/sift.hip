@@ -1478,9 +1478,13 @@ int sod_sift_to_queries(sod_ctx* ctx) {
   if (nq64 > (1 << 27)) return sod_fail(ctx, SOD_EINVAL, "query count out of range");
   const int32_t nq = (int32_t)nq64;
   SOD_TRY(sod_reserve(ctx, ctx->flags, 4));
-  SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p, 0, 12, ctx->stream));
+  // invalid-value count and the query max norm (flags[1], the DB's, stays)
+  SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p, 0, 4, ctx->stream));
+  SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p + 2, 0, 4, ctx->stream));
+  SOD_TRY(sod_inputs_begin(ctx));
   SOD_TRY(ctx->impl != 0 ? launch_pack_i8(ctx, W->all_desc.p, SOD_DTYPE_F32, nq, false)
                          : launch_pack_queries(ctx, W->all_desc.p, SOD_DTYPE_F32, nq));
+  SOD_TRY(sod_inputs_end(ctx));
   SOD_TRY(sod_reserve(ctx, ctx->qx, (size_t)nq));
   SOD_TRY(sod_reserve(ctx, ctx->qy, (size_t)nq));
   SOD_TRY(sod_reserve(ctx, ctx->qang, (size_t)nq));

@@ -139,6 +139,15 @@ struct sod_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool side_pending = false;    // main stream has not yet waited for the side work
 
+  // ---- matcher stream (sod_match_set_overlap): the match kernel runs there and waits only
+  // for the last input upload (ev_inputs) and for the merge that last read its partial-result
+  // slot (two slots alternate: ev_merged[slot])
+  hipStream_t mstream = nullptr;
+  hipEvent_t ev_inputs = nullptr, ev_matched = nullptr, ev_merged[2] = {nullptr, nullptr};
+  bool overlap = false;
+  int pslot = 0;                // partial-result slot of the last matcher launch
+  int64_t pslot_n = 0;          // its size (elements per array)
+
   // ---- timing ----
   hipEvent_t ev[8] = {};
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -202,6 +211,16 @@ int launch_pack_queries(sod_ctx* ctx, const void* dsrc, int dtype, int32_t nq);
 int launch_match(sod_ctx* ctx);
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db);
 int launch_match_i8(sod_ctx* ctx);
+// matcher-input writers call these around their writes; the match launchers around the
+// kernel (see sod_ctx::mstream)
+int sod_inputs_begin(sod_ctx* ctx);
+int sod_inputs_end(sod_ctx* ctx);
+// the next matcher launch: its stream and partial-result slot (n elements per array);
+// then, after the kernel, the context stream's wait, and after the merge the slot release
+int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1, int32_t** idx,
+                           float** d2);
+int sod_match_stream_end(sod_ctx* ctx);
+int sod_partials_merged(sod_ctx* ctx);
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2,
                  int nparts, int64_t stride);
 int launch_ratio(sod_ctx* ctx, double ratio);

@@ -280,3 +280,49 @@ def test_shared_db_contexts():
     for k in ("keys", "votes", "offsets", "members"):
         assert np.array_equal(ref_b[1][k], got_b[1][k])
     np.testing.assert_array_equal(ref_b[2]["params"], got_b[2]["params"])
+
+
+@pytest.mark.parametrize("use_comm", [False, True])
+def test_matcher_overlap_equals_serial(use_comm):
+    """sod_match_set_overlap: the matcher kernel on its own stream, overlapping the previous
+    query's Hough / select / affine stages (several pipelines enqueued back to back, a new
+    query upload in between, optionally a 1-rank RCCL communicator on the context stream) --
+    every result equals the serial context's bit for bit."""
+    db = synthetic.make_database(30, 1000, seed=51)
+    qsets = [synthetic.make_queries(5000, seed=52 + k, db_seed=51, kp_per_image=1000)
+             for k in range(2)]
+    bins = (32, 32, 8, 12)
+
+    def collect(c):
+        return (c.match_result(), c.valid_result(), c.affine_result(), c.all_bins())
+
+    ref = []
+    with _lib.Context(0) as c:
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        for qs in qsets:
+            c.upload_queries(qs.des, qs.kp)
+            c.pipeline(qs.shape, bins)
+            ref.append(collect(c))
+    with _lib.Context(0) as c:
+        if use_comm:
+            c.comm_init(1, 0, _lib.unique_id())
+        c.set_overlap(True)
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        got = []
+        for qs in qsets:
+            c.upload_queries(qs.des, qs.kp)
+            for _ in range(3):                  # back to back: matcher k+1 beside tail k
+                c.pipeline(qs.shape, bins)
+            c.synchronize()
+            got.append(collect(c))
+        c.set_overlap(False)
+    for (m0, v0, a0, b0), (m1, v1, a1, b1) in zip(ref, got):
+        for x, y in zip(m0, m1):
+            assert np.array_equal(x, y)
+        for k in ("keys", "votes", "offsets", "members", "means"):
+            assert np.array_equal(v0[k], v1[k]), k
+        assert np.array_equal(b0[0], b1[0]) and np.array_equal(b0[1], b1[1])
+        assert np.array_equal(a0["survived"], a1["survived"])
+        assert np.array_equal(a0["params"], a1["params"])
