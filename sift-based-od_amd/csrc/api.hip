@@ -74,7 +74,11 @@ int sod_inputs_end(sod_ctx* ctx) {
 int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1, int32_t** idx,
                            float** d2) {
   const int nslot = ctx->overlap ? 2 : 1;
-  SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(nslot * n)));   // (a reallocation syncs the device)
+  if (ctx->pd1.n < (size_t)(nslot * n)) {   // growing: no kernel or merge may still use them
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
+    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(nslot * n)));
   SOD_TRY(sod_reserve(ctx, ctx->pd2, (size_t)(nslot * n)));
   SOD_TRY(sod_reserve(ctx, ctx->pidx, (size_t)(nslot * n)));
   const bool resized = n != ctx->pslot_n;
