@@ -74,6 +74,10 @@ def parse():
                    help="matcher kernel on a stream of its own, overlapping the previous query "
                         "image's Hough/select/affine stages inside ONE context (collectives "
                         "stay on the context stream).  Default: on with several ranks")
+    p.add_argument("--cu-reserve", type=int, default=-1,
+                   help="CUs per XCD kept off the matcher for the other stages and the RCCL "
+                        "exchanges (sod_set_cu_reserve; implies --overlap 1).  Default: 1 "
+                        "(0 with --contexts > 1 or --overlap 0)")
     p.add_argument("--impl", default="i8", choices=sorted(IMPLS),
                    help="matcher kernel: int8 MFMA 16x16x64 (default, fastest), int8 32x32x32 "
                         "or bf16 MFMA; all bit-exact")
@@ -130,6 +134,12 @@ class Dist:
         t = torch.tensor([float(x)], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
+
+
+def _dbg(tag):
+    if os.environ.get("SOD_DEBUG"):
+        import ctypes
+        print("DBG", tag, ctypes.CDLL("libamdhip64.so").hipGetLastError(), flush=True)
 
 
 def device_sync(world, dev):
@@ -345,14 +355,22 @@ def main():
     ctx.upload_db(shard, row_offset=rank * n_shard)
     ctx.upload_queries(qs.des, qs.kp)
     from sift_based_od_amd.sharded import RcclComm, TorchHostComm, run_sharded
+    reserve = a.cu_reserve if a.cu_reserve >= 0 else (0 if a.contexts > 1 or a.overlap == 0
+                                                       else 1)
     comm = None
     if world > 1 and a.comm == "rccl":
+        if reserve:
+            # the collectives run on the reserved CUs (8 * reserve): at most that many
+            # channels, so every block of an RCCL kernel is resident at once
+            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(8 * reserve))
         comm = RcclComm(ctx, world, rank, D.bcast_bytes)
     elif world > 1:
         comm = TorchHostComm()
     own = (rank * n_shard, (rank + 1) * n_shard)
-    overlap = a.overlap if a.overlap >= 0 else (1 if world > 1 else 0)
+    overlap = a.overlap if a.overlap >= 0 else (1 if world > 1 or reserve else 0)
     ctx.set_overlap(bool(overlap))
+    if reserve:
+        ctx.set_cu_reserve(reserve)
     ncontexts = a.contexts if a.contexts > 0 else (2 if world == 1 and not overlap else 1)
     ctxs = [ctx]
     for _ in range(ncontexts - 1):
@@ -377,12 +395,14 @@ def main():
         for c in ctxs:
             c.synchronize()
 
+    _dbg("before warmup")
     for _ in range(a.warmup):
         step()
+        _dbg("warmup step")
     sync_all()
 
     # ---- timed region ----------------------------------------------------------------
-    match_ms, stage = [], []
+    stage = []
     D.barrier()
     sync_all()
     device_sync(world, dev)
@@ -395,16 +415,30 @@ def main():
     t1 = time.perf_counter()
     el = D.max(t1 - t0)
     ms_per_step = 1000.0 * el / a.steps
+    _dbg("after timed")
 
-    # ---- per-kernel timing (HIP events on the ctx stream), separate untimed steps -------
+    # ---- matcher kernel time inside the timed region: begin/end HIP events recorded around
+    # every launch on the matcher's own stream (sod_match_times), read back afterwards ----
+    live = []
+    for k, c in enumerate(ctxs):
+        n_k = len(range(k, a.steps, ncontexts))      # timed launches of context k
+        if n_k:
+            live.extend(c.match_times(min(n_k, 64)).tolist())
+    match_ms = float(np.mean(live))
+    _dbg("after match_times")
+
+    # ---- per-stage timing (HIP events on the ctx stream), separate untimed steps --------
+    match_iso = []
     for _ in range(max(3, min(a.steps, 10))):
         turn[0] = 0            # always the first context (its events are read below)
         step()
         ctx.synchronize()
-        match_ms.append(ctx.last_match_ms())
+        match_iso.append(ctx.last_match_ms())
         stage.append(ctx.stage_ms())
-    match_ms = float(np.mean(match_ms))
+    match_iso = float(np.mean(match_iso))
     stage = np.mean(np.array(stage), axis=0)
+    if reserve:
+        ctx.set_cu_reserve(0)      # post-processing and extras below on the whole chip
 
     # post-processing (main.py:159-168) over the surviving bins: timed
     # separately (it ends in a host DFS, so it is not inside the stream-ordered step)
@@ -449,6 +483,7 @@ def main():
             "queries": nq, "db_rows_per_gpu": n_shard, "db_rows_total": world * n_shard,
             "bins": list(bins), "parallelism": "db-shard%d" % world,
             "query_streams": ncontexts, "matcher_overlap": bool(overlap),
+            "cu_reserve_per_xcd": reserve,
             "comm": a.comm if world > 1 else None},
         "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
         "hough_stage_votes_per_s": n_votes / ((float(stage[2]) + float(stage[3])) / 1000.0),
@@ -456,7 +491,7 @@ def main():
         "good_matches": int(good.sum()),
         "valid_bins": V,
         "surviving_bins": int(aff["survived"].sum()) if aff else None,
-        "stage_ms": {"match_kernel": match_ms, "merge_gather_ratio": float(stage[1]),
+        "stage_ms": {"match_kernel": match_ms, "match_kernel_isolated": match_iso, "merge_gather_ratio": float(stage[1]),
                      "hough_vote": float(stage[2]), "select": float(stage[3]),
                      "affine": float(stage[4]), "post_process": post_ms},
         "final_poses": int(len(post["final_pose"])) if post is not None else None,

@@ -52,6 +52,10 @@ int sod_synchronize(sod_ctx* ctx);
 /* Kernel timing of the last enqueued matcher launch (ms), measured with HIP events on
  * the ctx stream; and the launch geometry used. */
 int sod_last_match_ms(sod_ctx* ctx, float* ms);
+/* Kernel times (ms) of the last n matcher launches, oldest first (n <= 64 and <= launches
+ * so far), from begin/end HIP events recorded on the matcher's stream around each launch:
+ * the kernel timed inside a pipelined run.  Waits for those launches. */
+int sod_match_times(sod_ctx* ctx, int n, float* ms);
 int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n); /* match,merge,hough,select,affine */
 
 /* ---- database (replaces main.py:36-66 flattening + GenerateDatabaseInfo.py format) --
@@ -116,6 +120,14 @@ int sod_match_set_impl(sod_ctx* ctx, int impl);
  * the previous query's Hough / select / affine stages, which stay on the context stream in
  * order (RCCL collectives included).  Results are unchanged. */
 int sod_match_set_overlap(sod_ctx* ctx, int on);
+/* Split the CUs: the matcher stream keeps all but `per_xcd` CUs of every XCD, the context
+ * and side streams (Hough / select / affine, merges, RCCL collectives, memsets) run on those
+ * reserved CUs, so one query's tail stages run beside the next query's matcher instead of
+ * being starved by it.  Implies sod_match_set_overlap(ctx, 1); 0 restores unmasked streams.
+ * Meant for streaming query batches through sod_pipeline_enqueue: every other entry point on
+ * the context stream (SIFT, uploads) also runs on the reserved CUs while it is set.
+ * Results are unchanged.  (No reference counterpart: an MI355X scheduling knob.) */
+int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd);
 /* multi-GPU: RCCL all-gather of every rank's per-query (d1^2, idx1, d2^2) and the
  * global merge.  No-op on a single rank. */
 int sod_match_allgather_enqueue(sod_ctx* ctx);

@@ -46,6 +46,7 @@ SIGNATURES = {
     "sod_last_error": (C.c_char_p, [c_ctx]),
     "sod_synchronize": (C.c_int, [c_ctx]),
     "sod_last_match_ms": (C.c_int, [c_ctx, c_f32p]),
+    "sod_match_times": (C.c_int, [c_ctx, C.c_int, c_f32p]),
     "sod_last_stage_ms": (C.c_int, [c_ctx, c_f32p, C.c_int]),
     "sod_db_set_keypoints": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_i32p,
                                        C.c_int32, c_f64p, c_i32p]),
@@ -62,6 +63,7 @@ SIGNATURES = {
     "sod_match_enqueue": (C.c_int, [c_ctx]),
     "sod_match_set_impl": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_set_overlap": (C.c_int, [c_ctx, C.c_int]),
+    "sod_set_cu_reserve": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
     "sod_ratio_enqueue": (C.c_int, [c_ctx, C.c_double]),
     "sod_match_get": (C.c_int, [c_ctx, c_i32p, c_f32p, c_f32p, c_u8p]),
@@ -259,6 +261,12 @@ class Context:
         one's Hough / select / affine stages (sod_match_set_overlap); results unchanged."""
         self._chk(self._L.sod_match_set_overlap(self._h, 1 if on else 0))
 
+    def set_cu_reserve(self, per_xcd=1):
+        """Run the matcher on all but `per_xcd` CUs of every XCD and the other stages (and
+        RCCL exchanges) on those, so a query's tail overlaps the next matcher instead of
+        being starved by it (sod_set_cu_reserve; implies set_overlap).  0 undoes it."""
+        self._chk(self._L.sod_set_cu_reserve(self._h, int(per_xcd)))
+
     # -- stages --
     def match(self):
         self._chk(self._L.sod_match_enqueue(self._h))
@@ -355,6 +363,12 @@ class Context:
         v = C.c_float()
         self._chk(self._L.sod_last_match_ms(self._h, C.byref(v)))
         return v.value
+
+    def match_times(self, n):
+        """Kernel times (ms) of the last n matcher launches, oldest first (n <= 64)."""
+        out = np.zeros(int(n), np.float32)
+        self._chk(self._L.sod_match_times(self._h, int(n), ptr(out, C.c_float)))
+        return out
 
     def stage_ms(self):
         out = np.zeros(5, np.float32)

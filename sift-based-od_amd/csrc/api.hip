@@ -98,6 +98,16 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
   if (resized) SOD_HIP(ctx, hipStreamWaitEvent(ctx->mstream, ctx->ev_merged[ctx->pslot ^ 1], 0));
   return SOD_OK;
 }
+int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end) {
+  hipEvent_t& e = ctx->mev[ctx->nmatch % sod_ctx::kMatchRing][end];
+  if (!e) SOD_HIP(ctx, hipEventCreate(&e));
+  SOD_HIP(ctx, hipEventRecord(e, ks));
+  // ev[0] / ev[1] also bound the matcher for sod_last_stage_ms (stage 0, and stage 1 starts
+  // at ev[1])
+  SOD_HIP(ctx, hipEventRecord(ctx->ev[end], ks));
+  if (end) ++ctx->nmatch;
+  return SOD_OK;
+}
 int sod_partials_merged(sod_ctx* ctx) {
   SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[ctx->pslot], ctx->stream));
   return SOD_OK;
@@ -180,6 +190,9 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->hist_rng); sod_release(ctx->bwh);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& pr : ctx->mev)
+    for (auto& e : pr)
+      if (e) (void)hipEventDestroy(e);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -207,8 +220,20 @@ int sod_last_match_ms(sod_ctx* ctx, float* ms) {
   SOD_TRY(set_dev(ctx));
   if (!ms) return sod_fail(ctx, SOD_EINVAL, "null output");
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "no matcher launch yet");
-  SOD_HIP(ctx, hipEventSynchronize(ctx->ev[1]));
-  SOD_HIP(ctx, hipEventElapsedTime(ms, ctx->ev[0], ctx->ev[1]));
+  return sod_match_times(ctx, 1, ms);
+}
+
+int sod_match_times(sod_ctx* ctx, int n, float* ms) {
+  SOD_TRY(set_dev(ctx));
+  if (!ms || n < 1) return sod_fail(ctx, SOD_EINVAL, "need n >= 1 and an output array");
+  if (n > sod_ctx::kMatchRing || n > ctx->nmatch)
+    return sod_fail(ctx, SOD_EINVAL, "fewer matcher launches recorded than requested");
+  for (int i = 0; i < n; ++i) {
+    const int64_t k = ctx->nmatch - n + i;
+    hipEvent_t* e = ctx->mev[k % sod_ctx::kMatchRing];
+    SOD_HIP(ctx, hipEventSynchronize(e[1]));
+    SOD_HIP(ctx, hipEventElapsedTime(&ms[i], e[0], e[1]));
+  }
   return SOD_OK;
 }
 
@@ -221,8 +246,10 @@ int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n) {
                        ctx->affined};
   for (int i = 0; i < n && i < 5; ++i) {
     float ms = 0.f;
-    if (rec[i] && rec[i + 1] && hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) != hipSuccess)
+    if (rec[i] && rec[i + 1] && hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) != hipSuccess) {
       ms = 0.f;
+      (void)hipGetLastError();   // not sticky: the next launch check must not see it
+    }
     ms_out[i] = ms;
   }
   return SOD_OK;
@@ -521,7 +548,60 @@ int sod_match_set_overlap(sod_ctx* ctx, int on) {
   // everything enqueued so far, on either stream, is ordered before the switch
   SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (!on && ctx->cu_reserve)
+    return sod_fail(ctx, SOD_ESTATE, "the CU split (sod_set_cu_reserve) needs the matcher stream");
   ctx->overlap = on != 0;
+  return SOD_OK;
+}
+
+// Split the chip between the matcher and everything else (SURVEY 8(e)/(f) overlap): a
+// kernel enqueued while the matcher holds every CU gets its waves placed beside the
+// matcher's and finishes only when the matcher does, so a step's Hough / select / affine
+// stages (and, with several ranks, the RCCL exchanges) would serialise with the next
+// matcher.  With per_xcd > 0 the context and side streams are re-created on `per_xcd` CUs
+// of every XCD (CU-mask bits num_cus-8*per_xcd .. num_cus-1: bit i lies on XCD i % 8,
+// measured with tools/cu_mask_probe.hip) and the matcher stream on the rest; the matcher
+// grid is sized for the CUs it keeps.  Implies sod_match_set_overlap(ctx, 1).  0 restores
+// unmasked streams.  Results are unchanged.
+static hipError_t make_stream(hipStream_t* s, const std::vector<uint32_t>& mask) {
+  if (mask.empty()) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size() * 32, mask.data());
+}
+
+int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
+  SOD_TRY(set_dev(ctx));
+  const int nx = 8;   // XCDs on an MI355X
+  if (per_xcd < 0 || (per_xcd > 0 && (ctx->num_cus % nx != 0 || per_xcd * nx * 2 > ctx->num_cus)))
+    return sod_fail(ctx, SOD_EINVAL, "cu reserve per XCD must be in [0, CUs per XCD / 2]");
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->side));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->side_pending = false;
+  const int n = ctx->num_cus, words = (n + 31) / 32, r = per_xcd * nx;
+  std::vector<uint32_t> tail, match;
+  if (per_xcd > 0) {
+    tail.assign(words, 0u);
+    match.assign(words, 0u);
+    for (int i = 0; i < n; ++i) (i >= n - r ? tail : match)[i / 32] |= 1u << (i % 32);
+  }
+  hipStream_t s = nullptr, sd = nullptr, ms = nullptr;
+  hipError_t e = make_stream(&s, tail);
+  if (e == hipSuccess) e = make_stream(&sd, tail);
+  if (e == hipSuccess) e = make_stream(&ms, match);
+  if (e != hipSuccess) {
+    if (s) (void)hipStreamDestroy(s);
+    if (sd) (void)hipStreamDestroy(sd);
+    return sod_fail(ctx, SOD_EHIP, std::string("cu reserve: ") + hipGetErrorString(e));
+  }
+  (void)hipStreamDestroy(ctx->stream);
+  (void)hipStreamDestroy(ctx->side);
+  (void)hipStreamDestroy(ctx->mstream);
+  ctx->stream = s;
+  ctx->side = sd;
+  ctx->mstream = ms;
+  ctx->cu_reserve = per_xcd;
+  ctx->reserved_cus = r;
+  if (per_xcd > 0) ctx->overlap = true;
   return SOD_OK;
 }
 

@@ -581,6 +581,70 @@ __device__ void block_scan_lds(uint32_t* a, int n, uint32_t* part) {
   __syncthreads();
 }
 
+// Small bins (the great majority: a few to a few dozen members) take a wave of their own:
+// each query votes a bin at most once, so query order is ascending order, and up to
+// kWaveCap members sort in registers (bitonic, kWaveE per lane, cross-lane stages by
+// shuffles) -- no LDS, no barriers, so the kernel stays fast on the few CUs a reserved
+// tail gets (sod_set_cu_reserve).  Also resets the bin -> valid index map of EVERY valid
+// bin; member_order_kernel then takes the bins above kWaveCap.
+constexpr int kWaveE = 4;
+constexpr int kWaveCap = 64 * kWaveE;
+
+template <int J>
+__device__ __forceinline__ void wave_sort_reg(uint32_t (&a)[kWaveE], int lane, int k) {
+#pragma unroll
+  for (int r = 0; r < kWaveE; ++r) {
+    if (r & J) continue;
+    const bool asc = ((lane * kWaveE + r) & k) == 0;
+    const uint32_t x = a[r], y = a[r | J];
+    const bool sw = asc ? (x > y) : (x < y);
+    a[r] = sw ? y : x;
+    a[r | J] = sw ? x : y;
+  }
+}
+
+__global__ __launch_bounds__(256) void member_order_small_kernel(
+    const uint32_t* __restrict__ scal, const uint32_t* __restrict__ vbin,
+    const int64_t* __restrict__ voff, uint32_t* __restrict__ vidx,
+    int32_t* __restrict__ members) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t V = scal[0];
+  for (int64_t v = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < V;
+       v += nwaves) {
+    const int64_t a0 = voff[v];
+    const int n = (int)(voff[v + 1] - a0);
+    if (lane == 0) vidx[vbin[v]] = 0xFFFFFFFFu;
+    if (n <= 1 || n > kWaveCap) continue;                     // uniform over the wave
+    uint32_t a[kWaveE];
+#pragma unroll
+    for (int r = 0; r < kWaveE; ++r) {
+      const int i = lane * kWaveE + r;
+      a[r] = i < n ? (uint32_t)members[a0 + i] : 0xFFFFFFFFu;
+    }
+    int p = kWaveE;
+    while (p < n) p <<= 1;
+    for (int k = 2; k <= p; k <<= 1) {
+      for (int j = k >> 1; j >= kWaveE; j >>= 1) {            // partner in lane ^ (j / E)
+#pragma unroll
+        for (int r = 0; r < kWaveE; ++r) {
+          const uint32_t o = __shfl_xor(a[r], j / kWaveE);
+          const int i = lane * kWaveE + r;
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          a[r] = keep_min ? min(a[r], o) : max(a[r], o);
+        }
+      }
+      if (k >= 4) wave_sort_reg<2>(a, lane, k);
+      wave_sort_reg<1>(a, lane, k);
+    }
+#pragma unroll
+    for (int r = 0; r < kWaveE; ++r) {
+      const int i = lane * kWaveE + r;
+      if (i < n) members[a0 + i] = (int32_t)a[r];
+    }
+  }
+}
+
 __global__ __launch_bounds__(kOrderT) void member_order_kernel(const uint32_t* __restrict__ scal,
                                                                const uint32_t* __restrict__ vbin,
                                                                const int64_t* __restrict__ voff,
@@ -595,8 +659,8 @@ __global__ __launch_bounds__(kOrderT) void member_order_kernel(const uint32_t* _
   for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
     const int64_t a = voff[v];
     const int n = (int)(voff[v + 1] - a);
-    if (threadIdx.x == 0) vidx[vbin[v]] = 0xFFFFFFFFu;
-    if (n <= 1 || n > kOrderCap || nblk > kOrderCap) continue;   // uniform over the group
+    // (bins up to kWaveCap: member_order_small_kernel, which also reset vidx)
+    if (n <= kWaveCap || n > kOrderCap || nblk > kOrderCap) continue;   // uniform over the group
     for (int i = threadIdx.x; i < n; i += kOrderT) key[i] = (uint32_t)members[a + i];
     for (int i = threadIdx.x; i < nblk; i += kOrderT) tab[i] = 0;
     __syncthreads();
@@ -1063,11 +1127,15 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
                      ctx->vidx.p, ctx->voff.p, ctx->cursor.p, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   const int nblk = (int)cdiv(nq, kFillQ);
-  hipLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->num_cus * 2)), dim3(kOrderT), 0,
+  hipLaunchKernelGGL(member_order_small_kernel, dim3(std::max(1, ctx->tail_cus() * 8)), dim3(256),
+                     0, ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, ctx->vidx.p,
+                     ctx->members.p);
+  SOD_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->tail_cus() * 2)), dim3(kOrderT), 0,
                      ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, nblk, ctx->vidx.p,
                      ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  const int wg = std::max(1, ctx->num_cus * 4);
+  const int wg = std::max(1, ctx->tail_cus() * 4);
   hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
                      ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
                      ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, nblk, ctx->members.p);
@@ -1078,14 +1146,14 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   SOD_TRY(sod_reserve(ctx, ctx->rtab, (size_t)ctx->mmax));
   SOD_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
   SOD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-  hipLaunchKernelGGL(means_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
+  hipLaunchKernelGGL(means_gather_kernel, dim3(std::max(1, ctx->tail_cus() * 4)), dim3(256), 0,
                      ctx->side, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p + sod_win0(ctx),
                      ctx->mimg.p, ctx->isize.p, ctx->mmax, ctx->mq.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(recip_table_kernel, dim3(std::max(1, ctx->num_cus)), dim3(256), 0,
+  hipLaunchKernelGGL(recip_table_kernel, dim3(std::max(1, ctx->tail_cus())), dim3(256), 0,
                      ctx->side, ctx->scal.p, ctx->rtab.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->num_cus * 8)), dim3(64), 0, ctx->side,
+  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->tail_cus() * 8)), dim3(64), 0, ctx->side,
                      ctx->scal.p, ctx->voff.p, ctx->mq.p, ctx->mmax, ctx->rtab.p, ctx->means.p);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
@@ -1107,7 +1175,7 @@ int launch_affine_gather(sod_ctx* ctx) {
   SOD_TRY(sod_reserve(ctx, ctx->aqy, (size_t)ctx->mmax));
   SOD_TRY(sod_reserve(ctx, ctx->aisig, (size_t)ctx->vmax));
   if (ctx->n_qimg) SOD_TRY(sod_reserve(ctx, ctx->bwh, (size_t)ctx->vmax * 2));
-  hipLaunchKernelGGL(affine_gather_kernel, dim3(std::max(1, ctx->num_cus * 4)), dim3(256), 0,
+  hipLaunchKernelGGL(affine_gather_kernel, dim3(std::max(1, ctx->tail_cus() * 4)), dim3(256), 0,
                      ctx->stream, ctx->scal.p, ctx->members.p, ctx->idx1.p + sod_win0(ctx),
                      ctx->mx.p, ctx->my.p, ctx->qx.p + sod_win0(ctx), ctx->qy.p + sod_win0(ctx),
                      ctx->vbin.p, ctx_bins(ctx), ctx->nbins1, ctx->n_qimg ? ctx->qshape.p : nullptr,
@@ -1121,7 +1189,7 @@ int launch_affine(sod_ctx* ctx, int64_t nb_host, bool count_on_device, const int
                   const int32_t* isig, int32_t qw, int32_t qh, const int32_t* bwh, double xf,
                   double yf, int32_t thr, int32_t max_iter, const double* params_in, uint8_t* surv,
                   int32_t* votes, double* params, uint8_t* alive, const uint32_t* dev_count) {
-  const int wg = std::max(1, ctx->num_cus * 4);
+  const int wg = std::max(1, ctx->tail_cus() * 4);
   hipLaunchKernelGGL(affine_kernel, dim3(wg), dim3(256), 0, ctx->stream, nb_host,
                      count_on_device ? dev_count : nullptr, offsets, mx, my, qx, qy, isig, qw, qh,
                      bwh, xf, yf, thr, max_iter, params_in, surv, votes, params, alive);

@@ -395,7 +395,7 @@ int launch_match(sod_ctx* ctx) {
   const int64_t qblocks = ceil_div(ctx->nqt, qtiles_per_wg);
   const int64_t nstages = ctx->nsub / SPS;
   // fill every CU twice (2 workgroups of 4 waves per CU); each split >= 1 stage
-  int64_t target = 2LL * ctx->num_cus;
+  int64_t target = 2LL * ctx->match_cus();
   // (rounded down: one work-group more than the slots would run as a second round)
   int64_t split = std::max<int64_t>(1, target / qblocks);
   split = std::min<int64_t>(split, nstages);
@@ -410,12 +410,12 @@ int launch_match(sod_ctx* ctx) {
   float *pd1, *pd2;
   int32_t* pidx;
   SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ks));
+  SOD_TRY(sod_match_mark(ctx, ks, 0));
   hipLaunchKernelGGL(match_kernel, dim3((unsigned)grid), dim3(NT), 0, ks,
                      ctx->dbpack.p, ctx->dn.p, ctx->nsub, ctx->qpack.p, ctx->qn.p, ctx->nqt,
                      nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset, pd1, pidx, pd2);
   SOD_HIP(ctx, hipGetLastError());
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ks));
+  SOD_TRY(sod_match_mark(ctx, ks, 1));
   SOD_TRY(sod_match_stream_end(ctx));
   SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad));
   return sod_partials_merged(ctx);   // the slot is free again

@@ -844,7 +844,7 @@ int launch_match_i8(sod_ctx* ctx) {
   const int64_t nstages = ctx->nsub / sps;
   // one round of work-groups (8 waves per CU): as few DB chunks as fill the chip (every chunk
   // restarts each query's running top-2, so more chunks mean more slow-path updates)
-  const int64_t slots = ((wide ? w::NW : NW16) == 4 ? 2LL : 1LL) * ctx->num_cus;   // in flight
+  const int64_t slots = ((wide ? w::NW : NW16) == 4 ? 2LL : 1LL) * ctx->match_cus();   // in flight
   // (rounded down: one work-group more than the slots would run as a second round)
   int64_t split = std::max<int64_t>(1, slots / qblocks);
   split = std::min<int64_t>(split, nstages);
@@ -858,7 +858,7 @@ int launch_match_i8(sod_ctx* ctx) {
   float *pd1, *pd2;
   int32_t* pidx;
   SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[0], ks));
+  SOD_TRY(sod_match_mark(ctx, ks, 0));
   if (wide)
     hipLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0,
                        ks, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
@@ -872,7 +872,7 @@ int launch_match_i8(sod_ctx* ctx) {
                        (int)split, st_per_split * sps, (int)ctx->row_offset, pd1,
                        pidx, pd2, (int)qblocks);
   SOD_HIP(ctx, hipGetLastError());
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[1], ks));
+  SOD_TRY(sod_match_mark(ctx, ks, 1));
   SOD_TRY(sod_match_stream_end(ctx));
   SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad));
   return sod_partials_merged(ctx);   // the slot is free again

@@ -35,6 +35,9 @@ struct sod_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   int num_cus = 256;
+  // CUs the matcher kernel may use / the other stages run on (sod_set_cu_reserve)
+  int match_cus() const { return num_cus - reserved_cus; }
+  int tail_cus() const { return reserved_cus ? reserved_cus : num_cus; }
   int impl = 1;                 // matcher: 1 = int8 MFMA 16x16x64 (default), 2 = int8 32x32x32 (match_i8.hip), 0 = bf16 (match.hip)
 
   // ---- database (keypoints replicated, descriptors = shard) ----
@@ -145,11 +148,20 @@ struct sod_ctx {
   hipStream_t mstream = nullptr;
   hipEvent_t ev_inputs = nullptr, ev_matched = nullptr, ev_merged[2] = {nullptr, nullptr};
   bool overlap = false;
+  // sod_set_cu_reserve: the top `reserved_cus` CU-mask bits (cu_reserve per XCD, mask bit i
+  // is on XCD i % 8) run the context / side streams; the matcher stream gets the rest
+  int cu_reserve = 0;
+  int reserved_cus = 0;
   int pslot = 0;                // partial-result slot of the last matcher launch
   int64_t pslot_n = 0;          // its size (elements per array)
 
   // ---- timing ----
   hipEvent_t ev[8] = {};
+  // begin/end events of the last kMatchRing matcher launches (sod_match_times), so the
+  // kernel is timed inside a pipelined run, not only in isolated launches
+  static constexpr int kMatchRing = 64;
+  hipEvent_t mev[kMatchRing][2] = {};
+  int64_t nmatch = 0;
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 };
 
@@ -159,7 +171,8 @@ int sod_fail(sod_ctx* ctx, int code, const std::string& msg);
   do {                                                                              \
     hipError_t e_ = (call);                                                         \
     if (e_ != hipSuccess)                                                           \
-      return sod_fail((ctx), SOD_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+      return sod_fail((ctx), SOD_EHIP, std::string(#call) + ": " + hipGetErrorString(e_) + \
+                      " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")");              \
   } while (0)
 #define SOD_TRY(x)          \
   do {                      \
@@ -217,6 +230,8 @@ int sod_inputs_begin(sod_ctx* ctx);
 int sod_inputs_end(sod_ctx* ctx);
 // the next matcher launch: its stream and partial-result slot (n elements per array);
 // then, after the kernel, the context stream's wait, and after the merge the slot release
+// record the begin (end = 0) or end (end = 1) event of a matcher launch on stream ks
+int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end);
 int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1, int32_t** idx,
                            float** d2);
 int sod_match_stream_end(sod_ctx* ctx);

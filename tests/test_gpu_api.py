@@ -282,12 +282,14 @@ def test_shared_db_contexts():
     np.testing.assert_array_equal(ref_b[2]["params"], got_b[2]["params"])
 
 
-@pytest.mark.parametrize("use_comm", [False, True])
-def test_matcher_overlap_equals_serial(use_comm):
+@pytest.mark.parametrize("use_comm,reserve", [(False, 0), (True, 0), (False, 1), (True, 1)])
+def test_matcher_overlap_equals_serial(use_comm, reserve):
     """sod_match_set_overlap: the matcher kernel on its own stream, overlapping the previous
     query's Hough / select / affine stages (several pipelines enqueued back to back, a new
-    query upload in between, optionally a 1-rank RCCL communicator on the context stream) --
-    every result equals the serial context's bit for bit."""
+    query upload in between, optionally a 1-rank RCCL communicator on the context stream);
+    with `reserve` the chip is split by CU masks (sod_set_cu_reserve: matcher on all but one
+    CU per XCD, the other stages on those) -- every result equals the serial context's bit
+    for bit."""
     db = synthetic.make_database(30, 1000, seed=51)
     qsets = [synthetic.make_queries(5000, seed=52 + k, db_seed=51, kp_per_image=1000)
              for k in range(2)]
@@ -307,7 +309,10 @@ def test_matcher_overlap_equals_serial(use_comm):
     with _lib.Context(0) as c:
         if use_comm:
             c.comm_init(1, 0, _lib.unique_id())
-        c.set_overlap(True)
+        if reserve:
+            c.set_cu_reserve(reserve)
+        else:
+            c.set_overlap(True)
         c.set_keypoints(db.kp, db.img, db.centroid, db.size)
         c.upload_db(db.des)
         got = []
@@ -317,6 +322,12 @@ def test_matcher_overlap_equals_serial(use_comm):
                 c.pipeline(qs.shape, bins)
             c.synchronize()
             got.append(collect(c))
+        times = c.match_times(3)                # the last three launches, timed live
+        assert times.shape == (3,) and np.all(times > 0)
+        if reserve:
+            with pytest.raises(_lib.SodError):  # the split needs the matcher stream
+                c.set_overlap(False)
+            c.set_cu_reserve(0)
         c.set_overlap(False)
     for (m0, v0, a0, b0), (m1, v1, a1, b1) in zip(ref, got):
         for x, y in zip(m0, m1):
