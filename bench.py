@@ -77,7 +77,8 @@ def parse():
     p.add_argument("--cu-reserve", type=int, default=-1,
                    help="CUs per XCD kept off the matcher for the other stages and the RCCL "
                         "exchanges (sod_set_cu_reserve; implies --overlap 1).  Default: 1 "
-                        "(0 with --contexts > 1 or --overlap 0)")
+                        "when the matcher dominates a step (>= 1e10 pairs per GPU), else 0 "
+                        "(and 0 with --contexts > 1 or --overlap 0)")
     p.add_argument("--impl", default="i8", choices=sorted(IMPLS),
                    help="matcher kernel: int8 MFMA 16x16x64 (default, fastest), int8 32x32x32 "
                         "or bf16 MFMA; all bit-exact")
@@ -134,12 +135,6 @@ class Dist:
         t = torch.tensor([float(x)], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
-
-
-def _dbg(tag):
-    if os.environ.get("SOD_DEBUG"):
-        import ctypes
-        print("DBG", tag, ctypes.CDLL("libamdhip64.so").hipGetLastError(), flush=True)
 
 
 def device_sync(world, dev):
@@ -355,8 +350,10 @@ def main():
     ctx.upload_db(shard, row_offset=rank * n_shard)
     ctx.upload_queries(qs.des, qs.kp)
     from sift_based_od_amd.sharded import RcclComm, TorchHostComm, run_sharded
-    reserve = a.cu_reserve if a.cu_reserve >= 0 else (0 if a.contexts > 1 or a.overlap == 0
-                                                       else 1)
+    # auto: split the chip when the matcher dominates a step (C3 / C5: ~4 ms against a
+    # ~1.3 ms tail on the 8 reserved CUs); C2's 0.2 ms matcher would wait on that tail
+    reserve = a.cu_reserve if a.cu_reserve >= 0 else (
+        0 if a.contexts > 1 or a.overlap == 0 or nq * shard.shape[0] < 10 ** 10 else 1)
     comm = None
     if world > 1 and a.comm == "rccl":
         if reserve:
@@ -395,10 +392,8 @@ def main():
         for c in ctxs:
             c.synchronize()
 
-    _dbg("before warmup")
     for _ in range(a.warmup):
         step()
-        _dbg("warmup step")
     sync_all()
 
     # ---- timed region ----------------------------------------------------------------
@@ -415,7 +410,6 @@ def main():
     t1 = time.perf_counter()
     el = D.max(t1 - t0)
     ms_per_step = 1000.0 * el / a.steps
-    _dbg("after timed")
 
     # ---- matcher kernel time inside the timed region: begin/end HIP events recorded around
     # every launch on the matcher's own stream (sod_match_times), read back afterwards ----
@@ -425,7 +419,6 @@ def main():
         if n_k:
             live.extend(c.match_times(min(n_k, 64)).tolist())
     match_ms = float(np.mean(live))
-    _dbg("after match_times")
 
     # ---- per-stage timing (HIP events on the ctx stream), separate untimed steps --------
     match_iso = []
@@ -507,7 +500,14 @@ def main():
         "datagen_s": gen_s,
     }
     if world == 1 and not a.no_extras:
-        out["extras"] = extras(ctxs[-1], ctx, shard, bins)
+        # on a context of their own (sharing the resident DB): ctx keeps the timed run's
+        # results for the CPU baselines below
+        ec = ctxs[-1]
+        if ec is ctx:
+            ec = _lib.Context(dev)
+            ec.set_impl(a.impl)
+            ec.share_db(ctx)
+        out["extras"] = extras(ec, ctx, shard, bins)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(qs.des, shard, a.cpu_queries)
         out["cpu_baseline_hough"] = cpu_hough_baseline(qs, (x, y, ang, octv), img, cent, size,
