@@ -58,7 +58,7 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=50)   # steady state: the last query's tail is 1/K of a step
     p.add_argument("--warmup", type=int, default=10)   # the clock settles over ~10 launches
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")

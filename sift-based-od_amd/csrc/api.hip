@@ -63,6 +63,16 @@ int flags_reset(sod_ctx* ctx) {
 // the last matcher kernel, then mark the inputs ready; the matcher kernel waits for the
 // inputs and for the previous merge of its partial results, and the context stream waits
 // for the kernel before merging.
+// cross-stream wait, skipped when the host already sees the event complete (a satisfied
+// wait still costs the matcher stream a barrier packet between two back-to-back launches)
+static int wait_unless_done(sod_ctx* ctx, hipStream_t s, hipEvent_t ev) {
+  const hipError_t q = hipEventQuery(ev);
+  if (q == hipSuccess) return SOD_OK;
+  if (q != hipErrorNotReady) return sod_fail(ctx, SOD_EHIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+  (void)hipGetLastError();   // hipErrorNotReady is an answer, not an error
+  SOD_HIP(ctx, hipStreamWaitEvent(s, ev, 0));
+  return SOD_OK;
+}
 int sod_inputs_begin(sod_ctx* ctx) {
   SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0));
   return SOD_OK;
@@ -92,19 +102,16 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
     return SOD_OK;
   }
   *ks = ctx->mstream;
-  SOD_HIP(ctx, hipStreamWaitEvent(ctx->mstream, ctx->ev_inputs, 0));
-  SOD_HIP(ctx, hipStreamWaitEvent(ctx->mstream, ctx->ev_merged[ctx->pslot], 0));
+  SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_inputs));
+  SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_merged[ctx->pslot]));
   // a new slot size moves the slots' boundaries: the other slot's last merge must be done too
-  if (resized) SOD_HIP(ctx, hipStreamWaitEvent(ctx->mstream, ctx->ev_merged[ctx->pslot ^ 1], 0));
+  if (resized) SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_merged[ctx->pslot ^ 1]));
   return SOD_OK;
 }
 int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end) {
   hipEvent_t& e = ctx->mev[ctx->nmatch % sod_ctx::kMatchRing][end];
   if (!e) SOD_HIP(ctx, hipEventCreate(&e));
   SOD_HIP(ctx, hipEventRecord(e, ks));
-  // ev[0] / ev[1] also bound the matcher for sod_last_stage_ms (stage 0, and stage 1 starts
-  // at ev[1])
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[end], ks));
   if (end) ++ctx->nmatch;
   return SOD_OK;
 }
@@ -244,9 +251,17 @@ int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n) {
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   const bool rec[6] = {ctx->matched, ctx->matched, ctx->houghed, ctx->houghed, ctx->selected,
                        ctx->affined};
+  // the last matcher launch's begin / end events (sod_match_mark) bound stages 0 and 1
+  hipEvent_t evs[6];
+  for (int i = 0; i < 6; ++i) evs[i] = ctx->ev[i];
+  if (ctx->nmatch > 0) {
+    hipEvent_t* m = ctx->mev[(ctx->nmatch - 1) % sod_ctx::kMatchRing];
+    evs[0] = m[0];
+    evs[1] = m[1];
+  }
   for (int i = 0; i < n && i < 5; ++i) {
     float ms = 0.f;
-    if (rec[i] && rec[i + 1] && hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) != hipSuccess) {
+    if (rec[i] && rec[i + 1] && hipEventElapsedTime(&ms, evs[i], evs[i + 1]) != hipSuccess) {
       ms = 0.f;
       (void)hipGetLastError();   // not sticky: the next launch check must not see it
     }
