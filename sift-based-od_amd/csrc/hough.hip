@@ -14,10 +14,11 @@
 //                    atomics (deterministic)
 //   select_*         votes that are the first touch of a bin with >= thr votes, compacted
 //                    in ordinal order = dict insertion order of main.py:126
-//   member_fill      per 256-query block: LDS sort of its (valid bin, query) votes, one
-//                    atomic per run reserves the run's slots in the bin's member list
-//   member_order     per bin: runs reordered by fill block = query order
-//   members_kernel   fallback for bins beyond the LDS cap: one wave scans the queries
+//   member_fill      wave-aggregated slot reservation: per vote slot, one atomic per distinct
+//                    bin among a wave's lanes reserves a run in the bin's member list
+//   member_order     query order per bin: <= 256 members sorted in one wave's registers,
+//                    larger bins through an LDS bitmap of their query range
+//   members_kernel   fallback for ranges beyond the bitmap (nq > 512 Ki): one wave scans
 //   means_kernel     PoseBin running means, sequential per bin (PoseBin.py:19-43)
 //   affine_kernel    one wave per bin: decoupled 3x3 normal equations, pinv by Jacobi,
 //                    outlier rejection, fixed point (AffineParameters.py:89-160)
@@ -409,176 +410,47 @@ __global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __
 
 // members, step 1: every vote into a valid bin reserves a slot in its bin's member list.
 // A bin voted by many matches (a real object: thousands of votes) would serialise on one
-// global cursor, so each block of kFillQ queries first sorts its (valid bin, query) votes
-// in LDS: equal bins form runs and ONE atomicAdd per run reserves the run's slots.  Runs
-// land in arbitrary block order; member_order_kernel restores query order per bin.
-constexpr int kFillQ = 256;                 // queries per block -> <= 4096 votes
-constexpr int kSortE = 16;                  // keys per thread in sort_block_u64
-
-// bitonic compare-exchange of registers r and r|J (J < kSortE) of thread t, stage size k
-template <int J>
-__device__ __forceinline__ void sort_reg_stage(uint64_t (&a)[kSortE], int t, int k) {
-#pragma unroll
-  for (int r = 0; r < kSortE; ++r) {
-    if (r & J) continue;
-    const bool asc = ((t * kSortE + r) & k) == 0;
-    const uint64_t x = a[r], y = a[r | J];
-    const bool sw = asc ? (x > y) : (x < y);
-    a[r] = sw ? y : x;
-    a[r | J] = sw ? x : y;
-  }
-}
-
-// Ascending bitonic sort of key[0..p) (p a power of two, kSortE <= p <= kSortE * blockDim)
-// held as kSortE consecutive keys per thread: strides below kSortE are register
-// compare-exchanges, larger ones one LDS exchange each.
-__device__ void sort_block_u64(uint64_t* key, int p) {
-  const int t = threadIdx.x;
-  const bool act = t * kSortE < p;
-  uint64_t a[kSortE];
-  if (act) {
-#pragma unroll
-    for (int r = 0; r < kSortE; ++r) a[r] = key[t * kSortE + r];
-  }
-  for (int k = 2; k <= p; k <<= 1) {
-    for (int j = k >> 1; j >= kSortE; j >>= 1) {   // partner in another thread
-      __syncthreads();
-      if (act) {
-#pragma unroll
-        for (int r = 0; r < kSortE; ++r) key[t * kSortE + r] = a[r];
-      }
-      __syncthreads();
-      if (act) {
-        const int lo = ((t * kSortE) & j) == 0;     // this thread holds the lower index
-#pragma unroll
-        for (int r = 0; r < kSortE; ++r) {
-          const int i = t * kSortE + r;
-          const uint64_t o = key[i ^ j];
-          const bool asc = (i & k) == 0;
-          a[r] = (lo == asc) ? (a[r] < o ? a[r] : o) : (a[r] > o ? a[r] : o);
-        }
-      }
-    }
-    if (act) {
-      if (k >= 16) sort_reg_stage<8>(a, t, k);
-      if (k >= 8) sort_reg_stage<4>(a, t, k);
-      if (k >= 4) sort_reg_stage<2>(a, t, k);
-      sort_reg_stage<1>(a, t, k);
-    }
-  }
-  __syncthreads();
-  if (act) {
-#pragma unroll
-    for (int r = 0; r < kSortE; ++r) key[t * kSortE + r] = a[r];
-  }
-  __syncthreads();
-}
-constexpr int kFillCap = kFillQ * 16;
+// global cursor, so the votes of a wave are aggregated first: per vote slot, the lanes
+// voting for the same bin take ONE atomicAdd (leader = lowest lane) and place their
+// queries in lane order inside the reserved run.  No LDS, no block barrier: the kernel
+// keeps full occupancy on the few CUs a reserved tail has (sod_set_cu_reserve).  Runs land
+// in arbitrary order; member_order_*_kernel sort each bin into query order afterwards.
 __global__ __launch_bounds__(256) void member_fill_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
     const int* __restrict__ qimg, int64_t nbins1, const uint32_t* __restrict__ vidx,
     const int64_t* __restrict__ voff,
     uint32_t* __restrict__ cursor, int32_t* __restrict__ members) {
-  __shared__ uint64_t key[kFillCap];
-  __shared__ uint32_t nvote;
-  __shared__ uint32_t sh[4];
-  if (threadIdx.x == 0) nvote = 0;
-  __syncthreads();
-  const int64_t q = (int64_t)blockIdx.x * kFillQ + threadIdx.x;
-  // 1. gather this block's votes into valid bins (order irrelevant: sorted next)
-  if (q < nq) {
-    const uint32_t m = vmask[q] & 0xFFFFu;
-    if (m) {
-      const uint32_t k = basekey[q];
-      const int ix = k & 0xFF, iy = (k >> 8) & 0xFF, it = (k >> 16) & 0xFF, is = k >> 24;
-      const uint32_t base = qimg ? (uint32_t)(qimg[q] * nbins1) : 0u;
-      for (int slot = 0; slot < 16; ++slot) {
-        if (!((m >> slot) & 1u)) continue;
-        const uint32_t lb = base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
-                                           it + ((slot >> 1) & 1), is + (slot & 1), b);
-        const uint32_t v = vidx[lb];
-        if (v == 0xFFFFFFFFu) continue;
-        key[atomicAdd(&nvote, 1u)] = ((uint64_t)v << 32) | (uint32_t)q;
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t q0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); q0 < nq; q0 += stride) {
+    const int64_t q = q0 + lane;
+    uint32_t m = 0, k = 0, base = 0;
+    if (q < nq) {
+      m = vmask[q] & 0xFFFFu;
+      k = basekey[q];
+      base = qimg ? (uint32_t)(qimg[q] * nbins1) : 0u;
+    }
+    if (__ballot(m != 0) == 0) continue;
+    const int ix = k & 0xFF, iy = (k >> 8) & 0xFF, it = (k >> 16) & 0xFF, is = k >> 24;
+    for (int slot = 0; slot < 16; ++slot) {
+      uint32_t v = 0xFFFFFFFFu;
+      if ((m >> slot) & 1u)
+        v = vidx[base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                it + ((slot >> 1) & 1), is + (slot & 1), b)];
+      uint64_t pend = __ballot(v != 0xFFFFFFFFu);
+      while (pend) {                                   // one round per distinct bin
+        const int leader = __ffsll((unsigned long long)pend) - 1;
+        const uint32_t vv = __shfl(v, leader);
+        const uint64_t same = __ballot(v == vv);
+        uint32_t r = 0;
+        if (lane == leader) r = atomicAdd(&cursor[vv], (uint32_t)__popcll(same));
+        r = __shfl(r, leader);
+        if (v == vv) members[voff[vv] + r + __popcll(same & below)] = (int32_t)q;
+        pend &= ~same;
       }
     }
   }
-  __syncthreads();
-  const int n = (int)nvote;
-  if (n == 0) return;
-  int p = kSortE;
-  while (p < n) p <<= 1;
-  for (int i = n + threadIdx.x; i < p; i += blockDim.x) key[i] = ~0ull;
-  __syncthreads();
-  // 2. bitonic sort by (bin, query): 16 keys per thread in registers
-  sort_block_u64(key, p);
-  // 3. run starts: start[i] = last index <= i where the bin changes (block max-scan,
-  //    16 consecutive elements per thread)
-  __shared__ uint32_t start_of[kFillCap];
-  __shared__ uint32_t tmax[4];
-  const int per = (p + 255) / 256;
-  const int i0 = threadIdx.x * per;
-  uint32_t run = 0;
-  for (int i = i0; i < i0 + per && i < n; ++i) {
-    if (i == 0 || (uint32_t)(key[i - 1] >> 32) != (uint32_t)(key[i] >> 32)) run = (uint32_t)i;
-    start_of[i] = run;   // provisional: only valid if a head occurred within this chunk
-  }
-  {
-    const uint32_t carry = block_scan256<true>(run, tmax);   // exclusive max over threads
-    bool head_seen = false;
-    for (int i = i0; i < i0 + per && i < n; ++i) {
-      if (i == 0 || (uint32_t)(key[i - 1] >> 32) != (uint32_t)(key[i] >> 32)) head_seen = true;
-      if (!head_seen) start_of[i] = carry;
-    }
-  }
-  __syncthreads();
-  // 4. the last element of each run reserves the run's slots (one atomic per run)
-  __shared__ uint32_t base_of[kFillCap];
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint32_t v = (uint32_t)(key[i] >> 32);
-    if (i == n - 1 || (uint32_t)(key[i + 1] >> 32) != v) {
-      const uint32_t st = start_of[i];
-      base_of[st] = atomicAdd(&cursor[v], (uint32_t)(i - st + 1));
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint32_t v = (uint32_t)(key[i] >> 32);
-    const uint32_t st = start_of[i];
-    members[voff[v] + base_of[st] + (i - st)] = (int32_t)(uint32_t)key[i];
-  }
-  (void)sh;
-}
-
-// members, step 2: restore query order (= vote order, main.py:91) inside each bin.  After
-// member_fill a bin's list is a concatenation of runs, one per fill block, each sorted by
-// query, in arbitrary block order; fill blocks cover disjoint query ranges (block =
-// query / kFillQ), so ordering the RUNS by block id orders the list.  Per bin (one
-// work-group, LDS): run starts by a max-scan of head positions, run lengths tabulated by
-// block id, an exclusive scan of that table gives each run's destination, one scatter.
-// Bins with more than kOrderCap members (or more than kOrderCap fill blocks) are rebuilt
-// by members_kernel (scan).  Also resets the bin -> valid index map for the next call.
-constexpr int kOrderCap = 8192;
-constexpr int kOrderT = 256;
-constexpr int kOrderPer = kOrderCap / kOrderT;   // elements per thread in the scans
-
-// in-place exclusive (sum) / inclusive (max) scan of a[0..n), n <= kOrderCap, 256 threads
-template <bool kMax>
-__device__ void block_scan_lds(uint32_t* a, int n, uint32_t* part) {
-  const int t = threadIdx.x, i0 = t * kOrderPer;
-  uint32_t acc = 0;
-  for (int i = i0; i < i0 + kOrderPer && i < n; ++i) acc = kMax ? max(acc, a[i]) : acc + a[i];
-  uint32_t run = block_scan256<kMax>(acc, part);
-  for (int i = i0; i < i0 + kOrderPer && i < n; ++i) {
-    const uint32_t v = a[i];
-    if (kMax) {
-      run = max(run, v);
-      a[i] = run;
-    } else {
-      a[i] = run;
-      run += v;
-    }
-  }
-  __syncthreads();
 }
 
 // Small bins (the great majority: a few to a few dozen members) take a wave of their own:
@@ -645,35 +517,66 @@ __global__ __launch_bounds__(256) void member_order_small_kernel(
   }
 }
 
+// Bins above kWaveCap members: one work-group per bin marks its members in an LDS bitmap
+// over the bin's query range [min, max] and writes them back in bit order (= query
+// order): a popcount scan over the words gives every word its output offset.  Ranges
+// beyond kBitWords*32 queries (only when nq > kBitQ) are rebuilt by members_kernel.
+constexpr int kOrderT = 256;
+constexpr int kBitWords = 16384;                // 64 KiB of LDS: query ranges up to 512 Ki
+constexpr int64_t kBitQ = (int64_t)kBitWords * 32;
+
+__device__ __forceinline__ uint32_t block_reduce_min256(uint32_t x, uint32_t* sh) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x = min(x, (uint32_t)__shfl_xor(x, d));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+  __syncthreads();
+  return min(min(sh[0], sh[1]), min(sh[2], sh[3]));
+}
+
 __global__ __launch_bounds__(kOrderT) void member_order_kernel(const uint32_t* __restrict__ scal,
-                                                               const uint32_t* __restrict__ vbin,
                                                                const int64_t* __restrict__ voff,
-                                                               int nblk,
-                                                               uint32_t* __restrict__ vidx,
+                                                               int64_t nq,
                                                                int32_t* __restrict__ members) {
-  __shared__ uint32_t key[kOrderCap];     // the bin's members as filled
-  __shared__ uint32_t start[kOrderCap];   // run start of each element
-  __shared__ uint32_t tab[kOrderCap];     // run length -> destination, by fill block
-  __shared__ uint32_t part[kOrderT];
+  __shared__ uint32_t bits[kBitWords];
+  __shared__ uint32_t red[2][4];
+  __shared__ uint32_t part[4];
+  if (nq > kBitQ) return;                                     // members_kernel rebuilds them
   const int64_t V = scal[0];
   for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
     const int64_t a = voff[v];
-    const int n = (int)(voff[v + 1] - a);
-    // (bins up to kWaveCap: member_order_small_kernel, which also reset vidx)
-    if (n <= kWaveCap || n > kOrderCap || nblk > kOrderCap) continue;   // uniform over the group
-    for (int i = threadIdx.x; i < n; i += kOrderT) key[i] = (uint32_t)members[a + i];
-    for (int i = threadIdx.x; i < nblk; i += kOrderT) tab[i] = 0;
+    const int64_t n = voff[v + 1] - a;
+    if (n <= kWaveCap) continue;                              // uniform over the group
+    uint32_t lo = 0xFFFFFFFFu, hi_neg = 0xFFFFFFFFu;
+    for (int64_t i = threadIdx.x; i < n; i += kOrderT) {
+      const uint32_t q = (uint32_t)members[a + i];
+      lo = min(lo, q);
+      hi_neg = min(hi_neg, ~q);
+    }
+    lo = block_reduce_min256(lo, red[0]);
+    const uint32_t hi = ~block_reduce_min256(hi_neg, red[1]);
+    const int words = (int)((hi - lo) / 32 + 1);
+    for (int w = threadIdx.x; w < words; w += kOrderT) bits[w] = 0u;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += kOrderT)
-      start[i] = (i == 0 || key[i] / kFillQ != key[i - 1] / kFillQ) ? (uint32_t)i : 0u;
+    for (int64_t i = threadIdx.x; i < n; i += kOrderT) {
+      const uint32_t d = (uint32_t)members[a + i] - lo;
+      atomicOr(&bits[d >> 5], 1u << (d & 31));
+    }
     __syncthreads();
-    block_scan_lds<true>(start, n, part);
-    for (int i = threadIdx.x; i < n; i += kOrderT)   // the run's last element records it
-      if (i == n - 1 || start[i + 1] != start[i]) tab[key[i] / kFillQ] = (uint32_t)i - start[i] + 1;
-    __syncthreads();
-    block_scan_lds<false>(tab, nblk, part);
-    for (int i = threadIdx.x; i < n; i += kOrderT)
-      members[a + tab[key[i] / kFillQ] + ((uint32_t)i - start[i])] = (int32_t)key[i];
+    // contiguous words per thread, exclusive scan of their popcounts, then write in order
+    const int per = (words + kOrderT - 1) / kOrderT;
+    const int w0 = threadIdx.x * per, w1 = min(words, w0 + per);
+    uint32_t cnt = 0;
+    for (int w = w0; w < w1; ++w) cnt += __popc(bits[w]);
+    uint32_t off = block_scan256<false>(cnt, part);
+    for (int w = w0; w < w1; ++w) {
+      uint32_t x = bits[w];
+      while (x) {
+        const int bit = __ffs(x) - 1;
+        members[a + off++] = (int32_t)(lo + (uint32_t)w * 32u + (uint32_t)bit);
+        x &= x - 1u;
+      }
+    }
     __syncthreads();
   }
 }
@@ -686,7 +589,7 @@ __global__ __launch_bounds__(256) void members_kernel(
     const int64_t* __restrict__ voff, const uint32_t* __restrict__ gcount,
     const uint32_t* __restrict__ gfirst, const uint32_t* __restrict__ basekey,
     const uint32_t* __restrict__ vmask, Bins b, const int* __restrict__ qimg, int64_t nbins1,
-    int nblk, int32_t* __restrict__ members) {
+    int32_t* __restrict__ members) {
   constexpr int U = 4;
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -698,7 +601,7 @@ __global__ __launch_bounds__(256) void members_kernel(
     const int bs_ = ll % b.s, bt_ = (ll / b.s) % b.t, by_ = (ll / (b.s * b.t)) % b.y,
               bx_ = ll / (b.s * b.t * b.y);
     const uint32_t need = gcount[lb];
-    if (need <= (uint32_t)kOrderCap && nblk <= kOrderCap) continue;   // fill + order
+    if (need <= (uint32_t)kWaveCap || nq <= kBitQ) continue;   // fill + order kernels
     const int64_t off = voff[v];
     uint32_t got = 0;
     for (int64_t q0 = gfirst[lb] >> 4; got < need && q0 < nq; q0 += 64 * U) {
@@ -1122,23 +1025,22 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   hipLaunchKernelGGL(member_offsets_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->vbin.p,
                      ctx->counts.p, ctx->scal.p, ctx->voff.p, ctx->cursor.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(member_fill_kernel, dim3((unsigned)cdiv(nq, kFillQ)), dim3(256), 0, ctx->stream,
+  const unsigned fill_wg = (unsigned)std::min<int64_t>(cdiv(nq, 256), (int64_t)ctx->tail_cus() * 16);
+  hipLaunchKernelGGL(member_fill_kernel, dim3(std::max(1u, fill_wg)), dim3(256), 0, ctx->stream,
                      nq, ctx->basekey.p, ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1,
                      ctx->vidx.p, ctx->voff.p, ctx->cursor.p, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  const int nblk = (int)cdiv(nq, kFillQ);
   hipLaunchKernelGGL(member_order_small_kernel, dim3(std::max(1, ctx->tail_cus() * 8)), dim3(256),
                      0, ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, ctx->vidx.p,
                      ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->tail_cus() * 2)), dim3(kOrderT), 0,
-                     ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, nblk, ctx->vidx.p,
-                     ctx->members.p);
+                     ctx->stream, ctx->scal.p, ctx->voff.p, nq, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   const int wg = std::max(1, ctx->tail_cus() * 4);
   hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
                      ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
-                     ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, nblk, ctx->members.p);
+                     ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   // PoseBin means depend only on the member lists: they run on the side stream, beside the
   // affine verification, and the main stream joins them at the next entry point (set_dev)

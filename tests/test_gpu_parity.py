@@ -156,11 +156,14 @@ def test_hough_affine_edges(ctx, name):
     _check_hough(ctx, g)
 
 
-def test_member_order_at_scale(ctx):
-    """Large bins (thousands of members from many 256-query fill blocks): every valid bin's
-    member list is in query order, holds exactly its vote count, and only good matches."""
+@pytest.mark.parametrize("nq", [40000, 530000])
+def test_member_order_at_scale(ctx, nq):
+    """Large bins (thousands of members, filled by many waves in arbitrary order): every
+    valid bin's member list is in query order, holds exactly its vote count, and only good
+    matches.  40 000 queries: small bins sorted in a wave, large ones through the LDS
+    bitmap; 530 000 (> 512 Ki): large bins rebuilt by members_kernel's query scan."""
     db = synthetic.make_database(20, 1000, seed=0)
-    qs = synthetic.make_queries(40000, seed=5, db_seed=0, kp_per_image=1000, n_objects=2)
+    qs = synthetic.make_queries(nq, seed=5, db_seed=0, kp_per_image=1000, n_objects=2)
     ctx.set_impl("i8")
     ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
     ctx.upload_db(db.des)
