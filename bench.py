@@ -353,7 +353,8 @@ def main():
     # auto: split the chip when the matcher dominates a step (C3 / C5: ~4 ms against a
     # ~1.3 ms tail on the 8 reserved CUs); C2's 0.2 ms matcher would wait on that tail
     reserve = a.cu_reserve if a.cu_reserve >= 0 else (
-        0 if a.contexts > 1 or a.overlap == 0 or nq * shard.shape[0] < 10 ** 10 else 1)
+        0 if a.contexts > 1 or a.overlap == 0 or nq * shard.shape[0] < 10 ** 10
+        or a.impl != "i8" else 1)   # grid sizing measured for the default int8 kernel only
     comm = None
     if world > 1 and a.comm == "rccl":
         if reserve:
