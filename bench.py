@@ -85,7 +85,10 @@ def parse():
     p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                    help="multi-rank exchange: RCCL on the device (default) or staged "
                         "through host memory over gloo (for >1 rank per GPU)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.overlap == 0 and a.cu_reserve > 0:
+        p.error("--cu-reserve > 0 runs the matcher on a stream of its own: it needs --overlap 1")
+    return a
 
 
 class Dist:
@@ -355,20 +358,19 @@ def main():
     reserve = a.cu_reserve if a.cu_reserve >= 0 else (
         0 if a.contexts > 1 or a.overlap == 0 or nq * shard.shape[0] < 10 ** 10
         or a.impl != "i8" else 1)   # grid sizing measured for the default int8 kernel only
-    comm = None
-    if world > 1 and a.comm == "rccl":
-        if reserve:
-            # the collectives run on the reserved CUs (8 * reserve): at most that many
-            # channels, so every block of an RCCL kernel is resident at once
-            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(8 * reserve))
-        comm = RcclComm(ctx, world, rank, D.bcast_bytes)
-    elif world > 1:
-        comm = TorchHostComm()
-    own = (rank * n_shard, (rank + 1) * n_shard)
     overlap = a.overlap if a.overlap >= 0 else (1 if world > 1 or reserve else 0)
     ctx.set_overlap(bool(overlap))
     if reserve:
         ctx.set_cu_reserve(reserve)
+        overlap = 1                 # the split runs the matcher on its own stream
+    comm = None
+    if world > 1 and a.comm == "rccl":
+        # created under the split: sod_comm_init caps NCCL_MAX_NCHANNELS at the reserved CU
+        # count (8 * reserve), so every block of an RCCL kernel is resident at once
+        comm = RcclComm(ctx, world, rank, D.bcast_bytes)
+    elif world > 1:
+        comm = TorchHostComm()
+    own = (rank * n_shard, (rank + 1) * n_shard)
     ncontexts = a.contexts if a.contexts > 0 else (2 if world == 1 and not overlap else 1)
     ctxs = [ctx]
     for _ in range(ncontexts - 1):

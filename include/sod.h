@@ -70,9 +70,12 @@ int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
 
 /* dst uses src's resident database (keypoints, image table, packed descriptors) without
  * a copy: several contexts -- each with its own stream and query state -- serve query
- * images concurrently over one DB.  src must outlive dst and must not re-upload its DB
- * while dst uses it; a later upload into dst gives dst its own buffers. */
-int sod_db_share(sod_ctx* dst, const sod_ctx* src);
+ * images concurrently over one DB.  src counts its sharers: while any exists, every DB
+ * write on src (set_keypoints, upload_descriptors, import_packed, set_impl) fails with
+ * SOD_ESTATE.  A DB write on dst first detaches it (dst then holds no DB until it uploads
+ * one of its own).  Destroying src waits for its sharers' queued work and detaches them.
+ * Contexts sharing a DB must not be driven concurrently from different host threads. */
+int sod_db_share(sod_ctx* dst, sod_ctx* src);
 
 /* ---- packed DB image (replaces the GenerateDatabaseInfo.py:35 pickle
  * + main.py:53-66 flattening as the descriptor store): the device's own fragment layout
@@ -126,7 +129,12 @@ int sod_match_set_overlap(sod_ctx* ctx, int on);
  * being starved by it.  Implies sod_match_set_overlap(ctx, 1); 0 restores unmasked streams.
  * Meant for streaming query batches through sod_pipeline_enqueue: every other entry point on
  * the context stream (SIFT, uploads) also runs on the reserved CUs while it is set.
- * Results are unchanged.  (No reference counterpart: an MI355X scheduling knob.) */
+ * Results are unchanged.  (No reference counterpart: an MI355X scheduling knob.)
+ * SOD_EINVAL on a device other than a whole MI355X (gfx950, 8 XCDs, 256 CUs: the CU-mask
+ * layout it relies on was measured there).  With an RCCL communicator every block of a
+ * collective must fit the reserved CUs: sod_comm_init under an active split caps
+ * NCCL_MAX_NCHANNELS at the reserved CU count (sets it if unset, SOD_ESTATE if larger),
+ * and this call fails with SOD_ESTATE on a communicator created without such a cap. */
 int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd);
 /* multi-GPU: RCCL all-gather of every rank's per-query (d1^2, idx1, d2^2) and the
  * global merge.  No-op on a single rank. */

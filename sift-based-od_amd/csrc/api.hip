@@ -1,6 +1,7 @@
 // api.hip -- extern "C" entry points of libsod.so (declared in include/sod.h).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -126,6 +127,55 @@ int sod_match_stream_end(sod_ctx* ctx) {
   return SOD_OK;
 }
 
+// ---- DB sharing bookkeeping (sod_db_share) ---------------------------------------------
+// A sharer drops its views of the source's DB buffers (views are never freed by it) and
+// leaves the source's list.  Its own streams must have drained any work reading them.
+static void db_detach(sod_ctx* ctx) {
+  sod_ctx* src = ctx->db_src;
+  if (!src) return;
+  auto& v = src->db_sharers;
+  v.erase(std::remove(v.begin(), v.end(), ctx), v.end());
+  ctx->db_src = nullptr;
+  sod_release(ctx->mx); sod_release(ctx->my); sod_release(ctx->mang);
+  sod_release(ctx->moct); sod_release(ctx->mimg); sod_release(ctx->cent);
+  sod_release(ctx->isize); sod_release(ctx->dbpack); sod_release(ctx->dn);
+  ctx->nsub = 0;
+  ctx->n_total = 0;
+  ctx->n_images = 0;
+  ctx->n_shard = 0;
+  ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+}
+
+static void drain_streams(sod_ctx* ctx) {
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+  if (ctx->mstream) (void)hipStreamSynchronize(ctx->mstream);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+}
+
+// Every DB writer calls this first: a source whose DB other contexts alias refuses (their
+// matchers may be reading it on their own streams); a sharer detaches, so the write goes
+// to buffers of its own and never into the source's.
+static int db_writable(sod_ctx* ctx) {
+  if (!ctx->db_sharers.empty())
+    return sod_fail(ctx, SOD_ESTATE,
+                    std::to_string(ctx->db_sharers.size()) +
+                        " context(s) use this database through sod_db_share; destroy them "
+                        "before changing it");
+  if (ctx->db_src) {
+    drain_streams(ctx);
+    db_detach(ctx);
+  }
+  return SOD_OK;
+}
+
+// NCCL_MAX_NCHANNELS as RCCL will read it at communicator creation (0 = unset / default)
+static int env_max_channels() {
+  const char* e = std::getenv("NCCL_MAX_NCHANNELS");
+  if (!e || !*e) return 0;
+  const long v = std::strtol(e, nullptr, 10);
+  return v > 0 && v < (1 << 20) ? (int)v : 0;
+}
+
 extern "C" {
 
 int sod_abi_version(void) { return 1; }
@@ -140,7 +190,13 @@ int sod_create(int device, sod_ctx** out) {
   if (e == hipSuccess) {
     hipDeviceProp_t prop;
     e = hipGetDeviceProperties(&prop, device);
-    if (e == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
+    if (e == hipSuccess) {
+      ctx->num_cus = prop.multiProcessorCount;
+      ctx->gfx950 = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+      int nx = 0;
+      if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, device) == hipSuccess && nx > 0)
+        ctx->num_xcds = nx;
+    }
   }
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
@@ -172,6 +228,15 @@ void sod_destroy(sod_ctx* ctx) {
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   if (ctx->mstream) (void)hipStreamSynchronize(ctx->mstream);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  db_detach(ctx);
+  // contexts still aliasing this DB: let their queued work finish, then drop their views
+  // (they report "no database" afterwards instead of reading freed memory)
+  const std::vector<sod_ctx*> sharers = ctx->db_sharers;
+  for (sod_ctx* s : sharers) {
+    drain_streams(s);
+    db_detach(s);
+  }
+  (void)hipSetDevice(ctx->device);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   sod_sift_free(ctx);
   sod_release(ctx->mx); sod_release(ctx->my); sod_release(ctx->mang);
@@ -277,6 +342,7 @@ int sod_db_set_keypoints(sod_ctx* ctx, int64_t n_total, const float* x, const fl
   SOD_TRY(set_dev(ctx));
   if (n_total < 0 || n_images < 1 || !x || !y || !angle || !octave || !img || !centroid || !size)
     return sod_fail(ctx, SOD_EINVAL, "sod_db_set_keypoints: bad arguments");
+  SOD_TRY(db_writable(ctx));
   for (int64_t i = 0; i < n_total; ++i)
     if (img[i] < 0 || img[i] >= n_images)
       return sod_fail(ctx, SOD_EINVAL, "keypoint image id out of range");
@@ -331,6 +397,7 @@ int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
   SOD_TRY(set_dev(ctx));
   if (n < 1 || row_offset < 0 || row_offset + n > (int64_t)0x7fffffff)
     return sod_fail(ctx, SOD_EINVAL, "descriptor rows out of range");
+  SOD_TRY(db_writable(ctx));
   SOD_HIP(ctx, hipMemsetAsync(ctx->flags.p + 1, 0, 4, ctx->stream));
   SOD_TRY(upload_descriptors(ctx, des, dtype, n, true));
   ctx->n_shard = n;
@@ -340,11 +407,15 @@ int sod_db_upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
 }
 
 // ---- DB shared between contexts (several query streams over one resident DB) ---------
-int sod_db_share(sod_ctx* dst, const sod_ctx* src) {
+int sod_db_share(sod_ctx* dst, sod_ctx* src) {
   SOD_TRY(set_dev(dst));
+  if (src && src->db_src) src = src->db_src;   // share from the owner of the buffers
   if (!src || src == dst) return sod_fail(dst, SOD_EINVAL, "bad source context");
   if (src->device != dst->device) return sod_fail(dst, SOD_EINVAL, "contexts on different devices");
   if (!src->nsub || !src->n_total) return sod_fail(dst, SOD_ESTATE, "source has no database");
+  SOD_TRY(db_writable(dst));   // dst's own DB is replaced: refused while others alias it
+  dst->db_src = src;
+  src->db_sharers.push_back(dst);
   sod_view(dst->mx, src->mx);
   sod_view(dst->my, src->my);
   sod_view(dst->mang, src->mang);
@@ -450,6 +521,7 @@ int sod_db_import_packed(sod_ctx* ctx, const void* in, int64_t bytes) {
       bytes < (int64_t)sizeof(h) + h.nsub * h.sub_bytes + h.norm_bytes)
     return sod_fail(ctx, SOD_EINVAL, "inconsistent packed DB image");
   const uint8_t* src = static_cast<const uint8_t*>(in) + sizeof(h);
+  SOD_TRY(db_writable(ctx));
   SOD_TRY(sod_inputs_begin(ctx));
   SOD_TRY(sod_reserve(ctx, ctx->dbpack, (size_t)(h.nsub * h.sub_bytes)));
   SOD_TRY(sod_reserve(ctx, ctx->dn, (size_t)(h.norm_bytes / 4)));
@@ -580,14 +652,38 @@ int sod_match_set_overlap(sod_ctx* ctx, int on) {
 // unmasked streams.  Results are unchanged.
 static hipError_t make_stream(hipStream_t* s, const std::vector<uint32_t>& mask) {
   if (mask.empty()) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size() * 32, mask.data());
+  // cuMaskSize counts uint32 words (HIP copies [cuMask, cuMask + cuMaskSize))
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
 }
 
 int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
   SOD_TRY(set_dev(ctx));
-  const int nx = 8;   // XCDs on an MI355X
-  if (per_xcd < 0 || (per_xcd > 0 && (ctx->num_cus % nx != 0 || per_xcd * nx * 2 > ctx->num_cus)))
-    return sod_fail(ctx, SOD_EINVAL, "cu reserve per XCD must be in [0, CUs per XCD / 2]");
+  const int nx = ctx->num_xcds;
+  if (per_xcd < 0) return sod_fail(ctx, SOD_EINVAL, "cu reserve per XCD must be >= 0");
+  if (per_xcd > 0) {
+    // the mask-bit -> XCD map (bit i on XCD i % 8) was measured on a full MI355X
+    // (tools/cu_mask_probe.hip); on another layout (a CPX/DPX partition, another SKU) the
+    // reserved CUs would not be one per XCD and the matcher grid sizing would be wrong
+    if (!ctx->gfx950 || nx != 8 || ctx->num_cus != 256)
+      return sod_fail(ctx, SOD_EINVAL,
+                      "CU split measured only on a whole MI355X (gfx950, 8 XCDs, 256 CUs); this "
+                      "device has " + std::to_string(nx) + " XCD(s) and " +
+                          std::to_string(ctx->num_cus) + " CUs");
+    if (per_xcd * nx * 2 > ctx->num_cus)
+      return sod_fail(ctx, SOD_EINVAL, "cu reserve per XCD must be in [0, CUs per XCD / 2]");
+    // a collective whose blocks do not all fit the reserved CUs could wait on a block that
+    // never gets a CU: the communicator must have been created with at most that many
+    // channels
+    if (ctx->comm && (ctx->comm_max_channels == 0 || ctx->comm_max_channels > per_xcd * nx))
+      return sod_fail(ctx, SOD_ESTATE,
+                      "the RCCL communicator was created with " +
+                          (ctx->comm_max_channels ? "up to " + std::to_string(ctx->comm_max_channels)
+                                                  : std::string("the default number of")) +
+                          " channels; the CU split runs collectives on " +
+                          std::to_string(per_xcd * nx) +
+                          " CUs: set NCCL_MAX_NCHANNELS <= that before sod_comm_init, or call "
+                          "sod_set_cu_reserve first");
+  }
   SOD_HIP(ctx, hipStreamSynchronize(ctx->side));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -625,6 +721,7 @@ int sod_match_set_impl(sod_ctx* ctx, int impl) {
   if (impl < 0 || impl > 2)
     return sod_fail(ctx, SOD_EINVAL, "impl must be 0 (bf16), 1 (int8 16x16x64) or 2 (int8 32x32x32)");
   if (impl != ctx->impl) {  // packed operands differ: uploads must be repeated
+    SOD_TRY(db_writable(ctx));
     ctx->impl = impl;
     ctx->nsub = 0;
     ctx->nqt = 0;
@@ -1057,6 +1154,19 @@ int sod_comm_init(sod_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[S
   ctx->rank = rank;
   // nranks == 1 also builds a communicator: the collectives then run (as copies), which is
   // how the RCCL path is exercised on a one-GPU machine
+  int cap = env_max_channels();
+  if (ctx->reserved_cus > 0) {   // collectives will run on the reserved CUs only
+    if (cap == 0) {
+      // RCCL reads the variable when the communicator is created
+      setenv("NCCL_MAX_NCHANNELS", std::to_string(ctx->reserved_cus).c_str(), 1);
+      cap = ctx->reserved_cus;
+    } else if (cap > ctx->reserved_cus) {
+      return sod_fail(ctx, SOD_ESTATE,
+                      "NCCL_MAX_NCHANNELS=" + std::to_string(cap) + " exceeds the " +
+                          std::to_string(ctx->reserved_cus) +
+                          " CUs reserved by sod_set_cu_reserve for the collectives");
+    }
+  }
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
@@ -1064,6 +1174,7 @@ int sod_comm_init(sod_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[S
     ctx->comm = nullptr;
     return sod_fail(ctx, SOD_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   }
+  ctx->comm_max_channels = cap;
   return SOD_OK;
 }
 

@@ -35,6 +35,8 @@ struct sod_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   int num_cus = 256;
+  int num_xcds = 1;             // hipDeviceAttributeNumberOfXccs
+  bool gfx950 = false;
   // CUs the matcher kernel may use / the other stages run on (sod_set_cu_reserve)
   int match_cus() const { return num_cus - reserved_cus; }
   int tail_cus() const { return reserved_cus ? reserved_cus : num_cus; }
@@ -136,6 +138,16 @@ struct sod_ctx {
   // ---- comm ----
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  // channel cap the communicator was created under (NCCL_MAX_NCHANNELS at sod_comm_init,
+  // 0 = RCCL's default): the CU split needs every block of a collective resident on the
+  // reserved CUs at once (sod_set_cu_reserve checks it)
+  int comm_max_channels = 0;
+
+  // ---- DB sharing (sod_db_share): a source counts the contexts that alias its DB buffers
+  // and refuses DB writes while any does; a sharer detaches (drops its views) before any DB
+  // write of its own and when it is destroyed
+  sod_ctx* db_src = nullptr;
+  std::vector<sod_ctx*> db_sharers;
 
   // ---- side stream: PoseBin means run beside the affine verification ----
   hipStream_t side = nullptr;

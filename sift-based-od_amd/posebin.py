@@ -1,53 +1,71 @@
 """Drop-in for ``PoseBin.py``: the state of one Hough pose bin.
 
-Same attributes and methods as the reference (``PoseBin.py:4-85``) because the
-post-processing and visualisation code read them (``PostProcessing.py:22-28,48-49,98-106``,
-``VisualHelperFunctions.py:7-11``).  The device pipeline computes the bins' votes, members
-and running means in one pass (hough.hip) and materialises PoseBin objects only when
-they are asked for; the per-vote update methods below are the reference's arithmetic for
-callers that drive a PoseBin by hand.
+The attribute names and the method names are the reference's (``PoseBin.py:4-85``) because
+the post-processing and visualisation code read them (``PostProcessing.py:22-28,48-49,
+98-106``, ``VisualHelperFunctions.py:7-11``).  The device pipeline computes every bin's
+votes, members and running means in one pass (hough.hip: ``hist_kernel``, ``member_*``,
+``means_kernel``) and builds these objects only when a caller asks for them
+(``pipeline.Main``); the update methods here are for callers that drive a bin by hand.
+
+Arithmetic contract (what the device's ``means_kernel`` reproduces bit for bit): each
+quantity q of a bin with n votes moves to ``(q * n + new) / (n + 1)`` -- one f64 multiply,
+one add, one correctly rounded divide, in that order (``PoseBin.py:19-43``).
 """
 from __future__ import annotations
 
 import numpy as np
 
 
+def _running_mean(old, new, n):
+    """One step of the reference's running mean: ``(old*n + new)/(n+1)`` (not fused)."""
+    return (old * n + new) / (n + 1)
+
+
+def _pair_mean(old, new, n):
+    return (_running_mean(old[0], new[0], n), _running_mean(old[1], new[1], n))
+
+
 class PoseBin:
+    """One (i_x, i_y, i_theta, i_sigma) bin.
+
+    ``centroid``/``angle``/``scale`` are the running means of the object poses voted into
+    the bin, ``img_size`` the running mean of the voting model images' (w, h);
+    ``keypoint_pairs`` the voting (model kp, query kp, ...) tuples in vote order;
+    ``affine_parameters`` is filled by ``affine.AffineParameters``.
+    """
+
+    __hash__ = None   # the reference defines __eq__ only, which makes bins unhashable
 
     def __init__(self, pose, img_size=(100, 100), votes=0, keypoint_pairs=None,
                  mean=(0, 0, 0, 0)):
-        self.pose = pose                  # (i_x, i_y, i_theta, i_sigma)
-        self.img_size = img_size          # (width, height) running mean
-        self.votes = votes
+        # the reference's default `keypoint_pairs=[]` is one list shared by every bin
+        # built without pairs; main.py always passes its own list, so a fresh one is kept
         self.keypoint_pairs = [] if keypoint_pairs is None else keypoint_pairs
-        self.centroid = mean[0], mean[1]
-        self.angle = mean[2]
-        self.scale = mean[3]
+        self.pose, self.img_size, self.votes = pose, img_size, votes
+        self.centroid = (mean[0], mean[1])
+        self.angle, self.scale = mean[2], mean[3]
         self.affine_parameters = []
 
-    def add_keypoint_pair(self, pair):
-        self.keypoint_pairs.append(pair)
+    # ---- per-vote updates (PoseBin.py:19-54) --------------------------------------------
+    def update_centroid(self, center):
+        self.centroid = _pair_mean(self.centroid, center, self.votes)
 
-    def update_centroid(self, center):                    # PoseBin.py:19-25
-        n = self.votes
-        self.centroid = ((self.centroid[0] * n + center[0]) / (n + 1),
-                         (self.centroid[1] * n + center[1]) / (n + 1))
+    def update_angle(self, alpha):
+        self.angle = _running_mean(self.angle, alpha, self.votes)
 
-    def update_angle(self, alpha):                        # PoseBin.py:27-30
-        self.angle = (self.angle * self.votes + alpha) / (self.votes + 1)
+    def update_scale(self, scale):
+        self.scale = _running_mean(self.scale, scale, self.votes)
 
-    def update_scale(self, scale):                        # PoseBin.py:32-35
-        self.scale = (self.scale * self.votes + scale) / (self.votes + 1)
+    def update_img_size(self, img_size):
+        self.img_size = _pair_mean(self.img_size, img_size, self.votes)
 
-    def update_img_size(self, img_size):                  # PoseBin.py:37-43
-        n = self.votes
-        self.img_size = ((self.img_size[0] * n + img_size[0]) / (n + 1),
-                         (self.img_size[1] * n + img_size[1]) / (n + 1))
-
-    def update_posebin(self, object_pose, img_size, keypoint_pair):   # PoseBin.py:45-51
-        self.update_centroid((object_pose[0], object_pose[1]))
-        self.update_angle(object_pose[2])
-        self.update_scale(object_pose[3])
+    def update_posebin(self, object_pose, img_size, keypoint_pair):
+        """One vote: every mean moves with the OLD count, then the pair is appended and the
+        count incremented (the reference's order, ``PoseBin.py:45-51``)."""
+        x, y, alpha, s = object_pose[:4]
+        self.update_centroid((x, y))
+        self.update_angle(alpha)
+        self.update_scale(s)
         self.update_img_size(img_size)
         self.add_keypoint_pair(keypoint_pair)
         self.add_vote()
@@ -55,29 +73,31 @@ class PoseBin:
     def add_vote(self, new_votes=1):
         self.votes += new_votes
 
-    def get_pts(self):                                    # PoseBin.py:56-67
-        if not self.keypoint_pairs:
-            e = np.array([])
-            return e, e.copy(), e.copy(), e.copy()
-        q = np.array([p[1].pt for p in self.keypoint_pairs], np.float64)
-        m = np.array([p[0].pt for p in self.keypoint_pairs], np.float64)
-        return q[:, 0], q[:, 1], m[:, 0], m[:, 1]
+    # ---- members ------------------------------------------------------------------------
+    def add_keypoint_pair(self, pair):
+        self.keypoint_pairs.append(pair)
 
     def remove_keypoint_pair(self, pair):
         self.keypoint_pairs.remove(pair)
 
+    def get_pts(self):
+        """(query x, query y, model x, model y) as f64 arrays in member order."""
+        n = len(self.keypoint_pairs)
+        pts = np.empty((4, n), np.float64)
+        for j, pair in enumerate(self.keypoint_pairs):
+            pts[0:2, j] = pair[1].pt
+            pts[2:4, j] = pair[0].pt
+        return pts[0], pts[1], pts[2], pts[3]
+
+    # ---- identity -----------------------------------------------------------------------
     def is_same_pose(self, pose):
-        return pose == self.pose
+        return self.pose == pose
 
     def __eq__(self, other):
-        if isinstance(other, PoseBin):
-            return other.pose == self.pose
-        return False
-
-    __hash__ = None   # like the reference (defines __eq__ only)
+        return isinstance(other, PoseBin) and self.pose == other.pose
 
     def __repr__(self):
-        return "[" + str(self.pose) + ", " + str(self.votes) + ", " + str(self.img_size) + "]"
+        return f"[{self.pose}, {self.votes}, {self.img_size}]"
 
     def __str__(self):
-        return "Pose: " + str(self.pose)
+        return f"Pose: {self.pose}"

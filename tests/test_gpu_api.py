@@ -282,6 +282,49 @@ def test_shared_db_contexts():
     np.testing.assert_array_equal(ref_b[2]["params"], got_b[2]["params"])
 
 
+def test_shared_db_write_rules():
+    """sod_db_share bookkeeping: the owner refuses DB writes while a context aliases its DB;
+    sharing from a sharer shares from the owner; a DB write on a sharer detaches it (its
+    own buffers, never the owner's); destroying the owner detaches what is left."""
+    db = synthetic.make_database(4, 300, seed=81)
+    db2 = synthetic.make_database(4, 300, seed=82)
+    qs = synthetic.make_queries(600, seed=83, db_seed=81, kp_per_image=300)
+    with _lib.Context(0) as c0:
+        c0.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c0.upload_db(db.des)
+        c0.upload_queries(qs.des, qs.kp)
+        c0.pipeline(qs.shape, 15)
+        ref = c0.match_result()
+        c1, c2 = _lib.Context(0), _lib.Context(0)
+        c1.share_db(c0)
+        c2.share_db(c1)                              # shares from the owner, c0
+        for bad in (lambda: c0.upload_db(db2.des),
+                    lambda: c0.set_keypoints(db2.kp, db2.img, db2.centroid, db2.size),
+                    lambda: c0.set_impl("bf16")):
+            with pytest.raises(_lib.SodError, match="sod_db_share"):
+                bad()
+        # c1 takes a DB of its own: c0's stays intact for c0 and c2
+        c1.set_keypoints(db2.kp, db2.img, db2.centroid, db2.size)
+        c1.upload_db(db2.des)
+        for c in (c0, c2):
+            c.upload_queries(qs.des, qs.kp)
+            c.pipeline(qs.shape, 15)
+            for x, y in zip(ref, c.match_result()):
+                assert np.array_equal(x, y)
+        c1.close()
+        with pytest.raises(_lib.SodError, match="sod_db_share"):
+            c0.upload_db(db.des)                     # c2 still aliases it
+        c2.close()
+        c0.upload_db(db.des)                         # no sharer left
+        # the owner destroyed first: its sharer reports "no database", reads nothing freed
+        c3 = _lib.Context(0)
+        c3.share_db(c0)
+        c3.upload_queries(qs.des, qs.kp)
+    with pytest.raises(_lib.SodError):
+        c3.pipeline(qs.shape, 15)
+    c3.close()
+
+
 @pytest.mark.parametrize("use_comm,reserve", [(False, 0), (True, 0), (False, 1), (True, 1)])
 def test_matcher_overlap_equals_serial(use_comm, reserve):
     """sod_match_set_overlap: the matcher kernel on its own stream, overlapping the previous
@@ -307,12 +350,12 @@ def test_matcher_overlap_equals_serial(use_comm, reserve):
             c.pipeline(qs.shape, bins)
             ref.append(collect(c))
     with _lib.Context(0) as c:
-        if use_comm:
-            c.comm_init(1, 0, _lib.unique_id())
         if reserve:
             c.set_cu_reserve(reserve)
         else:
             c.set_overlap(True)
+        if use_comm:      # under the split: channels capped at the reserved CU count
+            c.comm_init(1, 0, _lib.unique_id())
         c.set_keypoints(db.kp, db.img, db.centroid, db.size)
         c.upload_db(db.des)
         got = []
@@ -337,3 +380,25 @@ def test_matcher_overlap_equals_serial(use_comm, reserve):
         assert np.array_equal(b0[0], b1[0]) and np.array_equal(b0[1], b1[1])
         assert np.array_equal(a0["survived"], a1["survived"])
         assert np.array_equal(a0["params"], a1["params"])
+
+
+def test_cu_reserve_channel_cap(monkeypatch):
+    """The CU split runs collectives on the reserved CUs only, so every block of an RCCL
+    kernel must fit there: a communicator created with more channels than reserved CUs is
+    refused in either order (split then comm, comm then split)."""
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "16")
+    with _lib.Context(0) as c:
+        c.comm_init(1, 0, _lib.unique_id())
+        with pytest.raises(_lib.SodError, match="NCCL_MAX_NCHANNELS"):
+            c.set_cu_reserve(1)                       # 8 reserved CUs < 16 channels
+        c.set_cu_reserve(2)                           # 16 reserved CUs: fits
+        c.set_cu_reserve(0)
+    with _lib.Context(0) as c:
+        c.set_cu_reserve(1)
+        with pytest.raises(_lib.SodError, match="NCCL_MAX_NCHANNELS"):
+            c.comm_init(1, 0, _lib.unique_id())
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "8")
+    with _lib.Context(0) as c:
+        c.comm_init(1, 0, _lib.unique_id())
+        c.set_cu_reserve(1)
+        c.set_cu_reserve(0)

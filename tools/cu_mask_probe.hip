@@ -24,7 +24,7 @@ __global__ void probe(uint32_t* out) {
 
 static void run(const char* name, const std::vector<uint32_t>& mask) {
   hipStream_t s;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size() * 32, mask.data()) != hipSuccess) {
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data())  /* words */ != hipSuccess) {
     printf("%s: stream create failed\n", name);
     return;
   }
