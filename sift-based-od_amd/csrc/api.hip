@@ -245,7 +245,7 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->qx); sod_release(ctx->qy); sod_release(ctx->qang); sod_release(ctx->qoct);
   sod_release(ctx->stage_u8); sod_release(ctx->stage_f32);
   sod_release(ctx->pd1); sod_release(ctx->pd2); sod_release(ctx->pidx);
-  sod_release(ctx->cd1); sod_release(ctx->cd2); sod_release(ctx->cidx);
+  sod_release(ctx->cd1); sod_release(ctx->cd2); sod_release(ctx->cidx); sod_release(ctx->gthr);
   sod_release(ctx->gd1); sod_release(ctx->gd2); sod_release(ctx->gidx);
   sod_release(ctx->d1); sod_release(ctx->d2); sod_release(ctx->idx1); sod_release(ctx->good);
   sod_release(ctx->flags); sod_release(ctx->sig_lut); sod_release(ctx->counts);

@@ -289,9 +289,12 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
 __global__ void merge_kernel(const float* __restrict__ d1, const int* __restrict__ idx,
                              const float* __restrict__ d2, int nparts, int64_t stride, int64_t nq,
                              float* __restrict__ od1, int* __restrict__ oidx,
-                             float* __restrict__ od2) {
+                             float* __restrict__ od2, int* __restrict__ reset) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
+  // the matcher's shared thresholds of this partial-result slot: "nothing known" again for
+  // the next launch that takes the slot (it waits for this merge)
+  if (reset) reset[q] = (int)0x80808080;
   float v1 = d1[q], v2 = d2[q];
   int i1 = idx[q];
   for (int p = 1; p < nparts; ++p)
@@ -422,11 +425,11 @@ int launch_match(sod_ctx* ctx) {
 }
 
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2, int nparts,
-                 int64_t stride) {
+                 int64_t stride, int32_t* reset) {
   const int64_t nq_pad = sod_nq_pad(ctx);
   const int bs = 256;
   hipLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, bs)), dim3(bs), 0, ctx->stream,
-                     d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p, ctx->cd2.p);
+                     d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p, ctx->cd2.p, reset);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }

@@ -31,6 +31,7 @@
 // instead of 12 and half the MFMA issue holds, but the chip holds ~2.03 GHz on it vs ~2.2 on
 // 16x16x64: 4.7 vs 4.0-4.2 ms; kept as an option).
 #include <climits>
+#include <cstdlib>
 
 #include "sod_internal.h"
 
@@ -39,7 +40,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 namespace {
 
-constexpr int QT = 8;          // 16-query tiles per wave
+// QT = 16-query tiles per wave (a template parameter: 8 for large query sets, 4 / 2 so that
+// small ones still fill every wave and get longer DB chunks; launch_match_i8 chooses)
 #ifndef SOD_I8_NW
 #define SOD_I8_NW 8
 #endif
@@ -159,6 +161,24 @@ __device__ __forceinline__ void issue_norms(const int* __restrict__ dn, int64_t 
   if (lane < 2 * L) glds16(src, slot_norm + wave * (8 * R));
 }
 
+#ifndef SOD_I8_DMA
+#define SOD_I8_DMA 1       // 1: descriptor refill as buffer loads (SGPR offsets, no address VALU),
+#endif                     //    one 1 KiB piece per subtile over the stage; 0: burst at the barrier
+#ifndef SOD_I8_XCHUNK
+#define SOD_I8_XCHUNK 1    // thresholds shared between the DB chunks of a query (global max)
+#endif
+#if SOD_I8_DMA || SOD_I8_XCHUNK
+// buffer descriptor word 3 for CDNA (raw, untyped, 32-bit format field as the loads ignore it)
+constexpr int kRsrcWord3 = 0x00020000;
+#endif
+
+// one 1 KiB piece of a stage: lane i's 16 B land at slot + 16 i (M0 = the LDS piece base)
+__device__ __forceinline__ void issue_piece(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_piece,
+                                            uint32_t soff, int lane) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_piece, 16, (uint32_t)lane * 16u,
+                                           soff, 0, 0);
+}
+
 __device__ __forceinline__ void issue_stage(const uint8_t* __restrict__ dbpack,
                                             const int* __restrict__ dn, int64_t npad, int64_t sub0,
                                             uint8_t* slot, uint8_t* norm_slot, int wave, int lane) {
@@ -223,9 +243,11 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #define SOD_I8_DENSE 32    // leading subtiles of a chunk updated without threshold exchange (C2: +8 %)
 #endif
 constexpr int64_t kDense = SOD_I8_DENSE;
+constexpr int kShareLoad = 8, kShareApply = 24;   // subtiles of a stage (SOD_I8_XCHUNK)
 #ifndef SOD_SHARED_T
 #define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
 #endif
+
 constexpr int kRing = SOD_I8_RING;
 constexpr int kLoadsPerStage = kPiecesPerWave + 1;   // vm instructions per wave per stage
 
@@ -266,9 +288,11 @@ __device__ unsigned long long g_counts[8];
 // mode (wave-uniform): 0 = prefilter; 1 = dense (the chunk's first subtiles, where
 // t2 is still -inf and every tile takes the exact update: the threshold exchange is
 // skipped); 2 = the last dense subtile (the exchange then sets every tile's t2).
+template <int QT>
 __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin, int rowb,
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
-                                            int (&id)[QT], bool early = false, int mode = 0) {
+                                            int (&id)[QT], bool early = false, int mode = 0,
+                                            bool vmem = false) {
   uint64_t hit[QT];
   uint64_t any = 0;
 #pragma unroll
@@ -285,6 +309,7 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
     __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);                            // MFMA
     if (i < 3 * QT / 2) __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);       // VALU
     if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+    if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);      // refill piece
   }
 #endif
 #if SOD_I8_COLD
@@ -350,11 +375,12 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
 
 // One work unit: query block qb (NW16*QT tiles) against DB chunk sp (sub_per_split subtiles),
 // writing the chunk's partial top-2 of every query to slot sp of pd1/pidx/pd2.
+template <int QT>
 __device__ __forceinline__ void match_unit(
     uint8_t* lds, int sp, int qb, const uint8_t* __restrict__ dbpack, const int* __restrict__ dn,
     int64_t nsub, const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt,
     int64_t nq_pad, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
-    int* __restrict__ pidx, float* __restrict__ pd2) {
+    int* __restrict__ pidx, float* __restrict__ pd2, int* __restrict__ gthr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qt0 = (qb * NW16 + wave) * QT;
   const int64_t s_lo = (int64_t)sp * sub_per_split;
@@ -368,6 +394,12 @@ __device__ __forceinline__ void match_unit(
     if (j < nst)
       issue_stage(dbpack, dn, npad, s_lo + j * SPS, lds + j * kStageBytes, nring + j * kStageNorm,
                   wave, lane);
+#if SOD_I8_DMA
+  static_assert(kRing == 2, "spread refill: the slot refilled during stage s is stage s-1's");
+  // the chunk's descriptors as one buffer (< 2 GiB: launch_match_i8 sizes the chunks)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dbpack + s_lo * kSub), (short)0, (int)((s_hi - s_lo) * kSub), kRsrcWord3);
+#endif
 
   i32x4 bq[QT][2];
 #pragma unroll
@@ -387,6 +419,22 @@ __device__ __forceinline__ void match_unit(
     id[t] = 0x7fffffff;
   }
   const int rowl = row_offset + (int)(s_lo * kSubRows) + (lane >> 4) * 4;
+#if SOD_I8_XCHUNK
+  // Chunks of the same queries share their prefilter thresholds: gthr[q] = max over chunks of
+  // the t2 (= query-wide second best >> 1) they published.  A chunk holding t2 has two rows
+  // with y >= 2 t2, so a row below it can never be in the query's global top-2 (ties pass the
+  // >= test): any chunk may skip it.  At each stage boundary a wave publishes its tiles' t2
+  // (buffer atomic max, lanes of one lane group, only where above the last value read) and
+  // DMAs the current global values of its 128 queries into LDS, which the next boundary
+  // applies -- a value one stage old, or stale across XCDs, is still a valid bound, so
+  // nothing waits for it.  The chunk's own top-2 stays exact over the rows it keeps.
+  const int wq = __builtin_amdgcn_readfirstlane(wave);
+  const int ntile = max(0, min(QT, nqt - (qb * NW16 + wq) * QT));   // real tiles of the wave
+  int* const gw = gthr + (int64_t)(qb * NW16 + wq) * QT * 16;   // the wave's queries
+  const __amdgpu_buffer_rsrc_t rg =
+      __builtin_amdgcn_make_buffer_rsrc((void*)gw, (short)0, ntile * 64, kRsrcWord3);
+  uint8_t* const gl = lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64);
+#endif
 #if SOD_I8_PIPE
   // accumulators, norms and first row of the subtile whose prefilter is pending; the
   // initial "previous subtile" is empty (h = INT_MIN can never pass t2)
@@ -415,11 +463,24 @@ __device__ __forceinline__ void match_unit(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!(SOD_I8_EXP & 4)) __builtin_amdgcn_s_barrier();
     // every wave has finished stage s-1, so its slot takes stage s+kRing-1
+#if SOD_I8_DMA
+    // (descriptor pieces spread over this stage's first subtiles below; norms now)
+    if (!(SOD_I8_EXP & 1) && s + 1 < nst)
+      issue_norms<NW16, kStageRows>(dn, npad, (s_lo + (s + 1) * SPS) * kSubRows,
+                                    nring + ((s + 1) % kNormRing) * kStageNorm, wave, lane);
+    // the last stage re-reads itself into the free slot (never read again): the pieces stay
+    // unconditional, so no branch splits the subtile blocks
+    const int wv = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform: SGPR offsets
+    uint8_t* const refill = lds + (slot == 0 ? 1 : 0) * kStageBytes + wv * kPiecesPerWave * 1024;
+    const uint32_t refill_off =
+        (uint32_t)(min<int64_t>(s + 1, nst - 1) * kStageBytes + wv * kPiecesPerWave * 1024);
+#else
     if (!(SOD_I8_EXP & 1) && s + kRing - 1 < nst) {
       const int ns = slot == 0 ? kRing - 1 : slot - 1;
       issue_stage(dbpack, dn, npad, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageBytes,
                   nring + ((s + kRing - 1) % kNormRing) * kStageNorm, wave, lane);
     }
+#endif
     const uint8_t* sb = lds + slot * kStageBytes;
     const uint8_t* nb0 = nring + (s % kNormRing) * kStageNorm + norm_off(0, lane >> 4);
     slot = slot + 1 == kRing ? 0 : slot + 1;
@@ -445,6 +506,14 @@ __device__ __forceinline__ void match_unit(
 #pragma unroll
       for (int t = 0; t < QT; ++t)
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq[t][0], c, 0, 0, 0);
+#if SOD_I8_DMA
+      // piece u of the next stage (wave-uniform branch; u is a constant after unrolling)
+      const bool piece_here = u < kPiecesPerWave;
+      if (piece_here && !(SOD_I8_EXP & 1))
+        issue_piece(rs, refill + u * 1024, refill_off + u * 1024, lane);
+#else
+      const bool piece_here = false;
+#endif
       if (u + 1 < SPS) {   // next subtile's fragments in flight
         const uint8_t* nb = sb + (u + 1) * kSub + lane * 16;
         fa0 = *reinterpret_cast<const i32x4*>(nb);
@@ -472,19 +541,42 @@ __device__ __forceinline__ void match_unit(
         // the pending subtile's index in the chunk decides dense / final / prefilter
         const int64_t kp = s * SPS + u - 1;
         const int mode = kp < kDense - 1 ? 1 : (kp == kDense - 1 ? 2 : 0);
-        tile_update(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode);
+        tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t) accp[t] = acc[t];
       pp = p;
       rowp = rowb;
+#if SOD_I8_XCHUNK
+      // shared thresholds, twice per stage: at subtile kShareLoad the wave DMAs the global
+      // values of its queries into LDS; at kShareApply (they landed: vmcnt(0), the stage's
+      // refill pieces went out before the load) it publishes its own t2 where above them and
+      // raises t2 to them
+      if (u == kShareLoad && lane < QT * 4)   // the wave's QT x 16 values: QT*4 lanes x 16 B
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_void*)gl, 16, (uint32_t)lane * 16u, 0,
+                                                 0, 16 /* sc1: past this XCD's L2 */);
+      if (u == kShareApply) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15);
+        int gq[QT];
+#pragma unroll
+        for (int t = 0; t < QT; ++t) gq[t] = gv[16 * t];   // all reads, then one wait
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          if (lane < 16 && t < ntile && t2[t] > gq[t])
+            __hip_atomic_fetch_max(gw + 16 * t + lane, t2[t], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          t2[t] = max(t2[t], gq[t]);
+        }
+      }
+#endif
 #else
-      tile_update(acc, p, rowb, y1, y2, t2, id);
+      tile_update<QT>(acc, p, rowb, y1, y2, t2, id);
 #endif
     }
   }
 #if SOD_I8_PIPE
-  tile_update(accp, pp, rowp, y1, y2, t2, id, false, nst * SPS <= kDense ? 1 : 0);
+  tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, false, nst * SPS <= kDense ? 1 : 0);
 #endif
 #ifdef SOD_I8_COUNT
   if (lane == 0) atomicAdd(&g_counts[2], (unsigned long long)(nst * SPS));
@@ -516,12 +608,14 @@ __device__ __forceinline__ void match_unit(
 __device__ unsigned long long g_stamps[4096][8];
 #endif
 
-__global__ __launch_bounds__(NT16, 8 / NW16) void match_i8_kernel(
+template <int QT>
+__global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
-    int* __restrict__ pidx, float* __restrict__ pd2, int nqb) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageBytes + kNormRing * kStageNorm];
+    int* __restrict__ pidx, float* __restrict__ pd2, int nqb, int* __restrict__ gthr) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageBytes + kNormRing * kStageNorm +
+                                                     SOD_I8_XCHUNK * NW16 * QT * 64];
 #ifdef SOD_I8_STAMP
   unsigned long long t0 = 0, r0 = 0;
   if (threadIdx.x == 0) {
@@ -535,11 +629,11 @@ __global__ __launch_bounds__(NT16, 8 / NW16) void match_i8_kernel(
   // instead of all of them (bijective for any grid size; cdna_hip_programming.md T1)
   const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = blockIdx.x % 8;
   const unsigned u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blockIdx.x / 8;
-  match_unit(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
-             sub_per_split, row_offset, pd1, pidx, pd2);
+  match_unit<QT>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
+             sub_per_split, row_offset, pd1, pidx, pd2, gthr);
 #else
-  match_unit(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
-             nq_pad, sub_per_split, row_offset, pd1, pidx, pd2);
+  match_unit<QT>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
+             nq_pad, sub_per_split, row_offset, pd1, pidx, pd2, gthr);
 #endif
 #ifdef SOD_I8_STAMP
   if (threadIdx.x == 0 && blockIdx.x < 4096) {
@@ -834,11 +928,29 @@ extern "C" int sod_debug_stamps(unsigned long long* out, int n) {
 }
 #endif
 
+// Query tiles per wave for the 16x16x64 kernel.  A work-group holds 8*QT tiles; the chip is
+// filled by splitting the DB into chunks, and every chunk restarts its queries' top-2 (the
+// dense early phase), so fewer queries per work-group buy longer chunks and no padding tiles
+// for small query sets, at more LDS reads per MFMA.  SOD_MATCH_QT overrides (experiments).
+static int pick_qt(int32_t nqt) {
+  if (const char* e = std::getenv("SOD_MATCH_QT")) {
+    const int v = std::atoi(e);
+    if (v == 2 || v == 4 || v == 8) return v;
+  }
+  // measured (C3-sized DB, one MI355X): 8 from ~16 work-groups of 1024 queries up (20k
+  // queries: 8 is 3 % faster than 4), 4 below (10k x 100k: 11 % faster than 8; 2k x 1M: 12 %),
+  // 2 for one query image (500 queries: 2 and 4 equal, both 38 % faster than 8)
+  if (nqt >= 64 * 16) return 8;
+  if (nqt > 32) return 4;
+  return 2;
+}
+
 int launch_match_i8(sod_ctx* ctx) {
   const bool wide = ctx->impl == 2;
   const int rows = wide ? 32 : kSubRows;
   const int sps = wide ? w::SPS : SPS;
-  const int qt_per_wg = wide ? w::NW * w::QT : NW16 * QT;
+  const int qt = wide ? w::QT : pick_qt(ctx->nqt);
+  const int qt_per_wg = wide ? w::NW * w::QT : NW16 * qt;
   const int64_t nq_pad = (int64_t)ctx->nqt * rows;
   const int64_t qblocks = cdiv(ctx->nqt, qt_per_wg);
   const int64_t nstages = ctx->nsub / sps;
@@ -848,7 +960,10 @@ int launch_match_i8(sod_ctx* ctx) {
   // (rounded down: one work-group more than the slots would run as a second round)
   int64_t split = std::max<int64_t>(1, slots / qblocks);
   split = std::min<int64_t>(split, nstages);
-  const int64_t st_per_split = cdiv(nstages, split);
+  int64_t st_per_split = cdiv(nstages, split);
+  // a chunk is addressed through one buffer descriptor (32-bit byte offsets): < 1 GiB each
+  const int64_t max_st = ((int64_t)1 << 30) / (wide ? w::kStageBytes : kStageBytes);
+  if (st_per_split > max_st) st_per_split = max_st;
   split = cdiv(nstages, st_per_split);
   ctx->split = (int)split;
   SOD_TRY(sod_reserve(ctx, ctx->cd1, (size_t)nq_pad));
@@ -858,6 +973,23 @@ int launch_match_i8(sod_ctx* ctx) {
   float *pd1, *pd2;
   int32_t* pidx;
   SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
+  // shared thresholds, one array per partial-result slot: "nothing known" is bytes 0x80 (below
+  // every reachable t2); the merge that releases a slot resets its array for the next launch,
+  // a new query count (slot layout) resets both here (stream_begin waited for both merges)
+  int32_t* gthr = nullptr;
+  if (!wide) {
+    const int64_t nslot = ctx->overlap ? 2 : 1;
+    if (ctx->gthr.n < (size_t)(2 * nq_pad) || ctx->gthr_n != nq_pad) {
+      if (ctx->gthr.n < (size_t)(2 * nq_pad)) {
+        SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
+        SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        SOD_TRY(sod_reserve(ctx, ctx->gthr, (size_t)(2 * nq_pad)));
+      }
+      SOD_HIP(ctx, hipMemsetAsync(ctx->gthr.p, 0x80, (size_t)(nslot * nq_pad) * 4, ks));
+      ctx->gthr_n = nq_pad;
+    }
+    gthr = ctx->gthr.p + ctx->pslot * nq_pad;
+  }
   SOD_TRY(sod_match_mark(ctx, ks, 0));
   if (wide)
     hipLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0,
@@ -865,15 +997,19 @@ int launch_match_i8(sod_ctx* ctx) {
                        ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt,
                        nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, pd1,
                        pidx, pd2, (int)qblocks);
-  else
-    hipLaunchKernelGGL(match_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(NT16), 0, ks,
-                       ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,
-                       ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,
-                       (int)split, st_per_split * sps, (int)ctx->row_offset, pd1,
-                       pidx, pd2, (int)qblocks);
+  else {
+#define SOD_LAUNCH_I8(Q)                                                                      \
+  hipLaunchKernelGGL(match_i8_kernel<Q>, dim3((unsigned)(qblocks * split)), dim3(NT16), 0, ks,  \
+                     ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,        \
+                     ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,  \
+                     (int)split, st_per_split * sps, (int)ctx->row_offset, pd1, pidx, pd2,     \
+                     (int)qblocks, gthr)
+    if (qt == 8) SOD_LAUNCH_I8(8); else if (qt == 4) SOD_LAUNCH_I8(4); else SOD_LAUNCH_I8(2);
+#undef SOD_LAUNCH_I8
+  }
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(sod_match_mark(ctx, ks, 1));
   SOD_TRY(sod_match_stream_end(ctx));
-  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad));
+  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, gthr));
   return sod_partials_merged(ctx);   // the slot is free again
 }

@@ -82,6 +82,8 @@ struct sod_ctx {
   DevBuf<int32_t> pidx;
   DevBuf<float> cd1, cd2;       // merged (this shard / after allgather: global)  [nq_pad]
   DevBuf<int32_t> cidx;
+  DevBuf<int32_t> gthr;         // matcher: prefilter thresholds shared by the DB chunks
+  int64_t gthr_n = 0;           //   [partial-result slot][nq_pad]; reset by the slot's merge
   DevBuf<float> gd1, gd2;       // allgather landing [nranks * nq_pad]
   DevBuf<int32_t> gidx;
   DevBuf<float> d1, d2;         // sqrt distances [nq]
@@ -249,7 +251,7 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
 int sod_match_stream_end(sod_ctx* ctx);
 int sod_partials_merged(sod_ctx* ctx);
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2,
-                 int nparts, int64_t stride);
+                 int nparts, int64_t stride, int32_t* reset = nullptr);
 int launch_ratio(sod_ctx* ctx, double ratio);
 int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi);
 int launch_select(sod_ctx* ctx, int32_t thr);
