@@ -350,9 +350,9 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
           int g1 = y1[t], g2 = y2[t];
           top2_xor32(g1, g2);
           top2_xor16(g1, g2);
-          t2[t] = g2 >> 1;
+          t2[t] = max(t2[t], g2 >> 1);   // never below a shared bound already applied
 #else
-          t2[t] = y2[t] >> 1;
+          t2[t] = max(t2[t], y2[t] >> 1);
 #endif
         }
       }
@@ -364,9 +364,9 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
         int g1 = y1[t], g2 = y2[t];
         top2_xor32(g1, g2);
         top2_xor16(g1, g2);
-        t2[t] = g2 >> 1;
+        t2[t] = max(t2[t], g2 >> 1);
 #else
-        t2[t] = y2[t] >> 1;
+        t2[t] = max(t2[t], y2[t] >> 1);
 #endif
       }
     }

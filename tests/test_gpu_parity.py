@@ -73,6 +73,34 @@ def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
     assert np.array_equal(good, orc.ratio_test(f1, f2))
 
 
+@pytest.mark.parametrize("qt", ["2", "4", "8"])
+def test_matcher_query_tiles_shared_thresholds(ctx, monkeypatch, qt):
+    """int8 matcher with each query-tile count per wave (SOD_MATCH_QT) over a DB split into
+    many chunks, so the chunks exchange prefilter thresholds mid-run: DB rows duplicated far
+    apart (other chunks) make exact distance ties ACROSS chunks -- a shared threshold must
+    keep them (lowest trainIdx wins), and queries equal to a DB row (d1 = 0) or near one."""
+    monkeypatch.setenv("SOD_MATCH_QT", qt)
+    rng = np.random.default_rng(31)
+    ndb, nq = 150000, 2000
+    db = synthetic.sift_like_descriptors(rng, ndb)
+    db[100000:100600] = db[0:600]                      # ties across chunks
+    db[140000:140300] = db[50000:50300]
+    q = synthetic.sift_like_descriptors(rng, nq)
+    q[:600] = np.clip(db[:600].astype(int) + rng.integers(-2, 3, (600, 128)), 0, 255)
+    q[600:900] = db[50000:50300]                       # d1 = d2 = 0, two equal rows
+    ctx.set_impl("i8")
+    ctx.upload_db(db)
+    ctx.upload_queries(q)
+    for _ in range(2):        # the second launch reuses the reset threshold slot
+        ctx.match()
+    ctx.ratio(0.75)
+    idx1, d1, d2, good = ctx.match_result()
+    e1, f1, f2 = orc.knn2_match(q, db)
+    assert np.array_equal(idx1, e1)
+    assert np.array_equal(d1, f1) and np.array_equal(d2, f2)
+    assert np.array_equal(good, orc.ratio_test(f1, f2))
+
+
 @pytest.mark.parametrize("impl", IMPLS)
 def test_matcher_f32_input_and_validation(ctx, impl):
     rng = np.random.default_rng(11)
