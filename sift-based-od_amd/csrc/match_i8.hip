@@ -243,7 +243,18 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #define SOD_I8_DENSE 32    // leading subtiles of a chunk updated without threshold exchange (C2: +8 %)
 #endif
 constexpr int64_t kDense = SOD_I8_DENSE;
-constexpr int kShareLoad = 8, kShareApply = 24;   // subtiles of a stage (SOD_I8_XCHUNK)
+// shared-threshold exchange points (subtiles of a stage, SOD_I8_XCHUNK): the DMA issued at
+// kShareLoad[i] is applied at kShareApply[i] (the same stage when it is later, else the next)
+#ifndef SOD_I8_SHARE2
+#define SOD_I8_SHARE2 0
+#endif
+#if SOD_I8_SHARE2
+__device__ __forceinline__ constexpr bool share_load(int u) { return u == 8 || u == 24; }
+__device__ __forceinline__ constexpr bool share_apply(int u) { return u == 20 || u == 12; }
+#else
+__device__ __forceinline__ constexpr bool share_load(int u) { return u == 8; }
+__device__ __forceinline__ constexpr bool share_apply(int u) { return u == 24; }
+#endif
 #ifndef SOD_SHARED_T
 #define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
 #endif
@@ -552,10 +563,10 @@ __device__ __forceinline__ void match_unit(
       // values of its queries into LDS; at kShareApply (they landed: vmcnt(0), the stage's
       // refill pieces went out before the load) it publishes its own t2 where above them and
       // raises t2 to them
-      if (u == kShareLoad && lane < QT * 4)   // the wave's QT x 16 values: QT*4 lanes x 16 B
+      if (share_load(u) && lane < QT * 4)   // the wave's QT x 16 values: QT*4 lanes x 16 B
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_void*)gl, 16, (uint32_t)lane * 16u, 0,
                                                  0, 16 /* sc1: past this XCD's L2 */);
-      if (u == kShareApply) {
+      if (share_apply(u) && (SOD_I8_SHARE2 == 0 || u != 12 || s > 0)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15);
         int gq[QT];
@@ -575,6 +586,9 @@ __device__ __forceinline__ void match_unit(
 #endif
     }
   }
+  // LDS-DMA still in flight (the last stage's refill pieces re-read that stage, a shared-
+  // threshold load) must land before the work-group's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if SOD_I8_PIPE
   tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, false, nst * SPS <= kDense ? 1 : 0);
 #endif
