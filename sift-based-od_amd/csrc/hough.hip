@@ -408,49 +408,98 @@ __global__ __launch_bounds__(1024) void member_offsets_kernel(const uint32_t* __
   }
 }
 
-// members, step 1: every vote into a valid bin reserves a slot in its bin's member list.
-// A bin voted by many matches (a real object: thousands of votes) would serialise on one
-// global cursor, so the votes of a wave are aggregated first: per vote slot, the lanes
-// voting for the same bin take ONE atomicAdd (leader = lowest lane) and place their
-// queries in lane order inside the reserved run.  No LDS, no block barrier: the kernel
-// keeps full occupancy on the few CUs a reserved tail has (sod_set_cu_reserve).  Runs land
-// in arbitrary order; member_order_*_kernel sort each bin into query order afterwards.
-__global__ __launch_bounds__(256) void member_fill_kernel(
-    int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
-    const int* __restrict__ qimg, int64_t nbins1, const uint32_t* __restrict__ vidx,
-    const int64_t* __restrict__ voff,
+// members, step 1 (valid-bin count known to fit LDS): a work-group takes 256 consecutive
+// queries.  Their votes first reserve LDS slots per valid bin (local rank = the LDS atomic's
+// return), then ONE global atomicAdd per (work-group, bin it touched) reserves the run in
+// the bin's member list -- those atomics are independent, so a wave has them all in flight
+// at once instead of one returning atomic per distinct bin after another (the chain that
+// made the per-wave aggregation latency-bound on the few reserved CUs).  Runs land in
+// arbitrary order; member_order_*_kernel sort each bin into query order afterwards.
+// With V beyond the LDS table every wave aggregates its own votes instead: per vote slot,
+// the lanes voting for the same bin take ONE atomicAdd (leader = lowest lane) and place
+// their queries in lane order inside the reserved run.
+constexpr int kFillMaxV = 12288;   // 48 KiB of u32 per work-group
+constexpr int kFillBatch = 8;      // global atomics a thread keeps in flight
+
+__device__ __forceinline__ void fill_wave_aggregated(
+    int64_t q, bool in, uint32_t m, uint32_t k, uint32_t base, Bins b,
+    const uint32_t* __restrict__ vidx, const int64_t* __restrict__ voff,
     uint32_t* __restrict__ cursor, int32_t* __restrict__ members) {
   const int lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t q0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); q0 < nq; q0 += stride) {
-    const int64_t q = q0 + lane;
-    uint32_t m = 0, k = 0, base = 0;
-    if (q < nq) {
-      m = vmask[q] & 0xFFFFu;
-      k = basekey[q];
-      base = qimg ? (uint32_t)(qimg[q] * nbins1) : 0u;
-    }
-    if (__ballot(m != 0) == 0) continue;
-    const int ix = k & 0xFF, iy = (k >> 8) & 0xFF, it = (k >> 16) & 0xFF, is = k >> 24;
-    for (int slot = 0; slot < 16; ++slot) {
-      uint32_t v = 0xFFFFFFFFu;
-      if ((m >> slot) & 1u)
-        v = vidx[base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
-                                it + ((slot >> 1) & 1), is + (slot & 1), b)];
-      uint64_t pend = __ballot(v != 0xFFFFFFFFu);
-      while (pend) {                                   // one round per distinct bin
-        const int leader = __ffsll((unsigned long long)pend) - 1;
-        const uint32_t vv = __shfl(v, leader);
-        const uint64_t same = __ballot(v == vv);
-        uint32_t r = 0;
-        if (lane == leader) r = atomicAdd(&cursor[vv], (uint32_t)__popcll(same));
-        r = __shfl(r, leader);
-        if (v == vv) members[voff[vv] + r + __popcll(same & below)] = (int32_t)q;
-        pend &= ~same;
-      }
+  if (__ballot(in && m != 0) == 0) return;
+  const int ix = k & 0xFF, iy = (k >> 8) & 0xFF, it = (k >> 16) & 0xFF, is = k >> 24;
+  for (int slot = 0; slot < 16; ++slot) {
+    uint32_t v = 0xFFFFFFFFu;
+    if (in && ((m >> slot) & 1u))
+      v = vidx[base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                              it + ((slot >> 1) & 1), is + (slot & 1), b)];
+    uint64_t pend = __ballot(v != 0xFFFFFFFFu);
+    while (pend) {
+      const int leader = __ffsll((unsigned long long)pend) - 1;
+      const uint32_t vv = __shfl(v, leader);
+      const uint64_t same = __ballot(v == vv);
+      uint32_t r = 0;
+      if (lane == leader) r = atomicAdd(&cursor[vv], (uint32_t)__popcll(same));
+      r = __shfl(r, leader);
+      if (v == vv) members[voff[vv] + r + __popcll(same & below)] = (int32_t)q;
+      pend &= ~same;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void member_fill_lds_kernel(
+    int64_t nq, const uint32_t* __restrict__ scal, const uint32_t* __restrict__ basekey,
+    const uint32_t* __restrict__ vmask, Bins b, const int* __restrict__ qimg, int64_t nbins1,
+    const uint32_t* __restrict__ vidx, const int64_t* __restrict__ voff,
+    uint32_t* __restrict__ cursor, int32_t* __restrict__ members) {
+  __shared__ uint32_t cnt[kFillMaxV];
+  const int64_t V = scal[0];
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool in = q < nq;
+  uint32_t m = 0, k = 0, base = 0;
+  if (in) {
+    m = vmask[q] & 0xFFFFu;
+    k = basekey[q];
+    base = qimg ? (uint32_t)(qimg[q] * nbins1) : 0u;
+  }
+  if (V > kFillMaxV) {   // uniform over the grid
+    fill_wave_aggregated(q, in, m, k, base, b, vidx, voff, cursor, members);
+    return;
+  }
+  for (int64_t i = threadIdx.x; i < V; i += 256) cnt[i] = 0;
+  __syncthreads();
+  const int ix = k & 0xFF, iy = (k >> 8) & 0xFF, it = (k >> 16) & 0xFF, is = k >> 24;
+  uint32_t v[16], r[16];
+#pragma unroll
+  for (int slot = 0; slot < 16; ++slot)   // independent loads, one wait
+    v[slot] = ((m >> slot) & 1u)
+                  ? vidx[base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                        it + ((slot >> 1) & 1), is + (slot & 1), b)]
+                  : 0xFFFFFFFFu;
+#pragma unroll
+  for (int slot = 0; slot < 16; ++slot)
+    r[slot] = v[slot] != 0xFFFFFFFFu ? atomicAdd(&cnt[v[slot]], 1u) : 0u;
+  __syncthreads();
+  // the work-group's run of every bin it touched: kFillBatch returning atomics in flight
+  for (int64_t i0 = threadIdx.x; i0 < V; i0 += 256 * kFillBatch) {
+    uint32_t c[kFillBatch], o[kFillBatch];
+#pragma unroll
+    for (int j = 0; j < kFillBatch; ++j) {
+      const int64_t i = i0 + 256 * j;
+      c[j] = i < V ? cnt[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kFillBatch; ++j)
+      o[j] = c[j] ? atomicAdd(&cursor[i0 + 256 * j], c[j]) : 0u;
+#pragma unroll
+    for (int j = 0; j < kFillBatch; ++j)
+      if (c[j]) cnt[i0 + 256 * j] = o[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int slot = 0; slot < 16; ++slot)
+    if (v[slot] != 0xFFFFFFFFu) members[voff[v[slot]] + cnt[v[slot]] + r[slot]] = (int32_t)q;
 }
 
 // Small bins (the great majority: a few to a few dozen members) take a wave of their own:
@@ -632,6 +681,8 @@ __global__ __launch_bounds__(256) void members_kernel(
   }
 }
 
+constexpr int kGatherK = 4;   // members per thread per round in the gather kernels
+
 // PoseBin running means in vote order (PoseBin.py:19-43).  The recurrence
 //   v' = (v*n + new) / (n+1)
 // rounds at every step, so each bin's chain is inherently sequential; but the six
@@ -643,23 +694,39 @@ __global__ void means_gather_kernel(const uint32_t* __restrict__ scal,
                                     const double* __restrict__ pose, const int* __restrict__ idx1,
                                     const int* __restrict__ mimg, const int* __restrict__ isize,
                                     int64_t mstride, double* __restrict__ mq) {
+  // kGatherK members per thread per round: each level of the dependent gather (member ->
+  // query -> model keypoint -> model image -> size) is issued for all of them before the
+  // next, so a thread waits kGatherK times less on memory latency (the kernel runs on the
+  // few reserved CUs of a chip split, where latency, not bandwidth, bounds it)
   const int64_t M = scal[1];
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = members[e];
-    const double* p = pose + 4 * (int64_t)q;
-    const int im = mimg[idx1[q]];
-    mq[0 * mstride + e] = p[0];
-    mq[1 * mstride + e] = p[1];
-    mq[2 * mstride + e] = p[2];
-    mq[3 * mstride + e] = p[3];
-    mq[4 * mstride + e] = (double)isize[2 * im];
-    mq[5 * mstride + e] = (double)isize[2 * im + 1];
+  const int64_t step = (int64_t)gridDim.x * blockDim.x * kGatherK;
+  for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * kGatherK + threadIdx.x; e0 < M; e0 += step) {
+    int q[kGatherK], im[kGatherK];
+#pragma unroll
+    for (int i = 0; i < kGatherK; ++i) {
+      const int64_t e = e0 + (int64_t)i * blockDim.x;
+      q[i] = e < M ? members[e] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kGatherK; ++i) im[i] = idx1[q[i]];
+#pragma unroll
+    for (int i = 0; i < kGatherK; ++i) im[i] = mimg[im[i]];
+#pragma unroll
+    for (int i = 0; i < kGatherK; ++i) {
+      const int64_t e = e0 + (int64_t)i * blockDim.x;
+      if (e >= M) break;
+      const double* p = pose + 4 * (int64_t)q[i];
+      mq[0 * mstride + e] = p[0];
+      mq[1 * mstride + e] = p[1];
+      mq[2 * mstride + e] = p[2];
+      mq[3 * mstride + e] = p[3];
+      mq[4 * mstride + e] = (double)isize[2 * im[i]];
+      mq[5 * mstride + e] = (double)isize[2 * im[i] + 1];
+    }
   }
 }
 
-__global__ void recip_table_kernel(const uint32_t* __restrict__ scal, double* __restrict__ rtab) {
-  const int64_t M = scal[1];
+__global__ void recip_table_kernel(int64_t M, double* __restrict__ rtab) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M;
        i += (int64_t)gridDim.x * blockDim.x)
     rtab[i] = 1.0 / (double)(i + 1);
@@ -738,13 +805,26 @@ __global__ void affine_gather_kernel(const uint32_t* __restrict__ scal,
                                      int32_t* __restrict__ aisig, int32_t* __restrict__ bwh) {
   const int64_t M = scal[1], V = scal[0];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += stride) {
-    const int q = members[e];
-    const int m = idx1[q];
-    amx[e] = mx[m];
-    amy[e] = my[m];
-    aqx[e] = qx[q];
-    aqy[e] = qy[q];
+  // kGatherK members per thread per round, each gather level issued for all (as means_gather)
+  for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * kGatherK + threadIdx.x; e0 < M;
+       e0 += stride * kGatherK) {
+    int q[kGatherK], m[kGatherK];
+#pragma unroll
+    for (int i = 0; i < kGatherK; ++i) {
+      const int64_t e = e0 + (int64_t)i * blockDim.x;
+      q[i] = e < M ? members[e] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kGatherK; ++i) m[i] = idx1[q[i]];
+#pragma unroll
+    for (int i = 0; i < kGatherK; ++i) {
+      const int64_t e = e0 + (int64_t)i * blockDim.x;
+      if (e >= M) break;
+      amx[e] = mx[m[i]];
+      amy[e] = my[m[i]];
+      aqx[e] = qx[q[i]];
+      aqy[e] = qy[q[i]];
+    }
   }
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += stride) {
     aisig[v] = (int32_t)(vbin[v] % b.s);   // nbins1 is a multiple of b.s
@@ -809,6 +889,26 @@ __device__ void pinv3_sym(const double g[3][3], double p[3][3]) {
       p[i][j] = v[i][0] * inv[0] * v[j][0] + v[i][1] * inv[1] * v[j][1] + v[i][2] * inv[2] * v[j][2];
 }
 
+// sum over the kG lanes of a lane group (xor butterfly inside the group)
+template <int kG>
+__device__ __forceinline__ double group_sum(double x) {
+#pragma unroll
+  for (int m = kG / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+  return x;
+}
+template <int kG>
+__device__ __forceinline__ int group_sum_i(int x) {
+#pragma unroll
+  for (int m = kG / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+  return x;
+}
+
+// One lane group of kAffG lanes per bin, 64 / kAffG bins per wave: a bin's work is a serial
+// chain (member sums -> 3x3 Jacobi pinv -> residual test, repeated), so several bins in one
+// wave run their chains in the same instructions -- the few reserved CUs of a chip split
+// (sod_set_cu_reserve) hold 64 / kAffG times as many chains in flight.
+constexpr int kAffG = 64;   // 16 measured slower at C3: the large bins' member loops lengthen
+
 __global__ __launch_bounds__(256) void affine_kernel(
     int64_t nb_host, const uint32_t* __restrict__ nb_dev, const int64_t* __restrict__ off,
     const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
@@ -817,33 +917,42 @@ __global__ __launch_bounds__(256) void affine_kernel(
     const double* __restrict__ params_in,
     uint8_t* __restrict__ surv, int32_t* __restrict__ votes, double* __restrict__ params,
     uint8_t* __restrict__ alive) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  constexpr int G = kAffG;
+  const int lane = threadIdx.x & (G - 1);                 // lane within the bin's group
+  const int64_t ngroups = (int64_t)gridDim.x * (blockDim.x / G);
   const int64_t NB = nb_dev ? (int64_t)nb_dev[0] : nb_host;
-  for (int64_t v = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < NB; v += nwaves) {
-    const int64_t a = off[v], e = off[v + 1];
-    for (int64_t j = a + lane; j < e; j += 64) alive[j] = 1;
+  const int64_t g0 = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
+  // every group of the wave runs the loop the same number of times (shuffles need the
+  // whole wave): groups past the last bin idle with an empty member range
+  const int64_t wave_first = g0 - (threadIdx.x & 63) / G;
+  for (int64_t vb = wave_first; vb < NB; vb += ngroups) {
+    const int64_t v = vb + (threadIdx.x & 63) / G;
+    const bool live = v < NB;
+    const int64_t a = live ? off[v] : 0, e = live ? off[v + 1] : 0;
+    for (int64_t j = a + lane; j < e; j += G) alive[j] = 1;
     // AffineParameters.py:120-121: tolerance scales with the scale-bin INDEX pose[3]
-    const int64_t bw = bwh ? bwh[2 * v] : qw, bh = bwh ? bwh[2 * v + 1] : qh;
-    const double xref = (double)(bw * isig[v]) / xf;
-    const double yref = (double)(bh * isig[v]) / yf;
+    const int64_t bw = !live ? 0 : bwh ? bwh[2 * v] : qw;
+    const int64_t bh = !live ? 0 : bwh ? bwh[2 * v + 1] : qh;
+    const int32_t sig = live ? isig[v] : 0;
+    const double xref = (double)(bw * sig) / xf;
+    const double yref = (double)(bh * sig) / yf;
     int64_t n = e - a;
     double prm[6] = {0, 0, 0, 0, 0, 0};
     bool ok = false;
     const int rounds = max_iter < 1 ? 1 : max_iter;   // max_iter 0: solve once, remove nothing
     for (int it = 0; it < rounds; ++it) {
       double s[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (int64_t j = a + lane; j < e; j += 64) {
+      for (int64_t j = a + lane; j < e; j += G) {
         if (!alive[j]) continue;
         const double x = mx[j], y = my[j], u = qx[j], w = qy[j];
         s[0] += x * x; s[1] += x * y; s[2] += x; s[3] += y * y; s[4] += y; s[5] += 1.0;
         s[6] += x * u; s[7] += y * u; s[8] += u; s[9] += x * w; s[10] += y * w; s[11] += w;
       }
 #pragma unroll
-      for (int k = 0; k < 12; ++k) s[k] = wave_sum(s[k]);
+      for (int k = 0; k < 12; ++k) s[k] = group_sum<G>(s[k]);
       if (params_in) {  // remove_outliers with the caller's posebin.affine_parameters
 #pragma unroll
-        for (int k = 0; k < 6; ++k) prm[k] = params_in[6 * v + k];
+        for (int k = 0; k < 6; ++k) prm[k] = live ? params_in[6 * v + k] : 0.0;
       } else if (n > 0) {  // AffineParameters.py:105: no-op for an empty bin
         const double g[3][3] = {{s[0], s[1], s[2]}, {s[1], s[3], s[4]}, {s[2], s[4], s[5]}};
         double p[3][3];
@@ -862,7 +971,7 @@ __global__ __launch_bounds__(256) void affine_kernel(
       }
       // remove_outliers, AffineParameters.py:134-159
       int dropped = 0;
-      for (int64_t j = a + lane; j < e; j += 64) {
+      for (int64_t j = a + lane; j < e; j += G) {
         if (!alive[j]) continue;
         const double x = mx[j], y = my[j];
         const double up = (prm[0] * x + prm[1] * y) + prm[4];
@@ -872,8 +981,7 @@ __global__ __launch_bounds__(256) void affine_kernel(
           ++dropped;
         }
       }
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) dropped += __shfl_xor(dropped, m);
+      dropped = group_sum_i<G>(dropped);
       n -= dropped;
       if (n < thr) {  // main.py:152
         ok = false;
@@ -882,7 +990,7 @@ __global__ __launch_bounds__(256) void affine_kernel(
       ok = true;
       if (dropped == 0) break;  // main.py:151 fixed point
     }
-    if (lane == 0) {
+    if (lane == 0 && live) {
       surv[v] = ok ? 1 : 0;
       votes[v] = (int32_t)n;
       for (int k = 0; k < 6; ++k) params[6 * v + k] = prm[k];
@@ -1025,10 +1133,10 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   hipLaunchKernelGGL(member_offsets_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->vbin.p,
                      ctx->counts.p, ctx->scal.p, ctx->voff.p, ctx->cursor.p);
   SOD_HIP(ctx, hipGetLastError());
-  const unsigned fill_wg = (unsigned)std::min<int64_t>(cdiv(nq, 256), (int64_t)ctx->tail_cus() * 16);
-  hipLaunchKernelGGL(member_fill_kernel, dim3(std::max(1u, fill_wg)), dim3(256), 0, ctx->stream,
-                     nq, ctx->basekey.p, ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1,
-                     ctx->vidx.p, ctx->voff.p, ctx->cursor.p, ctx->members.p);
+  hipLaunchKernelGGL(member_fill_lds_kernel, dim3((unsigned)std::max<int64_t>(1, cdiv(nq, 256))),
+                     dim3(256), 0, ctx->stream, nq, ctx->scal.p, ctx->basekey.p, ctx->vmask.p,
+                     ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->vidx.p, ctx->voff.p,
+                     ctx->cursor.p, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(member_order_small_kernel, dim3(std::max(1, ctx->tail_cus() * 8)), dim3(256),
                      0, ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, ctx->vidx.p,
@@ -1045,6 +1153,9 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   // PoseBin means depend only on the member lists: they run on the side stream, beside the
   // affine verification, and the main stream joins them at the next entry point (set_dev)
   SOD_TRY(sod_reserve(ctx, ctx->mq, (size_t)ctx->mmax * 6));
+  // 1/(n+1) for every n a member list of this capacity can reach: built once per capacity
+  // (a bin's chain reads entry n - 1 for its n-th member)
+  const bool new_rtab = ctx->rtab.n < (size_t)ctx->mmax;
   SOD_TRY(sod_reserve(ctx, ctx->rtab, (size_t)ctx->mmax));
   SOD_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
   SOD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
@@ -1052,10 +1163,14 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
                      ctx->side, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p + sod_win0(ctx),
                      ctx->mimg.p, ctx->isize.p, ctx->mmax, ctx->mq.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(recip_table_kernel, dim3(std::max(1, ctx->tail_cus())), dim3(256), 0,
-                     ctx->side, ctx->scal.p, ctx->rtab.p);
-  SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->tail_cus() * 8)), dim3(64), 0, ctx->side,
+  if (new_rtab) {
+    hipLaunchKernelGGL(recip_table_kernel, dim3((unsigned)std::min<int64_t>(cdiv(ctx->rtab.n, 256), 4096)),
+                       dim3(256), 0, ctx->side, (int64_t)ctx->rtab.n, ctx->rtab.p);
+    SOD_HIP(ctx, hipGetLastError());
+  }
+  // one wave per bin, each a serial f64 chain: as many chains in flight as LDS allows
+  // (7 KiB per wave: 16 per CU)
+  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->tail_cus() * 16)), dim3(64), 0, ctx->side,
                      ctx->scal.p, ctx->voff.p, ctx->mq.p, ctx->mmax, ctx->rtab.p, ctx->means.p);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
