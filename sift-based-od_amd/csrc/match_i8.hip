@@ -290,6 +290,31 @@ __device__ __forceinline__ void top2_xor16(int& y1, int& y2) {
 #define PARITY_T i32x4            // the parity words
 #endif
 
+// max of N values as a v_max3 tree (ceil((N-1)/2) VALU), fully unrolled
+template <int N>
+struct MaxTree {
+  static __device__ __forceinline__ int f(const int* v) {
+    if constexpr (N == 1) {
+      return v[0];
+    } else if constexpr (N == 2) {
+      return max(v[0], v[1]);
+    } else {
+      constexpr int M = N / 3 + (N % 3 != 0);
+      int w[M];
+#pragma unroll
+      for (int i = 0; i < N / 3; ++i) w[i] = max(max(v[3 * i], v[3 * i + 1]), v[3 * i + 2]);
+      if constexpr (N % 3 == 2) w[M - 1] = max(v[N - 2], v[N - 1]);
+      if constexpr (N % 3 == 1) w[M - 1] = v[N - 1];
+      return MaxTree<M>::f(w);
+    }
+  }
+};
+
+#ifdef SOD_I8_TIME
+// diagnostic build only: per wave slot, s_memtime cycles inside the slow path and entries;
+// [.][2] whole work unit
+__device__ unsigned long long g_tm[32768][4];
+#endif
 #ifdef SOD_I8_COUNT
 // diagnostic build only: [0] slow-path entries, [1] hit tiles, [2] wave-subtiles,
 // [3] entries and [4] hit tiles within the first 64 subtiles of a chunk
@@ -308,6 +333,31 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
                                             int (&id)[QT], bool early = false, int mode = 0,
                                             bool vmem = false) {
+#if SOD_I8_EXP & 8
+  // timing bound only: one flat max over the lane's 4*QT values (v_max3 tree) + ONE compare
+  // per subtile, the cost of a prefilter whose thresholds live in C; cheap slow body
+  {
+    int v[4 * QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[4 * t + r] = acc[t][r];
+    const int vmax = MaxTree<4 * QT>::f(v);
+    const uint64_t h = __builtin_amdgcn_ballot_w64(vmax >= t2[0]);
+#if SOD_I8_SGB
+    constexpr int nv = 2 * QT + 1;
+#pragma unroll
+    for (int i = 0; i < 2 * QT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      if (2 * i < nv) __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);
+      if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+    }
+#endif
+    if (__builtin_expect(h != 0, 0)) t2[0] = max(t2[0], vmax);
+    return;
+  }
+#endif
   uint64_t hit[QT];
   uint64_t any = 0;
 #pragma unroll
@@ -329,6 +379,9 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
 #endif
 #if SOD_I8_COLD
   if (__builtin_expect(any != 0, 0)) {   // slow path laid out away from the hot loop
+#ifdef SOD_I8_TIME
+    const unsigned long long tsp0 = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef SOD_I8_COUNT
     if ((threadIdx.x & 63) == 0) {
       unsigned nh = 0;
@@ -385,6 +438,15 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
 #endif
       }
     }
+#ifdef SOD_I8_TIME
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const unsigned long long tsp1 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) {
+      const int wslot = (blockIdx.x * 8 + (threadIdx.x >> 6)) & 32767;
+      atomicAdd(&g_tm[wslot][0], tsp1 - tsp0);
+      atomicAdd(&g_tm[wslot][1], 1ull);
+    }
+#endif
   }
 }
 
@@ -398,6 +460,9 @@ __device__ __forceinline__ void match_unit(
     int* __restrict__ pidx, float* __restrict__ pd2, int* __restrict__ gthr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qt0 = (qb * NW16 + wave) * QT;
+#ifdef SOD_I8_TIME
+  const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
+#endif
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / SPS;
@@ -601,6 +666,9 @@ __device__ __forceinline__ void match_unit(
 #endif
 #ifdef SOD_I8_COUNT
   if (lane == 0) atomicAdd(&g_counts[2], (unsigned long long)(nst * SPS));
+#endif
+#ifdef SOD_I8_TIME
+  if (lane == 0) atomicAdd(&g_tm[(blockIdx.x * 8 + wave) & 32767][2], __builtin_amdgcn_s_memtime() - tu0);
 #endif
 
 #pragma unroll
@@ -933,6 +1001,17 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   return SOD_OK;
 }
 
+#ifdef SOD_I8_TIME
+extern "C" int sod_debug_times(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tm), sizeof(g_tm)) != hipSuccess) return 1;
+  if (reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_tm)) != hipSuccess) return 1;
+    if (hipMemset(p, 0, sizeof(g_tm)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
 #ifdef SOD_I8_COUNT
 extern "C" int sod_debug_counts(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_counts), 64) != hipSuccess) return 1;

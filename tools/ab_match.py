@@ -73,6 +73,18 @@ if hasattr(ctx._L, "sod_debug_stamps"):   # diagnostic build: in-kernel clock
     order = np.argsort(-dur)[:8]
     print("  slowest WGs (block, us, xcc, cu-slot):", [(int(b), int(dur[b]), int(xcc[b]),
                                                      int(place[b])) for b in order], flush=True)
+if hasattr(ctx._L, "sod_debug_times"):   # diagnostic build: slow-path cycles per wave
+    import ctypes as C
+    tm = np.zeros((32768, 4), np.uint64)
+    ctx._L.sod_debug_times(tm.ctypes.data_as(C.c_void_p), 1)
+    ctx.match()
+    ctx.synchronize()
+    ctx._L.sod_debug_times(tm.ctypes.data_as(C.c_void_p), 0)
+    cyc, n, tot = tm[:, 0].astype(np.float64), tm[:, 1].astype(np.float64), tm[:, 2].astype(np.float64)
+    print("slow path: %.0f cycles per entry, %.2f entries per wave, %.1f %% of the waves' cycles "
+          "(work unit median %.0f cycles)" % (cyc.sum() / max(n.sum(), 1), n.sum() / max((tot > 0).sum(), 1),
+                                             100.0 * cyc.sum() / max(tot.sum(), 1), np.median(tot[tot > 0])),
+          flush=True)
 if hasattr(ctx._L, "sod_debug_counts"):   # diagnostic build: slow-path statistics
     import ctypes as C
     cnt = np.zeros(8, np.uint64)
@@ -84,6 +96,11 @@ if hasattr(ctx._L, "sod_debug_counts"):   # diagnostic build: slow-path statisti
           "first 64 subtiles of a chunk: %.1f %% of entries, %.1f %% of hit tiles" % (
               cnt[0] / cnt[2], cnt[1] / cnt[2], cnt[2], 100.0 * cnt[3] / max(cnt[0], 1),
               100.0 * cnt[4] / max(cnt[1], 1)), flush=True)
+    if cnt[7]:   # s_memtime cycles inside the slow path (timer + atomics included)
+        print("slow path: %.0f cycles per entry (s_memtime)" % (cnt[7] / max(cnt[0], 1)), flush=True)
+    if cnt[5]:   # flipped kernel: (query, row-slot) groups with a passing lane, passing lanes
+        print("passing slots / wave-subtile %.4f, passing lanes / slot %.2f" % (
+            cnt[5] / cnt[2], cnt[6] / cnt[5]), flush=True)
 ctx.ratio(0.75)
 idx1, d1, d2, good = ctx.match_result()
 print("checksum", int(idx1.astype(np.int64).sum()), float(d1.astype(np.float64).sum()), flush=True)
