@@ -255,7 +255,14 @@ __device__ __forceinline__ constexpr bool share_apply(int u) { return u == 20 ||
 #ifndef SOD_I8_PUB_EVERY
 #define SOD_I8_PUB_EVERY 1   // 4 measured: 5 % less L2-miss traffic, time unchanged
 #endif
+#ifndef SOD_I8_XEVERY
+// stages between threshold exchanges (load + publish) after a chunk's first 4: every stage's
+// load of the wave's 128 global values (served past L2) was ~70 MB of a launch's L2-miss
+// traffic; every 4th: 541 -> 469 MB and -0.8 % time at C3, C2 equal (16th: 416 MB, C2 +4 %)
+#define SOD_I8_XEVERY 4
+#endif
 constexpr int64_t kPublishDense = 4, kPublishEvery = SOD_I8_PUB_EVERY;
+constexpr int64_t kXDense = 4, kXEvery = SOD_I8_XEVERY;
 __device__ __forceinline__ constexpr bool share_load(int u) { return u == 8; }
 __device__ __forceinline__ constexpr bool share_apply(int u) { return u == 24; }
 #endif
@@ -632,10 +639,11 @@ __device__ __forceinline__ void match_unit(
       // values of its queries into LDS; at kShareApply (they landed: vmcnt(0), the stage's
       // refill pieces went out before the load) it publishes its own t2 where above them and
       // raises t2 to them
-      if (share_load(u) && lane < QT * 4)   // the wave's QT x 16 values: QT*4 lanes x 16 B
+      const bool xstage = kXEvery == 1 || s < kXDense || s % kXEvery == 0;   // wave-uniform
+      if (share_load(u) && xstage && lane < QT * 4)   // the wave's QT x 16 values: QT*4 lanes x 16 B
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_void*)gl, 16, (uint32_t)lane * 16u, 0,
                                                  0, 16 /* sc1: past this XCD's L2 */);
-      if (share_apply(u) && (SOD_I8_SHARE2 == 0 || u != 12 || s > 0)) {
+      if (share_apply(u) && xstage && (SOD_I8_SHARE2 == 0 || u != 12 || s > 0)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15);
         // publishing is a device-scope atomic per query (a memory-side transaction each):
