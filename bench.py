@@ -296,9 +296,9 @@ def cpu_sift_baseline(h=800, w=1000):
 
 
 def pmc_traffic(kernel, config):
-    """HBM bytes per matcher launch from the committed PMC summary of the same kernel and
-    workload (profiles/*_pmc_<kernel>_<config>.json, from tools/gpu_pmc.sh +
-    tools/pmc_summary.py)."""
+    """The newest committed PMC summary of the same kernel and workload
+    (profiles/*_pmc_<kernel>_<config>.json, from tools/gpu_pmc.sh + tools/pmc_summary.py):
+    HBM bytes per launch, MFMA-busy fraction, clock."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s_%s.json" % (kernel, config)))):
@@ -306,7 +306,7 @@ def pmc_traffic(kernel, config):
     if not best:
         return None, None
     d = json.load(open(best))
-    return d.get("hbm_bytes"), os.path.relpath(best, REPO)
+    return d, os.path.relpath(best, REPO)
 
 
 def main():
@@ -456,7 +456,8 @@ def main():
     aff = ctx.affine_result() if run_affine else None
     idx1, d1, d2, good = ctx.match_result()
 
-    traffic, traffic_src = pmc_traffic(kernel, a.config)
+    pmc, traffic_src = pmc_traffic(kernel, a.config)
+    traffic = pmc.get("hbm_bytes") if pmc else None
     pairs = float(world) * nq * n_shard
     value = pairs / (ms_per_step / 1000.0)
     achieved = OPS_PER_PAIR * nq * n_shard / (match_ms / 1000.0) / 1e12
@@ -499,6 +500,13 @@ def main():
                      "unit": peak_unit, "frac": achieved / peak, "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, 2*FETCH_SIZE+WRITE_SIZE)",
                      "traffic_source": traffic_src,
+                     # rocprof counters against the gfx950 peaks (north_star): bytes past
+                     # L2 per launch over this run's launch time vs ~8 TB/s HBM; MFMA-busy
+                     # SIMD cycles / all SIMD cycles and the clock of the PMC passes
+                     "traffic_gb_per_s": traffic / (match_ms * 1e6) if traffic else None,
+                     "traffic_frac_of_hbm_peak": traffic / (match_ms * 1e6) / 8000.0 if traffic else None,
+                     "mfma_busy_frac_pmc": pmc.get("mfma_busy_frac") if pmc else None,
+                     "clock_ghz_pmc": pmc.get("clock_ghz") if pmc else None,
                      "algorithmic_bytes": alg_bytes,
                      "kernel": kernel,
                      "algorithmic": "256 op/pair x %d x %d pairs per launch" % (nq, n_shard)},
