@@ -1,5 +1,6 @@
 """Drop-in for ``cv2.BFMatcher().knnMatch(des_query, des, k=2)`` (call site
-``main.py:70-71``) running on the MI355X matcher kernel (match.hip), plus the ratio test
+``main.py:70-71``) running on the MI355X matcher kernel (int8 MFMA, match_i8.hip; bf16
+match.hip selectable), plus the ratio test
 of ``main.py:81-86``.
 
 ``knnMatch`` returns what OpenCV returns: per query a list of ``DMatch`` sorted by
@@ -69,8 +70,10 @@ class BFMatcher:
     def knnMatch(self, queryDescriptors, trainDescriptors, k=2):
         if k not in (1, 2):
             raise NotImplementedError("k must be 1 or 2 (main.py uses k=2)")
-        idx1, d1, d2 = knn2(queryDescriptors, trainDescriptors, self._ctx)
         ntrain = np.asarray(trainDescriptors).shape[0]
+        if ntrain == 0:   # OpenCV: no neighbours for any query
+            return [[] for _ in range(np.asarray(queryDescriptors).shape[0])]
+        idx1, d1, d2 = knn2(queryDescriptors, trainDescriptors, self._ctx)
         out = []
         if k == 1 or ntrain == 1:
             for q in range(len(idx1)):

@@ -32,6 +32,13 @@ def test_bfmatcher_single_train_row():
     assert all(len(m) == 1 and m[0].trainIdx == 0 for m in out)
 
 
+def test_bfmatcher_empty_sets():
+    """OpenCV's knnMatch: no queries -> no lists; no train rows -> an empty list per query."""
+    q = np.random.default_rng(1).integers(0, 256, (4, 128)).astype(np.uint8)
+    assert sod.BFMatcher().knnMatch(q[:0], q, k=2) == []
+    assert sod.BFMatcher().knnMatch(q, q[:0], k=2) == [[], [], [], []]
+
+
 def test_scalar_pose_and_bin_index():
     g = golden("pose_sweep")
     shape = tuple(int(v) for v in g["shape"])
