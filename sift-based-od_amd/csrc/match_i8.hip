@@ -68,7 +68,10 @@ constexpr int kStageNorm = 2 * SPS * kSubRows * 4;   // c and parity words
 // the parity words of a stage are read only on the slow path of its LAST subtile, which
 // runs (software pipeline) after the next stage's barrier -- when that stage's refill
 // already targets the descriptor slot
-constexpr int kNormRing = 4;
+#ifndef SOD_I8_RING
+#define SOD_I8_RING 2      // LDS stage slots (prefetch distance = RING - 1 stages)
+#endif
+constexpr int kNormRing = SOD_I8_RING + 1 > 4 ? SOD_I8_RING + 1 : 4;
 constexpr int kPiecesPerWave = kStageBytes / 1024 / NW16;   // 1 KiB LDS-DMA pieces
 constexpr int kPadNormI = 1 << 30;                        // ||d'||^2 of padding rows (w = -2^30)
 static_assert(kStageBytes / 1024 % NW16 == 0, "pieces split evenly");
@@ -218,9 +221,6 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
   }
 }
 
-#ifndef SOD_I8_RING
-#define SOD_I8_RING 2      // LDS stage slots (prefetch distance = RING - 1 stages)
-#endif
 #ifndef SOD_I8_PIPE
 #define SOD_I8_PIPE 1      // prefilter subtile u while the MFMAs of subtile u+1 run
 #endif

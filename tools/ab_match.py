@@ -24,6 +24,8 @@ q[: nq // 5] = np.clip(db[rng.integers(0, len(db), nq // 5)].astype(int) +
                        rng.integers(-3, 4, (nq // 5, 128)), 0, 255).astype(np.uint8)
 ctx = _lib.Context(0)
 ctx.set_impl(impl)
+if len(sys.argv) > 4 and int(sys.argv[4]):   # CU split (sod_set_cu_reserve) for the matcher
+    ctx.set_cu_reserve(int(sys.argv[4]))
 ctx.upload_db(db)
 ctx.upload_queries(q)
 ts = []
