@@ -29,6 +29,9 @@
 
 namespace {
 
+#ifndef SOD_SIFT_LANE_ORDER
+#define SOD_SIFT_LANE_ORDER 1   // histogram adds by a whole wave, same-bin lanes in lane order
+#endif
 #ifndef SOD_SIFT_EXP
 #define SOD_SIFT_EXP 0   // timing experiments only (wrong results): 1 no descriptor adds,
 #endif                   // 2 no orientation adds, 4 no small-octave extrema
@@ -738,6 +741,16 @@ __global__ __launch_bounds__(kOT) void orient_kernel(const float* __restrict__ g
         sval[nv + tid] = 0.f;
       }
       __syncthreads();
+#if SOD_SIFT_LANE_ORDER
+      // wave 0 adds 64 samples per LDS atomic instruction, sample k on lane k: lanes of one
+      // ds_add_f32 that hit the same bin are applied in lane order on gfx950 (probed:
+      // tools/lds_atomic_order.hip, 2000 order-sensitive trials), and the instructions of a
+      // wave in program order -- so every bin still sums in OpenCV's sample order
+      if (tid < 64 && !(SOD_SIFT_EXP & 2)) {
+        for (int t0 = 0; t0 < nv; t0 += 64)
+          if (t0 + tid < nv) atomicAdd(&temphist[sbin[t0 + tid]], sval[t0 + tid]);
+      }
+#else
       if (tid == 0 && !(SOD_SIFT_EXP & 2)) {
         for (int t0 = 0; t0 < nv; t0 += 16) {
           int4 b4[4];
@@ -756,6 +769,7 @@ __global__ __launch_bounds__(kOT) void orient_kernel(const float* __restrict__ g
           }
         }
       }
+#endif
       __syncthreads();
     }
     if (tid == 0) {
@@ -879,10 +893,12 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
   __shared__ int wcnt[kDT / 64];
   const int tid = threadIdx.x;
   const int nf = (int)*nfinal;
+#if !SOD_SIFT_LANE_ORDER
   // the eight bins of a sample relative to its first (lanes 0-7)
   const int off = tid == 0 ? 0 : tid == 1 ? 1 : tid == 2 ? kN + 2 : tid == 3 ? kN + 3
                 : tid == 4 ? (kD + 2) * (kN + 2) : tid == 5 ? (kD + 2) * (kN + 2) + 1
                 : tid == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
+#endif
   for (int id = blockIdx.x; id < nf; id += gridDim.x) {
     const Kp k = sorted[id];
     int octave = k.octave & 255;
@@ -966,6 +982,18 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
         for (int e = 0; e < 8; ++e) svalT[e][nv + tid] = 0.f;
       }
       __syncthreads();
+#if SOD_SIFT_LANE_ORDER
+      // wave 0 adds 8 samples per LDS atomic instruction: lane 8 s + e carries contribution
+      // e of sample s (same-bin lanes apply in lane order = sample order, see orient_kernel)
+      if (tid < 64 && !(SOD_SIFT_EXP & 1)) {
+        const int s8 = tid >> 3, e = tid & 7;
+        const int offe = e == 0 ? 0 : e == 1 ? 1 : e == 2 ? kN + 2 : e == 3 ? kN + 3
+                       : e == 4 ? (kD + 2) * (kN + 2) : e == 5 ? (kD + 2) * (kN + 2) + 1
+                       : e == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
+        for (int t0 = 0; t0 < nv; t0 += 8)
+          if (t0 + s8 < nv) atomicAdd(&hist[sidx[t0 + s8] + offe], svalT[e][t0 + s8]);
+      }
+#else
       if (tid < 8 && !(SOD_SIFT_EXP & 1)) {
         // 16 samples' indices and this lane's values read as 128-bit vectors, then the
         // 16 adds (in order, fire-and-forget)
@@ -986,6 +1014,7 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
           }
         }
       }
+#endif
       __syncthreads();
     }
     // finalize: fold the circular orientation bins, then OpenCV's sequential norms

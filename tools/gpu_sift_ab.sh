@@ -1,19 +1,10 @@
-# SIFT kernel timings of libsod.so and each tools/variants/*.so (rocprofv3 kernel stats)
+# SIFT parity (GPU suite, SIFT tests) with the tree's library, then single-image and batch
+# timing of the variants in tools/variants
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"
-export TMPDIR=/tmp
-mkdir -p gpurun_out/sift_ab
-: > gpurun_out/sift_ab/summary.txt
-for v in sift-based-od_amd/libsod.so tools/variants/*.so; do
-  [ -e "$v" ] || continue
-  n=$(basename "$v" .so)
-  SOD_LIB_PATH="$PWD/$v" timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/sift_ab/$n -o k --output-format csv -- python3 tools/sift_bench.py ${SIFT_H:-800} ${SIFT_W:-1000} 5 > gpurun_out/sift_ab/$n.log 2>&1 || exit $?
-  echo "== $n: $(grep '^sift' gpurun_out/sift_ab/$n.log)" >> gpurun_out/sift_ab/summary.txt
-  python3 - "$n" >> gpurun_out/sift_ab/summary.txt <<'PY'
-import csv, glob, sys
-f = glob.glob("gpurun_out/sift_ab/%s/**/k_kernel_stats.csv" % sys.argv[1], recursive=True)[0]
-for r in list(csv.DictReader(open(f)))[:12]:
-    print("  %-34s calls %4s avg %8.2f us total/img %8.1f us" % (r["Name"].split("::")[-1][:34], r["Calls"],
-          float(r["AverageNs"]) / 1e3, float(r["TotalDurationNs"]) / 6e3))
-PY
-done
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/siftab; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_sift.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for i in 1 2; do for v in tools/variants/*.so; do
+  echo "== $v" ; SOD_LIB_PATH=$PWD/$v timeout -k 10 120 python3 tools/sift_bench.py 800 1000 30 || exit 1
+  SOD_LIB_PATH=$PWD/$v timeout -k 10 120 python3 tools/sift_batch_bench.py || exit 1
+done; done
