@@ -77,7 +77,7 @@ def parse():
     p.add_argument("--cu-reserve", type=int, default=-1,
                    help="CUs per XCD kept off the matcher for the other stages and the RCCL "
                         "exchanges (sod_set_cu_reserve; implies --overlap 1).  Default: 1 "
-                        "when the matcher dominates a step (>= 1e10 pairs per GPU), else 0 "
+                        "from 1e9 pairs per GPU up (C2, C3, C5), else 0 "
                         "(and 0 with --contexts > 1 or --overlap 0)")
     p.add_argument("--impl", default="i8", choices=sorted(IMPLS),
                    help="matcher kernel: int8 MFMA 16x16x64 (default, fastest), int8 32x32x32 "
@@ -353,10 +353,11 @@ def main():
     ctx.upload_db(shard, row_offset=rank * n_shard)
     ctx.upload_queries(qs.des, qs.kp)
     from sift_based_od_amd.sharded import RcclComm, TorchHostComm, run_sharded
-    # auto: split the chip when the matcher dominates a step (C3 / C5: ~4 ms against a
-    # ~1.3 ms tail on the 8 reserved CUs); C2's 0.2 ms matcher would wait on that tail
+    # auto: split the chip for the int8 matcher from 1e9 pairs per GPU up (C3 / C5: ~3.8 ms
+    # against a ~0.8 ms tail on the 8 reserved CUs; C2: 0.209 vs 0.218 ms per step with two
+    # contexts, measured; 2 reserved CUs per XCD 0.258 ms)
     reserve = a.cu_reserve if a.cu_reserve >= 0 else (
-        0 if a.contexts > 1 or a.overlap == 0 or nq * shard.shape[0] < 10 ** 10
+        0 if a.contexts > 1 or a.overlap == 0 or nq * shard.shape[0] < 10 ** 9
         or a.impl != "i8" else 1)   # grid sizing measured for the default int8 kernel only
     overlap = a.overlap if a.overlap >= 0 else (1 if world > 1 or reserve else 0)
     ctx.set_overlap(bool(overlap))
