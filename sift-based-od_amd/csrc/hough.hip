@@ -111,8 +111,15 @@ __global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
                             const int* __restrict__ qimg, const int* __restrict__ qshape, Bins b,
                             const int* __restrict__ lut, int64_t own_lo, int64_t own_hi,
                             double* __restrict__ pose, uint32_t* __restrict__ basekey,
-                            uint32_t* __restrict__ vmask) {
+                            uint32_t* __restrict__ vmask, int64_t nbins,
+                            uint32_t* __restrict__ counts, uint32_t* __restrict__ first) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the histogram the next kernel fills starts empty: count 0, first touch "none" (folded
+  // in here instead of two memset launches on the tail's critical path)
+  for (int64_t b2 = q; b2 < nbins; b2 += (int64_t)gridDim.x * blockDim.x) {
+    counts[b2] = 0u;
+    first[b2] = 0xFFFFFFFFu;
+  }
   if (q >= nq) return;
   if (qimg) {   // batch of query images: this query's image shape (main.py:102)
     H = qshape[2 * qimg[q]];
@@ -1053,16 +1060,16 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
   SOD_TRY(sod_reserve(ctx, ctx->vmask, (size_t)nq));
   SOD_TRY(sod_reserve(ctx, ctx->counts, (size_t)ctx->nbins));
   SOD_TRY(sod_reserve(ctx, ctx->first, (size_t)ctx->nbins));
-  SOD_HIP(ctx, hipMemsetAsync(ctx->counts.p, 0, ctx->nbins * 4, ctx->stream));
-  SOD_HIP(ctx, hipMemsetAsync(ctx->first.p, 0xFF, ctx->nbins * 4, ctx->stream));
   const int bs = 256;
-  hipLaunchKernelGGL(pose_kernel, dim3((unsigned)cdiv(nq, bs)), dim3(bs), 0, ctx->stream, nq,
+  // one thread per query, and enough of them to clear the histogram in a few passes
+  const int64_t pgrid = std::max<int64_t>(cdiv(nq, bs), std::min<int64_t>(cdiv(ctx->nbins, 4 * bs), 4096));
+  hipLaunchKernelGGL(pose_kernel, dim3((unsigned)pgrid), dim3(bs), 0, ctx->stream, nq,
                      ctx->good.p + q0, ctx->idx1.p + q0, ctx->qx.p + q0, ctx->qy.p + q0,
                      ctx->qang.p + q0, ctx->qoct.p + q0,
                      ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p,
                      ctx->qh, ctx->qw, qimg_p(ctx), ctx->n_qimg ? ctx->qshape.p : nullptr,
                      ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
-                     ctx->basekey.p, ctx->vmask.p);
+                     ctx->basekey.p, ctx->vmask.p, ctx->nbins, ctx->counts.p, ctx->first.p);
   SOD_HIP(ctx, hipGetLastError());
   const int64_t nchunk = cdiv(nq, kChunk);
   dim3 grid((unsigned)cdiv(ctx->nbins, kSlab), (unsigned)nchunk);
@@ -1145,11 +1152,13 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   hipLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->tail_cus() * 2)), dim3(kOrderT), 0,
                      ctx->stream, ctx->scal.p, ctx->voff.p, nq, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  const int wg = std::max(1, ctx->tail_cus() * 4);
-  hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
-                     ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
-                     ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->members.p);
-  SOD_HIP(ctx, hipGetLastError());
+  if (nq > kBitQ) {   // beyond the LDS bitmap of member_order_kernel only (a no-op otherwise)
+    const int wg = std::max(1, ctx->tail_cus() * 4);
+    hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
+                       ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
+                       ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->members.p);
+    SOD_HIP(ctx, hipGetLastError());
+  }
   // PoseBin means depend only on the member lists: they run on the side stream, beside the
   // affine verification, and the main stream joins them at the next entry point (set_dev)
   SOD_TRY(sod_reserve(ctx, ctx->mq, (size_t)ctx->mmax * 6));
