@@ -623,6 +623,7 @@ int sod_valid_images_get(sod_ctx* ctx, int32_t* image) {
 int sod_match_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
+  ctx->ratio_fused = -1.0;   // set again by a final merge that applies the pipeline's ratio
   SOD_TRY(ctx->impl != 0 ? launch_match_i8(ctx) : launch_match(ctx));
   ctx->matched = true;
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
@@ -749,13 +750,14 @@ int sod_match_allgather_enqueue(sod_ctx* ctx) {
     return sod_fail(ctx, SOD_ECOMM, std::string("ncclAllGather: ") +
                                         ncclGetErrorString(r != ncclSuccess ? r : r2));
   // global merge in rank order (lexicographic on (d^2, trainIdx): order-independent anyway)
-  return launch_merge(ctx, ctx->gd1.p, ctx->gidx.p, ctx->gd2.p, ctx->nranks, (int64_t)nq_pad);
+  return launch_merge(ctx, ctx->gd1.p, ctx->gidx.p, ctx->gd2.p, ctx->nranks, (int64_t)nq_pad,
+                      nullptr, true);   // the global merge: final
 }
 
 int sod_ratio_enqueue(sod_ctx* ctx, double ratio) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
-  SOD_TRY(launch_ratio(ctx, ratio));
+  if (ctx->ratio_fused != ratio) SOD_TRY(launch_ratio(ctx, ratio));   // else the merge did it
   ctx->ratio_done = true;
   return SOD_OK;
 }
@@ -786,6 +788,7 @@ int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t
   SOD_HIP(ctx, hipMemsetAsync(ctx->d1.p, 0, (size_t)nq * 4, ctx->stream));
   SOD_HIP(ctx, hipMemsetAsync(ctx->d2.p, 0, (size_t)nq * 4, ctx->stream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->ratio_fused = -1.0;
   ctx->matched = ctx->ratio_done = true;
   ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
@@ -960,8 +963,11 @@ int sod_affine_get(sod_ctx* ctx, uint8_t* survived, int32_t* votes, double* para
 int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* a) {
   SOD_TRY(set_dev(ctx));
   if (!a) return sod_fail(ctx, SOD_EINVAL, "null args");
-  SOD_TRY(sod_match_enqueue(ctx));
-  SOD_TRY(sod_match_allgather_enqueue(ctx));
+  ctx->fuse_ratio = a->ratio >= 0.0 ? a->ratio : -1.0;   // the final merge applies it too
+  int rc = sod_match_enqueue(ctx);
+  if (rc == SOD_OK) rc = sod_match_allgather_enqueue(ctx);
+  ctx->fuse_ratio = -1.0;
+  SOD_TRY(rc);
   SOD_TRY(sod_ratio_enqueue(ctx, a->ratio));
   const int64_t lo = ctx->nranks > 1 ? ctx->row_offset : 0;
   const int64_t hi = ctx->nranks > 1 ? ctx->row_offset + ctx->n_shard : ctx->n_total;

@@ -286,24 +286,6 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
   }
 }
 
-__global__ void merge_kernel(const float* __restrict__ d1, const int* __restrict__ idx,
-                             const float* __restrict__ d2, int nparts, int64_t stride, int64_t nq,
-                             float* __restrict__ od1, int* __restrict__ oidx,
-                             float* __restrict__ od2, int* __restrict__ reset) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nq) return;
-  // the matcher's shared thresholds of this partial-result slot: "nothing known" again for
-  // the next launch that takes the slot (it waits for this merge)
-  if (reset) reset[q] = (int)0x80808080;
-  float v1 = d1[q], v2 = d2[q];
-  int i1 = idx[q];
-  for (int p = 1; p < nparts; ++p)
-    merge2(v1, i1, v2, d1[p * stride + q], idx[p * stride + q], d2[p * stride + q]);
-  od1[q] = v1;
-  oidx[q] = i1;
-  od2[q] = v2;
-}
-
 // Correctly rounded sqrt of an exact integer-valued float n >= 0 (OpenCV: std::sqrt on
 // the float sum).  The hardware estimate is within an ulp; it is then corrected with the
 // exact midpoint test: a midpoint m of two adjacent floats has <= 25 significant bits, so
@@ -345,6 +327,36 @@ __global__ void ratio_kernel(const float* __restrict__ cd1, const int* __restric
   d2[q] = b;
   idx1[q] = cidx[q];
   good[q] = ((double)a < ratio * (double)b) ? 1 : 0;   // main.py:82, Python floats
+}
+
+// per query: the partial top-2 of every DB chunk (or rank) merged; when this is the final
+// merge of a pipeline call (one rank, or the global merge after the all-gather) and ratio >=
+// 0, the ratio test of ratio_kernel is applied in the same pass (one launch fewer)
+__global__ void merge_kernel(const float* __restrict__ d1, const int* __restrict__ idx,
+                             const float* __restrict__ d2, int nparts, int64_t stride, int64_t nq,
+                             float* __restrict__ od1, int* __restrict__ oidx,
+                             float* __restrict__ od2, int* __restrict__ reset, double ratio,
+                             int64_t nq_real, float* __restrict__ rd1, float* __restrict__ rd2,
+                             int* __restrict__ ridx, uint8_t* __restrict__ rgood) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  // the matcher's shared thresholds of this partial-result slot: "nothing known" again for
+  // the next launch that takes the slot (it waits for this merge)
+  if (reset) reset[q] = (int)0x80808080;
+  float v1 = d1[q], v2 = d2[q];
+  int i1 = idx[q];
+  for (int p = 1; p < nparts; ++p)
+    merge2(v1, i1, v2, d1[p * stride + q], idx[p * stride + q], d2[p * stride + q]);
+  od1[q] = v1;
+  oidx[q] = i1;
+  od2[q] = v2;
+  if (ratio >= 0.0 && q < nq_real) {
+    const float a = sqrt_rn_exact(v1), b = sqrt_rn_exact(v2);
+    rd1[q] = a;
+    rd2[q] = b;
+    ridx[q] = i1;
+    rgood[q] = ((double)a < ratio * (double)b) ? 1 : 0;   // main.py:82, Python floats
+  }
 }
 
 }  // namespace
@@ -420,16 +432,28 @@ int launch_match(sod_ctx* ctx) {
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(sod_match_mark(ctx, ks, 1));
   SOD_TRY(sod_match_stream_end(ctx));
-  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad));
+  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, nullptr,
+                       ctx->nranks <= 1 && !ctx->comm));
   return sod_partials_merged(ctx);   // the slot is free again
 }
 
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2, int nparts,
-                 int64_t stride, int32_t* reset) {
+                 int64_t stride, int32_t* reset, bool final_merge) {
   const int64_t nq_pad = sod_nq_pad(ctx);
   const int bs = 256;
+  // sod_pipeline_enqueue announces its ratio: the final merge applies it as well
+  const bool fuse = final_merge && ctx->fuse_ratio >= 0.0;
+  if (fuse) {
+    SOD_TRY(sod_reserve(ctx, ctx->d1, (size_t)ctx->nq));
+    SOD_TRY(sod_reserve(ctx, ctx->d2, (size_t)ctx->nq));
+    SOD_TRY(sod_reserve(ctx, ctx->idx1, (size_t)ctx->nq));
+    SOD_TRY(sod_reserve(ctx, ctx->good, (size_t)ctx->nq));
+  }
   hipLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, bs)), dim3(bs), 0, ctx->stream,
-                     d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p, ctx->cd2.p, reset);
+                     d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p, ctx->cd2.p, reset,
+                     fuse ? ctx->fuse_ratio : -1.0, (int64_t)ctx->nq, ctx->d1.p, ctx->d2.p,
+                     ctx->idx1.p, ctx->good.p);
+  if (fuse) ctx->ratio_fused = ctx->fuse_ratio;
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }

@@ -1118,6 +1118,7 @@ int launch_match_i8(sod_ctx* ctx) {
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(sod_match_mark(ctx, ks, 1));
   SOD_TRY(sod_match_stream_end(ctx));
-  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, gthr));
+  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, gthr,
+                       ctx->nranks <= 1 && !ctx->comm));   // no exchange follows: final
   return sod_partials_merged(ctx);   // the slot is free again
 }

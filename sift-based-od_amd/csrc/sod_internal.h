@@ -91,6 +91,9 @@ struct sod_ctx {
   DevBuf<uint8_t> good;         // [nq]
   DevBuf<uint32_t> flags;       // [0]=invalid descriptor count, [1]=max dn bits, [2]=max qn bits
   bool matched = false, ratio_done = false;
+  // sod_pipeline_enqueue: the ratio its final merge applies in the same kernel (-1 = none),
+  // and the ratio that merge applied (-1 = not fused), which sod_ratio_enqueue then skips
+  double fuse_ratio = -1.0, ratio_fused = -1.0;
 
   // ---- hough ----
   int32_t bins[4] = {0, 0, 0, 0};
@@ -251,7 +254,7 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
 int sod_match_stream_end(sod_ctx* ctx);
 int sod_partials_merged(sod_ctx* ctx);
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2,
-                 int nparts, int64_t stride, int32_t* reset = nullptr);
+                 int nparts, int64_t stride, int32_t* reset = nullptr, bool final_merge = false);
 int launch_ratio(sod_ctx* ctx, double ratio);
 int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi);
 int launch_select(sod_ctx* ctx, int32_t thr);
