@@ -410,8 +410,11 @@ def main():
     sync_all()
     device_sync(world, dev)
     t0 = time.perf_counter()
+    host = 0.0                      # host time spent enqueueing (the calls return unsynced)
     for _ in range(a.steps):
+        h0 = time.perf_counter()
         step()
+        host += time.perf_counter() - h0
     sync_all()
     device_sync(world, dev)
     D.barrier()
@@ -474,6 +477,7 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": ms_per_step,
+        "host_enqueue_ms_per_step": 1000.0 * host / a.steps,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

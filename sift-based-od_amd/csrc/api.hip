@@ -250,9 +250,9 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->d1); sod_release(ctx->d2); sod_release(ctx->idx1); sod_release(ctx->good);
   sod_release(ctx->flags); sod_release(ctx->sig_lut); sod_release(ctx->counts);
   sod_release(ctx->first); sod_release(ctx->basekey); sod_release(ctx->vmask);
-  sod_release(ctx->pose); sod_release(ctx->blk); sod_release(ctx->scal); sod_release(ctx->vbin);
+  sod_release(ctx->pose); sod_release(ctx->selstat); sod_release(ctx->scal); sod_release(ctx->vbin);
   sod_release(ctx->voff); sod_release(ctx->members); sod_release(ctx->means);
-  sod_release(ctx->mq); sod_release(ctx->vidx); sod_release(ctx->cursor);
+  sod_release(ctx->vidx); sod_release(ctx->cursor);
   sod_release(ctx->rtab);
   sod_release(ctx->allbin); sod_release(ctx->amx); sod_release(ctx->amy); sod_release(ctx->aqx);
   sod_release(ctx->aqy); sod_release(ctx->aisig); sod_release(ctx->surv);

@@ -12,14 +12,16 @@
 //   hist_kernel      LDS-privatised histogram over a slab of bins: counts + first-touch
 //                    ordinal (q*16 + slot = dict insertion order), flushed with integer
 //                    atomics (deterministic)
-//   select_*         votes that are the first touch of a bin with >= thr votes, compacted
-//                    in ordinal order = dict insertion order of main.py:126
+//   select_kernel    votes that are the first touch of a bin with >= thr votes, compacted
+//                    in ordinal order = dict insertion order of main.py:126 (one pass,
+//                    decoupled look-back)
 //   member_fill      wave-aggregated slot reservation: per vote slot, one atomic per distinct
 //                    bin among a wave's lanes reserves a run in the bin's member list
 //   member_order     query order per bin: <= 256 members sorted in one wave's registers,
 //                    larger bins through an LDS bitmap of their query range
 //   members_kernel   fallback for ranges beyond the bitmap (nq > 512 Ki): one wave scans
-//   means_kernel     PoseBin running means, sequential per bin (PoseBin.py:19-43)
+//   means_kernel     PoseBin running means, sequential per bin (PoseBin.py:19-43), its
+//                    members' inputs gathered a batch ahead
 //   affine_kernel    one wave per bin: decoupled 3x3 normal equations, pinv by Jacobi,
 //                    outlier rejection, fixed point (AffineParameters.py:89-160)
 #include <algorithm>
@@ -192,31 +194,81 @@ __global__ void bin_index_batch_kernel(int64_t n, const double* __restrict__ pos
 }
 
 // ---------------------------------------------------------------------------------------
-// LDS-privatised histogram.  blockIdx.x = bin slab, blockIdx.y = query chunk.
-constexpr int kSlab = 8192;     // bins per workgroup: 2 x 32 KiB of LDS
-constexpr int kChunk = 4096;    // queries per workgroup
-constexpr int kHistThreads = 512;
+// LDS-privatised histogram.  blockIdx.x = bin slab, blockIdx.y = query chunk.  A query's 16
+// votes lie in a window of lin_bin(1,1,1,1) bins above its base bin, so a work-group first
+// lists the voting queries of its chunk whose window meets its slab (an LDS list, one atomic
+// per wave) and then votes only those: ~1/slabs of the chunk instead of every query, which
+// cuts the issued LDS atomics (each executed for a wave's in-slab lanes only) by that factor.
+constexpr int kSlab = 8192;     // bins per workgroup
+constexpr int kChunk = 8192;    // queries per workgroup
+constexpr int kHistThreads = 1024;
 
 __global__ __launch_bounds__(kHistThreads) void hist_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
     int64_t nbins, const int* __restrict__ qimg, int64_t nbins1, const int* __restrict__ rng,
     uint32_t* __restrict__ gcount, uint32_t* __restrict__ gfirst) {
-  __shared__ uint32_t cnt[kSlab];
+  // 64 KiB: two work-groups per CU
+  __shared__ uint32_t cnt2[kSlab / 2];     // two u16 counts per word (<= kChunk votes per bin)
   __shared__ uint32_t fst[kSlab];
+  __shared__ unsigned short lst[kChunk];   // chunk-relative queries voting into the slab
+  __shared__ uint32_t nlst;
   // batch of query images: a chunk only visits the slabs of its images' bin ranges
   const int64_t slab = rng ? (int64_t)rng[2 * blockIdx.y] + blockIdx.x : blockIdx.x;
   if (rng && slab > rng[2 * blockIdx.y + 1]) return;
   const uint32_t slab0 = (uint32_t)(slab * kSlab);
   for (int i = threadIdx.x; i < kSlab; i += kHistThreads) {
-    cnt[i] = 0;
+    if (i < kSlab / 2) cnt2[i] = 0;
     fst[i] = 0xFFFFFFFFu;
   }
+  if (threadIdx.x == 0) nlst = 0;
   __syncthreads();
   const int64_t q0 = (int64_t)blockIdx.y * kChunk;
   const int64_t q1 = min(nq, q0 + kChunk);
-  for (int64_t q = q0 + threadIdx.x; q < q1; q += kHistThreads) {
+  const int64_t span = (int64_t)lin_bin(1, 1, 1, 1, b);
+  const int lane = threadIdx.x & 63;
+  // all of a thread's queries are loaded before any is listed: one memory latency per
+  // work-group instead of one per query (the kernel is latency-bound on a CU split's few
+  // reserved CUs)
+  constexpr int kPer = kChunk / kHistThreads;
+  uint32_t mv[kPer], kv[kPer], bv[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t q = q0 + threadIdx.x + (int64_t)u * kHistThreads;
+    mv[u] = q < q1 ? vmask[q] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t q = q0 + threadIdx.x + (int64_t)u * kHistThreads;
+    kv[u] = (mv[u] & 0x10000u) ? basekey[q] : 0u;
+    bv[u] = (qimg && (mv[u] & 0x10000u)) ? (uint32_t)(qimg[q] * nbins1) : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    bool hit = false;
+    // no vote, or the match's DB row is not in this shard: not listed
+    if ((mv[u] & 0xFFFFu) && (mv[u] & 0x10000u)) {
+      const uint32_t key = kv[u];
+      const int64_t lo = (int64_t)bv[u] +
+                         lin_bin(key & 0xFF, (key >> 8) & 0xFF, (key >> 16) & 0xFF, key >> 24, b) -
+                         (int64_t)slab0;
+      hit = lo < kSlab && lo + span >= 0;
+    }
+    const uint64_t bal = __ballot(hit);
+    if (bal) {
+      const int leader = __ffsll((unsigned long long)bal) - 1;
+      uint32_t pos = 0;
+      if (lane == leader) pos = atomicAdd(&nlst, (uint32_t)__popcll(bal));
+      pos = __shfl(pos, leader);
+      if (hit)
+        lst[pos + __popcll(bal & ((1ull << lane) - 1ull))] =
+            (unsigned short)(threadIdx.x + u * kHistThreads);
+    }
+  }
+  __syncthreads();
+  const uint32_t n = nlst;
+  for (uint32_t i = threadIdx.x; i < n; i += kHistThreads) {
+    const int64_t q = q0 + lst[i];
     const uint32_t m = vmask[q];
-    if (!(m & 0x10000u)) continue;  // no vote, or the match's DB row is not in this shard
     const uint32_t key = basekey[q];
     const int ix = key & 0xFF, iy = (key >> 8) & 0xFF, it = (key >> 16) & 0xFF, is = key >> 24;
     const uint32_t base = qimg ? (uint32_t)(qimg[q] * nbins1) : 0u;
@@ -226,14 +278,14 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
       const uint32_t lb = base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
                                          it + ((slot >> 1) & 1), is + (slot & 1), b) - slab0;
       if (lb < (uint32_t)kSlab) {
-        atomicAdd(&cnt[lb], 1u);
+        atomicAdd(&cnt2[lb >> 1], 1u << ((lb & 1u) * 16u));
         atomicMin(&fst[lb], (uint32_t)(q * 16 + slot));
       }
     }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kSlab; i += kHistThreads) {
-    const uint32_t c = cnt[i];
+    const uint32_t c = (cnt2[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
     if (c && slab0 + i < nbins) {
       atomicAdd(&gcount[slab0 + i], c);
       atomicMin(&gfirst[slab0 + i], fst[i]);
@@ -307,65 +359,52 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
   return off + x - v;
 }
 
-__global__ __launch_bounds__(kSelThreads) void select_count_kernel(
+// One pass, decoupled look-back (no count / scan / write kernel chain): a block counts its
+// queries' first-touch slots, publishes its aggregate, and its thread 0 walks back over the
+// preceding blocks' published words until one carries an inclusive prefix.  A status word is
+// (epoch * 4 + flag) << 32 | value, flag 1 = aggregate, 2 = inclusive prefix; a word of an
+// older call (other epoch) reads as "not yet published", so the array needs no reset.
+// Blocks are dispatched in blockIdx order, so every block waited on is resident or done.
+__global__ __launch_bounds__(kSelThreads) void select_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
     const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b,
-    const int* __restrict__ qimg, int64_t nbins1, uint32_t thr, uint32_t* __restrict__ blk) {
+    const int* __restrict__ qimg, int64_t nbins1, uint32_t thr, uint64_t* __restrict__ status,
+    uint32_t epoch, uint32_t* __restrict__ out, uint32_t* __restrict__ vidx,
+    uint32_t* __restrict__ total) {
   __shared__ uint32_t sh[kSelThreads / 64];
+  __shared__ uint32_t excl_s;
   const int64_t q = (int64_t)blockIdx.x * kSelThreads + threadIdx.x;
   uint32_t tmp[16];
   const uint32_t qb = (qimg && q < nq) ? (uint32_t)(qimg[q] * nbins1) : 0u;
   const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, qb, thr, tmp) : 0;
   uint32_t tot;
-  block_excl_scan(n, sh, &tot);
-  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
-}
-
-// single-workgroup exclusive scan, in place; total -> *out_total
-__global__ __launch_bounds__(1024) void scan_u32_kernel(uint32_t* __restrict__ a, int64_t n,
-                                                        uint32_t* __restrict__ out_total) {
-  __shared__ uint32_t sh[16];
-  __shared__ uint32_t carry_s;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (threadIdx.x == 0) carry_s = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < n; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const uint32_t v = i < n ? a[i] : 0;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(x, d);
-      if (lane >= d) x += y;
+  const uint32_t loc = block_excl_scan(n, sh, &tot);
+  if (threadIdx.x == 0) {
+    const uint64_t e4 = (uint64_t)(epoch << 2);
+    const int blk = (int)blockIdx.x;
+    uint32_t ex = 0;
+    if (blk > 0) {
+      __hip_atomic_store(&status[blk], ((e4 | 1u) << 32) | tot, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      for (int j = blk - 1; j >= 0;) {
+        const uint64_t st = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t h = (uint32_t)(st >> 32);
+        if ((h & ~3u) != (uint32_t)e4 || (h & 3u) == 0u) {   // not published yet
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        ex += (uint32_t)st;
+        if ((h & 3u) == 2u) break;
+        --j;
+      }
     }
-    if (lane == 63) sh[w] = x;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int k = 0; k < 16; ++k) {
-      if (k < w) off += sh[k];
-      tot += sh[k];
-    }
-    const uint32_t c = carry_s;
-    if (i < n) a[i] = c + off + x - v;
-    __syncthreads();
-    if (threadIdx.x == 0) carry_s = c + tot;
-    __syncthreads();
+    __hip_atomic_store(&status[blk], ((e4 | 2u) << 32) | (ex + tot), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (blk == (int)gridDim.x - 1) *total = ex + tot;
+    excl_s = ex;
   }
-  if (threadIdx.x == 0) *out_total = carry_s;
-}
-
-__global__ __launch_bounds__(kSelThreads) void select_write_kernel(
-    int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
-    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b,
-    const int* __restrict__ qimg, int64_t nbins1, uint32_t thr, const uint32_t* __restrict__ blk,
-    uint32_t* __restrict__ out, uint32_t* __restrict__ vidx) {
-  __shared__ uint32_t sh[kSelThreads / 64];
-  const int64_t q = (int64_t)blockIdx.x * kSelThreads + threadIdx.x;
-  uint32_t tmp[16];
-  const uint32_t qb = (qimg && q < nq) ? (uint32_t)(qimg[q] * nbins1) : 0u;
-  const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, qb, thr, tmp) : 0;
-  uint32_t tot;
-  const uint32_t pos = blk[blockIdx.x] + block_excl_scan(n, sh, &tot);
+  __syncthreads();
+  const uint32_t pos = excl_s + loc;
   for (uint32_t i = 0; i < n; ++i) {
     out[pos + i] = tmp[i];
     if (vidx) vidx[tmp[i]] = pos + i;   // bin -> valid index (reset after the member sort)
@@ -688,50 +727,17 @@ __global__ __launch_bounds__(256) void members_kernel(
   }
 }
 
-constexpr int kGatherK = 4;   // members per thread per round in the gather kernels
-
 // PoseBin running means in vote order (PoseBin.py:19-43).  The recurrence
 //   v' = (v*n + new) / (n+1)
 // rounds at every step, so each bin's chain is inherently sequential; but the six
-// quantities are independent chains and their inputs can be fetched in parallel first:
-// means_gather_kernel writes per-member SoA values (x, y, alpha, s, w, h), then
-// means_kernel runs one wave per bin (six quantity chains in lockstep).
-__global__ void means_gather_kernel(const uint32_t* __restrict__ scal,
-                                    const int32_t* __restrict__ members,
-                                    const double* __restrict__ pose, const int* __restrict__ idx1,
-                                    const int* __restrict__ mimg, const int* __restrict__ isize,
-                                    int64_t mstride, double* __restrict__ mq) {
-  // kGatherK members per thread per round: each level of the dependent gather (member ->
-  // query -> model keypoint -> model image -> size) is issued for all of them before the
-  // next, so a thread waits kGatherK times less on memory latency (the kernel runs on the
-  // few reserved CUs of a chip split, where latency, not bandwidth, bounds it)
-  const int64_t M = scal[1];
-  const int64_t step = (int64_t)gridDim.x * blockDim.x * kGatherK;
-  for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * kGatherK + threadIdx.x; e0 < M; e0 += step) {
-    int q[kGatherK], im[kGatherK];
-#pragma unroll
-    for (int i = 0; i < kGatherK; ++i) {
-      const int64_t e = e0 + (int64_t)i * blockDim.x;
-      q[i] = e < M ? members[e] : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < kGatherK; ++i) im[i] = idx1[q[i]];
-#pragma unroll
-    for (int i = 0; i < kGatherK; ++i) im[i] = mimg[im[i]];
-#pragma unroll
-    for (int i = 0; i < kGatherK; ++i) {
-      const int64_t e = e0 + (int64_t)i * blockDim.x;
-      if (e >= M) break;
-      const double* p = pose + 4 * (int64_t)q[i];
-      mq[0 * mstride + e] = p[0];
-      mq[1 * mstride + e] = p[1];
-      mq[2 * mstride + e] = p[2];
-      mq[3 * mstride + e] = p[3];
-      mq[4 * mstride + e] = (double)isize[2 * im[i]];
-      mq[5 * mstride + e] = (double)isize[2 * im[i] + 1];
-    }
-  }
-}
+// quantities (x, y, alpha, s, w, h) are independent chains and their inputs can be fetched in
+// parallel first.  One wave per valid bin; lanes 0-5 run the six chains in lockstep (same n,
+// same 1/(n+1)).  All 64 lanes gather the next 64 members' inputs (member -> query -> pose,
+// model keypoint -> model image -> size) into LDS while the chains run on the current batch,
+// so a chain step is 5 dependent f64 ops and never a memory wait.  Division r / d (d = n + 1)
+// is RN(r * inv) corrected by one FMA residual step (Markstein): with inv = RN(1/d) the result
+// equals the correctly rounded r / d (verified against r / d on 2e8 random cases).
+constexpr int kGatherK = 4;   // members per thread per round in affine_gather_kernel
 
 __global__ void recip_table_kernel(int64_t M, double* __restrict__ rtab) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M;
@@ -739,15 +745,13 @@ __global__ void recip_table_kernel(int64_t M, double* __restrict__ rtab) {
     rtab[i] = 1.0 / (double)(i + 1);
 }
 
-// One wave per valid bin; lanes 0-5 run the six quantity chains in lockstep (same n, same
-// 1/(n+1)).  All 64 lanes stage the next 64 members' inputs (coalesced) into LDS while the
-// chains run on the current batch, so a chain step is 5 dependent f64 ops and never a
-// memory wait.  Division r / d (d = n + 1) is RN(r * inv) corrected by one FMA residual
-// step (Markstein): with inv = RN(1/d) the result equals the correctly rounded r / d
-// (verified against r / d on 2e8 random cases).
 __global__ __launch_bounds__(64) void means_kernel(const uint32_t* __restrict__ scal,
                                                    const int64_t* __restrict__ voff,
-                                                   const double* __restrict__ mq, int64_t mstride,
+                                                   const int32_t* __restrict__ members,
+                                                   const double* __restrict__ pose,
+                                                   const int* __restrict__ idx1,
+                                                   const int* __restrict__ mimg,
+                                                   const int* __restrict__ isize,
                                                    const double* __restrict__ rtab,
                                                    double* __restrict__ means) {
   __shared__ double xs[2][7][64];   // [buffer][quantity 0-5, 1/(n+1)][member]
@@ -756,26 +760,32 @@ __global__ __launch_bounds__(64) void means_kernel(const uint32_t* __restrict__ 
   const int64_t V = scal[0];
   for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
     const int64_t a = voff[v], e = voff[v + 1];
-    double m = mq[k * mstride + a];        // first vote: mean = pose / model size
-    // batch b covers members a+1+64b ... ; n of member j is j - a
+    // batch b covers members a+64b ... ; n of member j is j - a (the first one sets the mean)
     double nx[7];
     auto fetch = [&](int64_t j0) {
       const int64_t j = j0 + lane;
+      const bool in = j < e;
+      const int q = in ? members[j] : 0;
+      const int im = mimg[idx1[q]];
+      const double* p = pose + 4 * (int64_t)q;
 #pragma unroll
-      for (int q = 0; q < 6; ++q) nx[q] = j < e ? mq[q * mstride + j] : 0.0;
-      nx[6] = j < e ? rtab[j - a] : 0.0;   // 1 / (n + 1)
+      for (int c = 0; c < 4; ++c) nx[c] = in ? p[c] : 0.0;
+      nx[4] = in ? (double)isize[2 * im] : 0.0;
+      nx[5] = in ? (double)isize[2 * im + 1] : 0.0;
+      nx[6] = in ? rtab[j - a] : 0.0;   // 1 / (n + 1)
     };
+    double m = 0.0;
     int buf = 0;
-    fetch(a + 1);
-    for (int64_t j0 = a + 1; j0 < e; j0 += 64) {
+    fetch(a);
+    for (int64_t j0 = a; j0 < e; j0 += 64) {
 #pragma unroll
-      for (int q = 0; q < 7; ++q) xs[buf][q][lane] = nx[q];
+      for (int c = 0; c < 7; ++c) xs[buf][c][lane] = nx[c];
       __builtin_amdgcn_wave_barrier();
       if (j0 + 64 < e) fetch(j0 + 64);     // in flight during the chains below
       const int cnt = (int)min<int64_t>(64, e - j0);
       if (lane < 6) {
         const double n0 = (double)(j0 - a);
-        if (cnt == 64) {   // full batch: unrolled, LDS reads run ahead of the chain
+        if (cnt == 64 && j0 != a) {   // full batch: unrolled, LDS reads run ahead of the chain
 #pragma unroll
           for (int i = 0; i < 64; ++i) {
             const double n = n0 + i, d = n + 1.0, inv = xs[buf][6][i];
@@ -784,7 +794,12 @@ __global__ __launch_bounds__(64) void means_kernel(const uint32_t* __restrict__ 
             m = __builtin_fma(__builtin_fma(-q0, d, r), inv, q0);
           }
         } else {
-          for (int i = 0; i < cnt; ++i) {
+          int i0 = 0;
+          if (j0 == a) {              // first vote: mean = pose / model size
+            m = xs[buf][k][0];
+            i0 = 1;
+          }
+          for (int i = i0; i < cnt; ++i) {
             const double n = n0 + i, d = n + 1.0, inv = xs[buf][6][i];
             const double r = m * n + xs[buf][k][i];
             const double q0 = r * inv;
@@ -812,7 +827,7 @@ __global__ void affine_gather_kernel(const uint32_t* __restrict__ scal,
                                      int32_t* __restrict__ aisig, int32_t* __restrict__ bwh) {
   const int64_t M = scal[1], V = scal[0];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // kGatherK members per thread per round, each gather level issued for all (as means_gather)
+  // kGatherK members per thread per round, each gather level issued for all of them
   for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * kGatherK + threadIdx.x; e0 < M;
        e0 += stride * kGatherK) {
     int q[kGatherK], m[kGatherK];
@@ -1105,18 +1120,16 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
 static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* total_slot,
                           uint32_t* vidx) {
   const int64_t nq = sod_win_n(ctx);
-  const int64_t nblk = cdiv(nq, kSelThreads);
-  SOD_TRY(sod_reserve(ctx, ctx->blk, (size_t)nblk));
-  hipLaunchKernelGGL(select_count_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream,
-                     nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
-                     qimg_p(ctx), ctx->nbins1, thr, ctx->blk.p);
-  SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(scan_u32_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->blk.p, nblk,
+  const int64_t nblk = std::max<int64_t>(1, cdiv(nq, kSelThreads));
+  if (ctx->selstat.n < (size_t)nblk) {   // look-back words: zero = never published
+    SOD_TRY(sod_reserve(ctx, ctx->selstat, (size_t)nblk));
+    SOD_HIP(ctx, hipMemsetAsync(ctx->selstat.p, 0, ctx->selstat.n * 8, ctx->stream));
+  }
+  ctx->sel_epoch = ctx->sel_epoch >= (1u << 30) - 1 ? 1u : ctx->sel_epoch + 1;
+  hipLaunchKernelGGL(select_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream, nq,
+                     ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
+                     qimg_p(ctx), ctx->nbins1, thr, ctx->selstat.p, ctx->sel_epoch, out, vidx,
                      total_slot);
-  SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(select_write_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream,
-                     nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
-                     qimg_p(ctx), ctx->nbins1, thr, ctx->blk.p, out, vidx);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
@@ -1161,17 +1174,12 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   }
   // PoseBin means depend only on the member lists: they run on the side stream, beside the
   // affine verification, and the main stream joins them at the next entry point (set_dev)
-  SOD_TRY(sod_reserve(ctx, ctx->mq, (size_t)ctx->mmax * 6));
   // 1/(n+1) for every n a member list of this capacity can reach: built once per capacity
-  // (a bin's chain reads entry n - 1 for its n-th member)
+  // (a bin's chain reads entry n for its member n)
   const bool new_rtab = ctx->rtab.n < (size_t)ctx->mmax;
   SOD_TRY(sod_reserve(ctx, ctx->rtab, (size_t)ctx->mmax));
   SOD_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
   SOD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-  hipLaunchKernelGGL(means_gather_kernel, dim3(std::max(1, ctx->tail_cus() * 4)), dim3(256), 0,
-                     ctx->side, ctx->scal.p, ctx->members.p, ctx->pose.p, ctx->idx1.p + sod_win0(ctx),
-                     ctx->mimg.p, ctx->isize.p, ctx->mmax, ctx->mq.p);
-  SOD_HIP(ctx, hipGetLastError());
   if (new_rtab) {
     hipLaunchKernelGGL(recip_table_kernel, dim3((unsigned)std::min<int64_t>(cdiv(ctx->rtab.n, 256), 4096)),
                        dim3(256), 0, ctx->side, (int64_t)ctx->rtab.n, ctx->rtab.p);
@@ -1180,7 +1188,9 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   // one wave per bin, each a serial f64 chain: as many chains in flight as LDS allows
   // (7 KiB per wave: 16 per CU)
   hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->tail_cus() * 16)), dim3(64), 0, ctx->side,
-                     ctx->scal.p, ctx->voff.p, ctx->mq.p, ctx->mmax, ctx->rtab.p, ctx->means.p);
+                     ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->pose.p,
+                     ctx->idx1.p + sod_win0(ctx), ctx->mimg.p, ctx->isize.p, ctx->rtab.p,
+                     ctx->means.p);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
   ctx->side_pending = true;

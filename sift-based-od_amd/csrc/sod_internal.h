@@ -108,13 +108,13 @@ struct sod_ctx {
   bool houghed = false;
 
   // ---- select / CSR / means ----
-  DevBuf<uint32_t> blk;         // block counts / offsets for compaction
+  DevBuf<uint64_t> selstat;     // look-back words of select_kernel (one per block)
+  uint32_t sel_epoch = 0;       // select_kernel call count: tags the look-back words
   DevBuf<uint32_t> scal;        // device scalars: [0]=V, [1]=total members, [2]=B (all bins)
   DevBuf<uint32_t> vbin;        // [vmax] linear bin id, first-touch order
   DevBuf<int64_t> voff;         // [vmax+1]
   DevBuf<int32_t> members;      // [mmax] query index
   DevBuf<double> means;         // [vmax*6]
-  DevBuf<double> mq;            // [6][mmax] per-member mean inputs
   DevBuf<uint32_t> vidx;        // [nbins] bin -> valid index (0xFFFFFFFF otherwise)
   DevBuf<uint32_t> cursor;      // [vmax] member fill cursors
   DevBuf<double> rtab;          // [mmax] 1/(n+1) for the running means
