@@ -400,6 +400,8 @@ def main():
         for c in ctxs:
             c.synchronize()
 
+    for c in ctxs:
+        c.set_stage_timing(False)   # stage events are marker packets on the tail's path
     for _ in range(a.warmup):
         step()
     sync_all()
@@ -433,6 +435,7 @@ def main():
 
     # ---- per-stage timing (HIP events on the ctx stream), separate untimed steps --------
     match_iso = []
+    ctx.set_stage_timing(True)
     for _ in range(max(3, min(a.steps, 10))):
         turn[0] = 0            # always the first context (its events are read below)
         step()

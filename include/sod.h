@@ -57,6 +57,10 @@ int sod_last_match_ms(sod_ctx* ctx, float* ms);
  * the kernel timed inside a pipelined run.  Waits for those launches. */
 int sod_match_times(sod_ctx* ctx, int n, float* ms);
 int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n); /* match,merge,hough,select,affine */
+/* Stage events (the bounds sod_last_stage_ms reads) on (1, the default) or off (0): each is
+ * a marker packet on the tail's critical path, so a timed loop turns them off.  With them
+ * off, sod_last_stage_ms reports 0 for the stages after the matcher. */
+int sod_set_stage_timing(sod_ctx* ctx, int on);
 
 /* ---- database (replaces main.py:36-66 flattening + GenerateDatabaseInfo.py format) --
  * Keypoints and the per-image table cover the WHOLE database (replicated on every

@@ -48,6 +48,7 @@ SIGNATURES = {
     "sod_last_match_ms": (C.c_int, [c_ctx, c_f32p]),
     "sod_match_times": (C.c_int, [c_ctx, C.c_int, c_f32p]),
     "sod_last_stage_ms": (C.c_int, [c_ctx, c_f32p, C.c_int]),
+    "sod_set_stage_timing": (C.c_int, [c_ctx, C.c_int]),
     "sod_db_set_keypoints": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_i32p,
                                        C.c_int32, c_f64p, c_i32p]),
     "sod_db_upload_descriptors": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int64, C.c_int64]),
@@ -369,6 +370,10 @@ class Context:
         out = np.zeros(int(n), np.float32)
         self._chk(self._L.sod_match_times(self._h, int(n), ptr(out, C.c_float)))
         return out
+
+    def set_stage_timing(self, on):
+        """Record the per-stage events read by stage_ms (default on; off in timed loops)."""
+        self._chk(self._L.sod_set_stage_timing(self._h, 1 if on else 0))
 
     def stage_ms(self):
         out = np.zeros(5, np.float32)

@@ -23,6 +23,7 @@ int set_dev(sod_ctx* ctx, bool join = true) {
   if (join && ctx->side_pending) {
     SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
     ctx->side_pending = false;
+    ctx->means_waited = ctx->means_id;   // ev_join follows the newest means launch
   }
   return SOD_OK;
 }
@@ -75,7 +76,7 @@ static int wait_unless_done(sod_ctx* ctx, hipStream_t s, hipEvent_t ev) {
   return SOD_OK;
 }
 int sod_inputs_begin(sod_ctx* ctx) {
-  SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0));
+  SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_matched_p ? ctx->ev_matched_p : ctx->ev_matched, 0));
   return SOD_OK;
 }
 int sod_inputs_end(sod_ctx* ctx) {
@@ -104,7 +105,12 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
   }
   *ks = ctx->mstream;
   SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_inputs));
-  SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_merged[ctx->pslot]));
+  // the slot's previous merge (two launches back) must be done before the kernel rewrites
+  // it: the host waits for it here rather than the matcher stream (a satisfied barrier packet
+  // between two back-to-back matcher launches costs ~6 us per launch, C2 0.166 vs 0.160 ms per
+  // step); it bounds a context to two matcher launches in flight, and the merge it waits for
+  // ran right after the launch before the previous one, so the wait is normally over already
+  SOD_HIP(ctx, hipEventSynchronize(ctx->ev_merged[ctx->pslot]));
   // a new slot size moves the slots' boundaries: the other slot's last merge must be done too
   if (resized) SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_merged[ctx->pslot ^ 1]));
   return SOD_OK;
@@ -120,10 +126,25 @@ int sod_partials_merged(sod_ctx* ctx) {
   SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[ctx->pslot], ctx->stream));
   return SOD_OK;
 }
-int sod_match_stream_end(sod_ctx* ctx) {
+// begin / end events of the next matcher launch, recorded by the launch itself
+// (hipExtLaunchKernelGGL: timestamps in the dispatch, no marker packets around the kernel)
+int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end) {
+  hipEvent_t* e = ctx->mev[ctx->nmatch % sod_ctx::kMatchRing];
+  for (int i = 0; i < 2; ++i)
+    if (!e[i]) SOD_HIP(ctx, hipEventCreate(&e[i]));
+  *begin = e[0];
+  *end = e[1];
+  ++ctx->nmatch;
+  return SOD_OK;
+}
+int sod_match_stream_end(sod_ctx* ctx, hipEvent_t done) {
   const hipStream_t ks = ctx->overlap ? ctx->mstream : ctx->stream;
-  SOD_HIP(ctx, hipEventRecord(ctx->ev_matched, ks));
-  if (ctx->overlap) SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0));
+  if (!done) {
+    SOD_HIP(ctx, hipEventRecord(ctx->ev_matched, ks));
+    done = ctx->ev_matched;
+  }
+  ctx->ev_matched_p = done;
+  if (ctx->overlap) SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, done, 0));
   return SOD_OK;
 }
 
@@ -253,7 +274,9 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->pose); sod_release(ctx->selstat); sod_release(ctx->scal); sod_release(ctx->vbin);
   sod_release(ctx->voff); sod_release(ctx->members); sod_release(ctx->means);
   sod_release(ctx->vidx); sod_release(ctx->cursor);
-  sod_release(ctx->rtab);
+  sod_release(ctx->rtab); sod_release(ctx->msize);
+  sod_release(ctx->pose_b); sod_release(ctx->msize_b); sod_release(ctx->scal_b);
+  sod_release(ctx->voff_b); sod_release(ctx->members_b); sod_release(ctx->means_b);
   sod_release(ctx->allbin); sod_release(ctx->amx); sod_release(ctx->amy); sod_release(ctx->aqx);
   sod_release(ctx->aqy); sod_release(ctx->aisig); sod_release(ctx->surv);
   sod_release(ctx->fvotes); sod_release(ctx->params); sod_release(ctx->alive);
@@ -267,6 +290,10 @@ void sod_destroy(sod_ctx* ctx) {
       if (e) (void)hipEventDestroy(e);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  for (int i = 0; i < 2; ++i) {
+    if (ctx->ev_hread[i]) (void)hipEventDestroy(ctx->ev_hread[i]);
+    if (ctx->ev_sread[i]) (void)hipEventDestroy(ctx->ev_sread[i]);
+  }
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->ev_inputs) (void)hipEventDestroy(ctx->ev_inputs);
   for (auto& ev : ctx->ev_merged)
@@ -309,13 +336,21 @@ int sod_match_times(sod_ctx* ctx, int n, float* ms) {
   return SOD_OK;
 }
 
+int sod_set_stage_timing(sod_ctx* ctx, int on) {
+  SOD_TRY(set_dev(ctx));
+  if (on != 0 && on != 1) return sod_fail(ctx, SOD_EINVAL, "stage timing must be 0 or 1");
+  ctx->stage_timing = on != 0;
+  return SOD_OK;
+}
+
 int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n) {
   // [match kernel, merge+allgather+ratio, hough vote (+allreduce), select, affine]
   SOD_TRY(set_dev(ctx));
   if (!ms_out) return sod_fail(ctx, SOD_EINVAL, "null output");
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  const bool rec[6] = {ctx->matched, ctx->matched, ctx->houghed, ctx->houghed, ctx->selected,
-                       ctx->affined};
+  const bool st = ctx->stage_timing;
+  const bool rec[6] = {ctx->matched, ctx->matched, st && ctx->houghed, st && ctx->houghed,
+                       st && ctx->selected, st && ctx->affined};
   // the last matcher launch's begin / end events (sod_match_mark) bound stages 0 and 1
   hipEvent_t evs[6];
   for (int i = 0; i < 6; ++i) evs[i] = ctx->ev[i];
@@ -621,7 +656,7 @@ int sod_valid_images_get(sod_ctx* ctx, int32_t* image) {
 
 // ---- matcher --------------------------------------------------------------------------
 int sod_match_enqueue(sod_ctx* ctx) {
-  SOD_TRY(set_dev(ctx));
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
   ctx->ratio_fused = -1.0;   // set again by a final merge that applies the pipeline's ratio
   SOD_TRY(ctx->impl != 0 ? launch_match_i8(ctx) : launch_match(ctx));
@@ -732,7 +767,7 @@ int sod_match_set_impl(sod_ctx* ctx, int impl) {
 }
 
 int sod_match_allgather_enqueue(sod_ctx* ctx) {
-  SOD_TRY(set_dev(ctx));
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
   if (ctx->nranks <= 1 && !ctx->comm) return SOD_OK;   // a 1-rank communicator still runs
   if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
@@ -755,7 +790,7 @@ int sod_match_allgather_enqueue(sod_ctx* ctx) {
 }
 
 int sod_ratio_enqueue(sod_ctx* ctx, double ratio) {
-  SOD_TRY(set_dev(ctx));
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
   if (ctx->ratio_fused != ratio) SOD_TRY(launch_ratio(ctx, ratio));   // else the merge did it
   ctx->ratio_done = true;
@@ -811,7 +846,7 @@ int sod_match_exact_order(sod_ctx* ctx, int* exact) {
 // ---- hough ----------------------------------------------------------------------------
 int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int32_t bins[4],
                       int64_t own_lo, int64_t own_hi) {
-  SOD_TRY(set_dev(ctx));
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "match + ratio first");
   if (!ctx->n_total || !ctx->qx.p) return sod_fail(ctx, SOD_ESTATE, "keypoints not uploaded");
   if (query_h < 1 || query_w < 1) return sod_fail(ctx, SOD_EINVAL, "bad query image shape");
@@ -823,16 +858,16 @@ int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int3
   }
   ctx->qh = query_h;
   ctx->qw = query_w;
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+  if (ctx->stage_timing) SOD_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
   SOD_TRY(launch_hough(ctx, own_lo, own_hi));
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+  if (ctx->stage_timing) SOD_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
   ctx->houghed = true;
   ctx->selected = ctx->affined = false;
   return SOD_OK;
 }
 
 int sod_hough_allreduce_enqueue(sod_ctx* ctx) {
-  SOD_TRY(set_dev(ctx));
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
   if (ctx->nranks <= 1 && !ctx->comm) return SOD_OK;   // a 1-rank communicator still runs
   if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
@@ -849,10 +884,10 @@ int sod_hough_allreduce_enqueue(sod_ctx* ctx) {
 }
 
 int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold) {
-  SOD_TRY(set_dev(ctx));
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
   SOD_TRY(launch_select(ctx, vote_threshold));
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+  if (ctx->stage_timing) SOD_HIP(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->vote_thr = vote_threshold;
   ctx->selected = true;
   ctx->affined = false;
@@ -941,7 +976,7 @@ int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_
                         x_factor, y_factor, threshold, 1 << 30,
                         nullptr, ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p,
                         ctx->scal.p));
-  SOD_HIP(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+  if (ctx->stage_timing) SOD_HIP(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
   ctx->affined = true;
   return SOD_OK;
 }
@@ -961,7 +996,7 @@ int sod_affine_get(sod_ctx* ctx, uint8_t* survived, int32_t* votes, double* para
 
 // ---- fused pipeline -------------------------------------------------------------------
 int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* a) {
-  SOD_TRY(set_dev(ctx));
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!a) return sod_fail(ctx, SOD_EINVAL, "null args");
   ctx->fuse_ratio = a->ratio >= 0.0 ? a->ratio : -1.0;   // the final merge applies it too
   int rc = sod_match_enqueue(ctx);

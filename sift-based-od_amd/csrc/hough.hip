@@ -25,6 +25,7 @@
 //   affine_kernel    one wave per bin: decoupled 3x3 normal equations, pinv by Jacobi,
 //                    outlier rejection, fixed point (AffineParameters.py:89-160)
 #include <algorithm>
+#include <utility>
 
 #include "sod_internal.h"
 
@@ -114,7 +115,8 @@ __global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
                             const int* __restrict__ lut, int64_t own_lo, int64_t own_hi,
                             double* __restrict__ pose, uint32_t* __restrict__ basekey,
                             uint32_t* __restrict__ vmask, int64_t nbins,
-                            uint32_t* __restrict__ counts, uint32_t* __restrict__ first) {
+                            uint32_t* __restrict__ counts, uint32_t* __restrict__ first,
+                            const int* __restrict__ isize, int2* __restrict__ msize) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // the histogram the next kernel fills starts empty: count 0, first touch "none" (folded
   // in here instead of two memset launches on the tail's critical path)
@@ -141,6 +143,7 @@ __global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
   pose[4 * q + 1] = p[1];
   pose[4 * q + 2] = p[2];
   pose[4 * q + 3] = p[3];
+  msize[q] = make_int2(isize[2 * im], isize[2 * im + 1]);   // PoseBin img_size input
   basekey[q] = (uint32_t)ix[0] | ((uint32_t)ix[1] << 8) | ((uint32_t)ix[2] << 16) |
                ((uint32_t)ix[3] << 24);
   // main.py:105-110: 16 votes, kept when every index is < bins (no theta wrap)
@@ -745,70 +748,79 @@ __global__ void recip_table_kernel(int64_t M, double* __restrict__ rtab) {
     rtab[i] = 1.0 / (double)(i + 1);
 }
 
+constexpr int kMeansU = 4;                  // members per lane per fetch: 256 per batch
+constexpr int kMeansB = 64 * kMeansU;
+
 __global__ __launch_bounds__(64) void means_kernel(const uint32_t* __restrict__ scal,
                                                    const int64_t* __restrict__ voff,
                                                    const int32_t* __restrict__ members,
                                                    const double* __restrict__ pose,
-                                                   const int* __restrict__ idx1,
-                                                   const int* __restrict__ mimg,
-                                                   const int* __restrict__ isize,
+                                                   const int2* __restrict__ msize,
                                                    const double* __restrict__ rtab,
                                                    double* __restrict__ means) {
-  __shared__ double xs[2][7][64];   // [buffer][quantity 0-5, 1/(n+1)][member]
+  // one buffer: the wave stores a batch, runs its chains, and only then stores the next
+  __shared__ double xs[7][kMeansB];   // [quantity 0-5, 1/(n+1)][member]
   const int lane = threadIdx.x;
   const int k = lane < 6 ? lane : 0;
   const int64_t V = scal[0];
   for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
     const int64_t a = voff[v], e = voff[v + 1];
-    // batch b covers members a+64b ... ; n of member j is j - a (the first one sets the mean)
-    double nx[7];
-    auto fetch = [&](int64_t j0) {
-      const int64_t j = j0 + lane;
-      const bool in = j < e;
-      const int q = in ? members[j] : 0;
-      const int im = mimg[idx1[q]];
-      const double* p = pose + 4 * (int64_t)q;
+    // batch b covers members a+256b ... ; n of member j is j - a (the first one sets the mean)
+    double nx[kMeansU][7];
+    auto fetch = [&](int64_t j0) {   // two dependent levels: member -> (pose, model size)
+      int q[kMeansU];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) nx[c] = in ? p[c] : 0.0;
-      nx[4] = in ? (double)isize[2 * im] : 0.0;
-      nx[5] = in ? (double)isize[2 * im + 1] : 0.0;
-      nx[6] = in ? rtab[j - a] : 0.0;   // 1 / (n + 1)
+      for (int u = 0; u < kMeansU; ++u) {
+        const int64_t j = j0 + u * 64 + lane;
+        q[u] = j < e ? members[j] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < kMeansU; ++u) {
+        const int64_t j = j0 + u * 64 + lane;
+        const bool in = q[u] >= 0;
+        const double* p = pose + 4 * (int64_t)(in ? q[u] : 0);
+        const int2 wh = msize[in ? q[u] : 0];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) nx[u][c] = in ? p[c] : 0.0;
+        nx[u][4] = in ? (double)wh.x : 0.0;
+        nx[u][5] = in ? (double)wh.y : 0.0;
+        nx[u][6] = in ? rtab[j - a] : 0.0;   // 1 / (n + 1)
+      }
     };
     double m = 0.0;
-    int buf = 0;
     fetch(a);
-    for (int64_t j0 = a; j0 < e; j0 += 64) {
+    for (int64_t j0 = a; j0 < e; j0 += kMeansB) {
 #pragma unroll
-      for (int c = 0; c < 7; ++c) xs[buf][c][lane] = nx[c];
+      for (int u = 0; u < kMeansU; ++u)
+#pragma unroll
+        for (int c = 0; c < 7; ++c) xs[c][u * 64 + lane] = nx[u][c];
       __builtin_amdgcn_wave_barrier();
-      if (j0 + 64 < e) fetch(j0 + 64);     // in flight during the chains below
-      const int cnt = (int)min<int64_t>(64, e - j0);
+      if (j0 + kMeansB < e) fetch(j0 + kMeansB);   // in flight during the chains below
+      const int cnt = (int)min<int64_t>(kMeansB, e - j0);
       if (lane < 6) {
         const double n0 = (double)(j0 - a);
-        if (cnt == 64 && j0 != a) {   // full batch: unrolled, LDS reads run ahead of the chain
+        int i = 0;
+        if (j0 == a) {              // first vote: mean = pose / model size
+          m = xs[k][0];
+          i = 1;
+        }
+        for (; i + 16 <= cnt; i += 16) {   // unrolled: LDS reads run ahead of the chain
 #pragma unroll
-          for (int i = 0; i < 64; ++i) {
-            const double n = n0 + i, d = n + 1.0, inv = xs[buf][6][i];
-            const double r = m * n + xs[buf][k][i];   // -ffp-contract=off: 2 roundings
-            const double q0 = r * inv;
-            m = __builtin_fma(__builtin_fma(-q0, d, r), inv, q0);
-          }
-        } else {
-          int i0 = 0;
-          if (j0 == a) {              // first vote: mean = pose / model size
-            m = xs[buf][k][0];
-            i0 = 1;
-          }
-          for (int i = i0; i < cnt; ++i) {
-            const double n = n0 + i, d = n + 1.0, inv = xs[buf][6][i];
-            const double r = m * n + xs[buf][k][i];
+          for (int t = 0; t < 16; ++t) {
+            const double n = n0 + (i + t), d = n + 1.0, inv = xs[6][i + t];
+            const double r = m * n + xs[k][i + t];   // -ffp-contract=off: 2 roundings
             const double q0 = r * inv;
             m = __builtin_fma(__builtin_fma(-q0, d, r), inv, q0);
           }
         }
+        for (; i < cnt; ++i) {
+          const double n = n0 + i, d = n + 1.0, inv = xs[6][i];
+          const double r = m * n + xs[k][i];
+          const double q0 = r * inv;
+          m = __builtin_fma(__builtin_fma(-q0, d, r), inv, q0);
+        }
       }
       __builtin_amdgcn_wave_barrier();
-      buf ^= 1;
     }
     if (lane < 6) means[6 * v + k] = m;
   }
@@ -1068,11 +1080,37 @@ int launch_bin_index_batch(sod_ctx* ctx, int64_t n, const double* pose, int32_t*
   return SOD_OK;
 }
 
+// the next parity of a double-buffered set: usable once the means that read it are done
+// (no wait when the stream already waited for that launch or a later one, or it is done)
+static int next_parity(sod_ctx* ctx, int& par, hipEvent_t (&ev)[2], uint64_t (&id)[2]) {
+  par ^= 1;
+  if (id[par] == 0 || id[par] <= ctx->means_waited) return SOD_OK;
+  const hipError_t q = hipEventQuery(ev[par]);
+  if (q != hipSuccess) {
+    if (q != hipErrorNotReady) SOD_HIP(ctx, q);
+    (void)hipGetLastError();   // hipErrorNotReady is an answer, not an error
+    SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ev[par], 0));
+  }
+  ctx->means_waited = id[par];
+  return SOD_OK;
+}
+
+static int mark_read(sod_ctx* ctx, hipStream_t s, int par, hipEvent_t (&ev)[2], uint64_t (&id)[2]) {
+  if (!ev[par]) SOD_HIP(ctx, hipEventCreateWithFlags(&ev[par], hipEventDisableTiming));
+  SOD_HIP(ctx, hipEventRecord(ev[par], s));
+  id[par] = ctx->means_id;
+  return SOD_OK;
+}
+
 int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
   const int64_t nq = sod_win_n(ctx), q0 = sod_win0(ctx);
+  std::swap(ctx->pose, ctx->pose_b);
+  std::swap(ctx->msize, ctx->msize_b);
+  SOD_TRY(next_parity(ctx, ctx->hpar, ctx->ev_hread, ctx->hread_id));
   SOD_TRY(sod_reserve(ctx, ctx->pose, (size_t)nq * 4));
   SOD_TRY(sod_reserve(ctx, ctx->basekey, (size_t)nq));
   SOD_TRY(sod_reserve(ctx, ctx->vmask, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->msize, (size_t)nq * 2));
   SOD_TRY(sod_reserve(ctx, ctx->counts, (size_t)ctx->nbins));
   SOD_TRY(sod_reserve(ctx, ctx->first, (size_t)ctx->nbins));
   const int bs = 256;
@@ -1084,7 +1122,8 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
                      ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p,
                      ctx->qh, ctx->qw, qimg_p(ctx), ctx->n_qimg ? ctx->qshape.p : nullptr,
                      ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
-                     ctx->basekey.p, ctx->vmask.p, ctx->nbins, ctx->counts.p, ctx->first.p);
+                     ctx->basekey.p, ctx->vmask.p, ctx->nbins, ctx->counts.p, ctx->first.p,
+                     ctx->isize.p, reinterpret_cast<int2*>(ctx->msize.p));
   SOD_HIP(ctx, hipGetLastError());
   const int64_t nchunk = cdiv(nq, kChunk);
   dim3 grid((unsigned)cdiv(ctx->nbins, kSlab), (unsigned)nchunk);
@@ -1136,6 +1175,11 @@ static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* t
 
 int launch_select(sod_ctx* ctx, int32_t thr) {
   const int64_t nq = sod_win_n(ctx);
+  std::swap(ctx->scal, ctx->scal_b);
+  std::swap(ctx->voff, ctx->voff_b);
+  std::swap(ctx->members, ctx->members_b);
+  std::swap(ctx->means, ctx->means_b);
+  SOD_TRY(next_parity(ctx, ctx->spar, ctx->ev_sread, ctx->sread_id));
   if (thr < 1) thr = 1;  // a bin exists only once voted for
   ctx->vmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * nq));
   ctx->mmax = std::max<int64_t>(1, 16 * nq);
@@ -1173,7 +1217,8 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
     SOD_HIP(ctx, hipGetLastError());
   }
   // PoseBin means depend only on the member lists: they run on the side stream, beside the
-  // affine verification, and the main stream joins them at the next entry point (set_dev)
+  // affine verification and the next step's matcher tail (their inputs are double-buffered);
+  // entry points that read results join them (set_dev)
   // 1/(n+1) for every n a member list of this capacity can reach: built once per capacity
   // (a bin's chain reads entry n for its member n)
   const bool new_rtab = ctx->rtab.n < (size_t)ctx->mmax;
@@ -1186,12 +1231,14 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
     SOD_HIP(ctx, hipGetLastError());
   }
   // one wave per bin, each a serial f64 chain: as many chains in flight as LDS allows
-  // (7 KiB per wave: 16 per CU)
-  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->tail_cus() * 16)), dim3(64), 0, ctx->side,
+  // (14 KiB per wave: 11 per CU)
+  hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->tail_cus() * 11)), dim3(64), 0, ctx->side,
                      ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->pose.p,
-                     ctx->idx1.p + sod_win0(ctx), ctx->mimg.p, ctx->isize.p, ctx->rtab.p,
-                     ctx->means.p);
+                     reinterpret_cast<const int2*>(ctx->msize.p), ctx->rtab.p, ctx->means.p);
   SOD_HIP(ctx, hipGetLastError());
+  ++ctx->means_id;
+  SOD_TRY(mark_read(ctx, ctx->side, ctx->hpar, ctx->ev_hread, ctx->hread_id));
+  SOD_TRY(mark_read(ctx, ctx->side, ctx->spar, ctx->ev_sread, ctx->sread_id));
   SOD_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
   ctx->side_pending = true;
   return SOD_OK;

@@ -33,6 +33,8 @@
 #include <climits>
 #include <cstdlib>
 
+#include <hip/hip_ext.h>
+
 #include "sod_internal.h"
 
 typedef __attribute__((ext_vector_type(4))) int i32x4;
@@ -1098,26 +1100,26 @@ int launch_match_i8(sod_ctx* ctx) {
     }
     gthr = ctx->gthr.p + ctx->pslot * nq_pad;
   }
-  SOD_TRY(sod_match_mark(ctx, ks, 0));
+  hipEvent_t eb, ee;
+  SOD_TRY(sod_match_events(ctx, &eb, &ee));
   if (wide)
-    hipLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0,
-                       ks, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
-                       ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt,
-                       nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, pd1,
-                       pidx, pd2, (int)qblocks);
+    hipExtLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0,
+                          ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
+                          ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),
+                          ctx->nqt, nq_pad, (int)split, st_per_split * sps,
+                          (int)ctx->row_offset, pd1, pidx, pd2, (int)qblocks);
   else {
 #define SOD_LAUNCH_I8(Q)                                                                      \
-  hipLaunchKernelGGL(match_i8_kernel<Q>, dim3((unsigned)(qblocks * split)), dim3(NT16), 0, ks,  \
-                     ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p), ctx->nsub,        \
-                     ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt, nq_pad,  \
-                     (int)split, st_per_split * sps, (int)ctx->row_offset, pd1, pidx, pd2,     \
-                     (int)qblocks, gthr)
+  hipExtLaunchKernelGGL(match_i8_kernel<Q>, dim3((unsigned)(qblocks * split)), dim3(NT16), 0,   \
+                        ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),  \
+                        ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),       \
+                        ctx->nqt, nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, \
+                        pd1, pidx, pd2, (int)qblocks, gthr)
     if (qt == 8) SOD_LAUNCH_I8(8); else if (qt == 4) SOD_LAUNCH_I8(4); else SOD_LAUNCH_I8(2);
 #undef SOD_LAUNCH_I8
   }
   SOD_HIP(ctx, hipGetLastError());
-  SOD_TRY(sod_match_mark(ctx, ks, 1));
-  SOD_TRY(sod_match_stream_end(ctx));
+  SOD_TRY(sod_match_stream_end(ctx, ee));
   SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, gthr,
                        ctx->nranks <= 1 && !ctx->comm));   // no exchange follows: final
   return sod_partials_merged(ctx);   // the slot is free again

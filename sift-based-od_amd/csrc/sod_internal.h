@@ -105,6 +105,8 @@ struct sod_ctx {
   DevBuf<uint32_t> basekey;     // [nq] ix | iy<<8 | it<<16 | is<<24
   DevBuf<uint32_t> vmask;       // [nq] 16-bit vote mask (0 = no vote)
   DevBuf<double> pose;          // [nq*4]
+  DevBuf<double> pose_b;        // the other step parity of pose / msize
+  DevBuf<int32_t> msize_b;
   bool houghed = false;
 
   // ---- select / CSR / means ----
@@ -115,8 +117,13 @@ struct sod_ctx {
   DevBuf<int64_t> voff;         // [vmax+1]
   DevBuf<int32_t> members;      // [mmax] query index
   DevBuf<double> means;         // [vmax*6]
+  DevBuf<uint32_t> scal_b;      // the other step parity of scal / voff / members / means
+  DevBuf<int64_t> voff_b;
+  DevBuf<int32_t> members_b;
+  DevBuf<double> means_b;
   DevBuf<uint32_t> vidx;        // [nbins] bin -> valid index (0xFFFFFFFF otherwise)
   DevBuf<uint32_t> cursor;      // [vmax] member fill cursors
+  DevBuf<int32_t> msize;        // [nq][2] model image (w, h) of a voting query's match
   DevBuf<double> rtab;          // [mmax] 1/(n+1) for the running means
   DevBuf<uint32_t> allbin;      // [bmax] all occupied bins, first-touch order
   int64_t vmax = 0, mmax = 0;
@@ -158,12 +165,23 @@ struct sod_ctx {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool side_pending = false;    // main stream has not yet waited for the side work
+  // per-step buffer sets read by the PoseBin means on the side stream (pose, msize: Hough;
+  // scal, voff, members, means: select) are double-buffered, so the next step's kernels
+  // overwrite the other set instead of waiting for the means; a set is reused only after
+  // the means that read it (ev_hread / ev_sread of that parity) has finished
+  int hpar = 0, spar = 0;
+  hipEvent_t ev_hread[2] = {nullptr, nullptr}, ev_sread[2] = {nullptr, nullptr};
+  // id of the means launch that last read a set (0 = none) and the newest id the main
+  // stream has already waited for: one wait covers both sets of a step
+  uint64_t hread_id[2] = {0, 0}, sread_id[2] = {0, 0}, means_id = 0, means_waited = 0;
 
   // ---- matcher stream (sod_match_set_overlap): the match kernel runs there and waits only
   // for the last input upload (ev_inputs) and for the merge that last read its partial-result
   // slot (two slots alternate: ev_merged[slot])
   hipStream_t mstream = nullptr;
   hipEvent_t ev_inputs = nullptr, ev_matched = nullptr, ev_merged[2] = {nullptr, nullptr};
+  hipEvent_t ev_matched_p = nullptr;   // the last matcher launch's completion event
+  bool stage_timing = true;   // sod_set_stage_timing: ev[2..5] around the tail stages
   bool overlap = false;
   // sod_set_cu_reserve: the top `reserved_cus` CU-mask bits (cu_reserve per XCD, mask bit i
   // is on XCD i % 8) run the context / side streams; the matcher stream gets the rest
@@ -251,7 +269,8 @@ int sod_inputs_end(sod_ctx* ctx);
 int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end);
 int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1, int32_t** idx,
                            float** d2);
-int sod_match_stream_end(sod_ctx* ctx);
+int sod_match_stream_end(sod_ctx* ctx, hipEvent_t done = nullptr);
+int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end);
 int sod_partials_merged(sod_ctx* ctx);
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2,
                  int nparts, int64_t stride, int32_t* reset = nullptr, bool final_merge = false);
