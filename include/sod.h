@@ -125,7 +125,9 @@ int sod_match_set_impl(sod_ctx* ctx, int impl);
  * matcher kernel of the next sod_match_enqueue / sod_pipeline_enqueue only waits for the
  * previous merge of its partial results (and for the last descriptor upload), so it overlaps
  * the previous query's Hough / select / affine stages, which stay on the context stream in
- * order (RCCL collectives included).  Results are unchanged. */
+ * order (RCCL collectives included).  The host thread waits inside the enqueue until
+ * that merge (two launches back) is done, so at most two matcher launches per context are
+ * in flight.  Results are unchanged. */
 int sod_match_set_overlap(sod_ctx* ctx, int on);
 /* Split the CUs: the matcher stream keeps all but `per_xcd` CUs of every XCD, the context
  * and side streams (Hough / select / affine, merges, RCCL collectives, memsets) run on those
