@@ -58,8 +58,12 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)   # steady state: the last query's tail is 1/K of a step
-    p.add_argument("--warmup", type=int, default=10)   # the clock settles over ~10 launches
+    # defaults per config: ~100 ms of warmup (the clock ramps over the first ~60 ms of
+    # back-to-back launches: C2 0.163 ms per step after 10 warmup steps, 0.142 after 500;
+    # C3 equal after 10 or 40) and a timed region of >= 30 ms (the last query's tail is 1/K
+    # of a step)
+    p.add_argument("--steps", type=int, default=None, help="default 50 (C2: 200)")
+    p.add_argument("--warmup", type=int, default=None, help="default 10 (C2: 500)")
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true",
@@ -86,6 +90,11 @@ def parse():
                    help="multi-rank exchange: RCCL on the device (default) or staged "
                         "through host memory over gloo (for >1 rank per GPU)")
     a = p.parse_args()
+    short = a.config in ("c2", "tiny")
+    if a.steps is None:
+        a.steps = 200 if short else 50
+    if a.warmup is None:
+        a.warmup = 500 if short else 10
     if a.overlap == 0 and a.cu_reserve > 0:
         p.error("--cu-reserve > 0 runs the matcher on a stream of its own: it needs --overlap 1")
     return a

@@ -332,21 +332,26 @@ def test_shared_db_write_rules():
     c3.close()
 
 
-@pytest.mark.parametrize("use_comm,reserve", [(False, 0), (True, 0), (False, 1), (True, 1)])
-def test_matcher_overlap_equals_serial(use_comm, reserve):
+@pytest.mark.parametrize("use_comm,reserve,affine", [(False, 0, True), (True, 0, True),
+                                                     (False, 1, True), (True, 1, True),
+                                                     (False, 1, False)])
+def test_matcher_overlap_equals_serial(use_comm, reserve, affine):
     """sod_match_set_overlap: the matcher kernel on its own stream, overlapping the previous
-    query's Hough / select / affine stages (several pipelines enqueued back to back, a new
-    query upload in between, optionally a 1-rank RCCL communicator on the context stream);
-    with `reserve` the chip is split by CU masks (sod_set_cu_reserve: matcher on all but one
-    CU per XCD, the other stages on those) -- every result equals the serial context's bit
-    for bit."""
+    query's Hough / select / affine stages (several pipelines enqueued back to back with
+    different vote thresholds -- so consecutive steps have different valid-bin and member
+    counts while the PoseBin means of the step before still run on the side stream over
+    their double-buffered inputs -- a new query upload in between, optionally a 1-rank RCCL
+    communicator on the context stream); with `reserve` the chip is split by CU masks
+    (sod_set_cu_reserve: matcher on all but one CU per XCD, the other stages on those) --
+    every result equals the serial context's bit for bit."""
     db = synthetic.make_database(30, 1000, seed=51)
     qsets = [synthetic.make_queries(5000, seed=52 + k, db_seed=51, kp_per_image=1000)
              for k in range(2)]
     bins = (32, 32, 8, 12)
 
     def collect(c):
-        return (c.match_result(), c.valid_result(), c.affine_result(), c.all_bins())
+        return (c.match_result(), c.valid_result(), c.affine_result() if affine else None,
+                c.all_bins())
 
     ref = []
     with _lib.Context(0) as c:
@@ -354,7 +359,7 @@ def test_matcher_overlap_equals_serial(use_comm, reserve):
         c.upload_db(db.des)
         for qs in qsets:
             c.upload_queries(qs.des, qs.kp)
-            c.pipeline(qs.shape, bins)
+            c.pipeline(qs.shape, bins, run_affine=affine)
             ref.append(collect(c))
     with _lib.Context(0) as c:
         if reserve:
@@ -368,8 +373,8 @@ def test_matcher_overlap_equals_serial(use_comm, reserve):
         got = []
         for qs in qsets:
             c.upload_queries(qs.des, qs.kp)
-            for _ in range(3):                  # back to back: matcher k+1 beside tail k
-                c.pipeline(qs.shape, bins)
+            for thr in (3, 8, 5):               # back to back: matcher k+1 beside tail k
+                c.pipeline(qs.shape, bins, vote_threshold=thr, run_affine=affine)
             c.synchronize()
             got.append(collect(c))
         times = c.match_times(3)                # the last three launches, timed live
@@ -385,8 +390,9 @@ def test_matcher_overlap_equals_serial(use_comm, reserve):
         for k in ("keys", "votes", "offsets", "members", "means"):
             assert np.array_equal(v0[k], v1[k]), k
         assert np.array_equal(b0[0], b1[0]) and np.array_equal(b0[1], b1[1])
-        assert np.array_equal(a0["survived"], a1["survived"])
-        assert np.array_equal(a0["params"], a1["params"])
+        if affine:
+            assert np.array_equal(a0["survived"], a1["survived"])
+            assert np.array_equal(a0["params"], a1["params"])
 
 
 def test_cu_reserve_channel_cap(monkeypatch):
