@@ -241,6 +241,9 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_LAZYP
 #define SOD_I8_LAZYP 1     // parity words read from LDS on the slow path only
 #endif
+#ifndef SOD_I8_SEED
+#define SOD_I8_SEED 1      // seed pass over a chunk's first stage instead of the dense phase
+#endif
 #ifndef SOD_I8_DENSE
 #define SOD_I8_DENSE 32    // leading subtiles of a chunk updated without threshold exchange (C2: +8 %)
 #endif
@@ -572,6 +575,40 @@ __device__ __forceinline__ void match_unit(
 #endif
     const uint8_t* sb = lds + slot * kStageBytes;
     const uint8_t* nb0 = nring + (s % kNormRing) * kStageNorm + norm_off(0, lane >> 4);
+#if SOD_I8_SEED
+    if (s == 0) {
+      // Seed pass: the chunk's first stage through the MFMAs once with no top-2 work, only a
+      // running max of each lane's values per tile (the lane's 4 rows per subtile, one query).
+      // The second largest of a query's 4 lane-group maxima comes from two distinct rows of
+      // this chunk, so the query's final second best is >= it: a valid prefilter threshold
+      // (and a valid shared bound) from the first subtile on.  The stage is then processed
+      // normally, its rows below the seed skipped, instead of every tile of its 32 subtiles
+      // taking the exact update (the dense phase).
+      int sm[QT];
+#pragma unroll
+      for (int t = 0; t < QT; ++t) sm[t] = INT_MIN;
+#pragma unroll 1
+      for (int u = 0; u < SPS; ++u) {
+        const uint8_t* nb = sb + u * kSub + lane * 16;
+        const i32x4 a0 = *reinterpret_cast<const i32x4*>(nb);
+        const i32x4 a1 = *reinterpret_cast<const i32x4*>(nb + 1024);
+        const i32x4 c = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u, 0));
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq[t][0], c, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq[t][1], acc, 0, 0, 0);
+          sm[t] = max(sm[t], max(max(acc[0], acc[1]), max(acc[2], acc[3])));
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        int g1 = sm[t], g2 = INT_MIN;
+        top2_xor32(g1, g2);
+        top2_xor16(g1, g2);
+        t2[t] = max(t2[t], g2);
+      }
+    }
+#endif
     slot = slot + 1 == kRing ? 0 : slot + 1;
     i32x4 fa0 = *reinterpret_cast<const i32x4*>(sb + lane * 16);
     i32x4 fa1 = *reinterpret_cast<const i32x4*>(sb + 1024 + lane * 16);
@@ -629,7 +666,7 @@ __device__ __forceinline__ void match_unit(
       {
         // the pending subtile's index in the chunk decides dense / final / prefilter
         const int64_t kp = s * SPS + u - 1;
-        const int mode = kp < kDense - 1 ? 1 : (kp == kDense - 1 ? 2 : 0);
+        const int mode = SOD_I8_SEED ? 0 : (kp < kDense - 1 ? 1 : (kp == kDense - 1 ? 2 : 0));
         tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
       }
 #pragma unroll
@@ -672,7 +709,8 @@ __device__ __forceinline__ void match_unit(
   // threshold load) must land before the work-group's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if SOD_I8_PIPE
-  tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, false, nst * SPS <= kDense ? 1 : 0);
+  tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, false,
+                  !SOD_I8_SEED && nst * SPS <= kDense ? 1 : 0);
 #endif
 #ifdef SOD_I8_COUNT
   if (lane == 0) atomicAdd(&g_counts[2], (unsigned long long)(nst * SPS));
