@@ -244,6 +244,12 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_SEED
 #define SOD_I8_SEED 1      // seed pass over a chunk's first stage instead of the dense phase
 #endif
+#ifndef SOD_I8_SEEDPUB
+#define SOD_I8_SEEDPUB 1   // publish the seed thresholds to the other chunks right away
+#endif
+#ifndef SOD_I8_SEEDLOAD
+#define SOD_I8_SEEDLOAD 1  // then read the other chunks' seeds before the stage's main pass
+#endif
 #ifndef SOD_I8_DENSE
 #define SOD_I8_DENSE 32    // leading subtiles of a chunk updated without threshold exchange (C2: +8 %)
 #endif
@@ -469,7 +475,7 @@ __device__ __forceinline__ void match_unit(
     uint8_t* lds, int sp, int qb, const uint8_t* __restrict__ dbpack, const int* __restrict__ dn,
     int64_t nsub, const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt,
     int64_t nq_pad, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
-    int* __restrict__ pidx, float* __restrict__ pd2, int* __restrict__ gthr) {
+    int* __restrict__ pidx, float* __restrict__ pd2, int* __restrict__ gthr, int seedload) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qt0 = (qb * NW16 + wave) * QT;
 #ifdef SOD_I8_TIME
@@ -606,7 +612,33 @@ __device__ __forceinline__ void match_unit(
         top2_xor32(g1, g2);
         top2_xor16(g1, g2);
         t2[t] = max(t2[t], g2);
+#if SOD_I8_XCHUNK && SOD_I8_SEEDPUB
+        // out to the chunks of the same queries now: their first threshold load (this
+        // stage's share_load) then already sees the other chunks' seeds
+        if (lane < 16 && t < ntile)
+          __hip_atomic_fetch_max(gw + 16 * t + lane, t2[t], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+#endif
       }
+#if SOD_I8_XCHUNK && SOD_I8_SEEDPUB && SOD_I8_SEEDLOAD
+      // the chunks of a query block run their seed passes side by side: one round trip
+      // now gives the stage's main pass the max of the seeds published so far.  The wait
+      // also covers the next stage's prefetch (loads return in order), which costs more
+      // than it saves when the DB stream dominates (many chunks of few queries: 500 x 1M,
+      // 124 chunks, 0.078 vs 0.070 ms), so the launch enables it up to 64 chunks only, and
+      // the one-image kernel (QT 2) does not carry the code (its mere presence cost 2-3 %)
+      if (QT >= 4 && seedload) {
+        int gq[QT];
+#pragma unroll
+        for (int t = 0; t < QT; ++t)   // one load per query (lanes 0-15), then to its groups
+          gq[t] = lane < 16 && t < ntile
+                      ? __hip_atomic_load(gw + 16 * t + lane, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT)
+                      : INT_MIN;
+#pragma unroll
+        for (int t = 0; t < QT; ++t) t2[t] = max(t2[t], __shfl(gq[t], lane & 15));
+      }
+#endif
     }
 #endif
     slot = slot + 1 == kRing ? 0 : slot + 1;
@@ -750,7 +782,8 @@ __global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
-    int* __restrict__ pidx, float* __restrict__ pd2, int nqb, int* __restrict__ gthr) {
+    int* __restrict__ pidx, float* __restrict__ pd2, int nqb, int* __restrict__ gthr,
+    int seedload) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageBytes + kNormRing * kStageNorm +
                                                      SOD_I8_XCHUNK * NW16 * QT * 64];
 #ifdef SOD_I8_STAMP
@@ -767,10 +800,10 @@ __global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
   const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = blockIdx.x % 8;
   const unsigned u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blockIdx.x / 8;
   match_unit<QT>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
-             sub_per_split, row_offset, pd1, pidx, pd2, gthr);
+             sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
 #else
   match_unit<QT>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
-             nq_pad, sub_per_split, row_offset, pd1, pidx, pd2, gthr);
+             nq_pad, sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
 #endif
 #ifdef SOD_I8_STAMP
   if (threadIdx.x == 0 && blockIdx.x < 4096) {
@@ -1138,6 +1171,7 @@ int launch_match_i8(sod_ctx* ctx) {
     }
     gthr = ctx->gthr.p + ctx->pslot * nq_pad;
   }
+  const int seedload = split <= 64 ? 1 : 0;   // see match_unit (SOD_I8_SEEDLOAD)
   hipEvent_t eb, ee;
   SOD_TRY(sod_match_events(ctx, &eb, &ee));
   if (wide)
@@ -1152,7 +1186,7 @@ int launch_match_i8(sod_ctx* ctx) {
                         ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),  \
                         ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),       \
                         ctx->nqt, nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, \
-                        pd1, pidx, pd2, (int)qblocks, gthr)
+                        pd1, pidx, pd2, (int)qblocks, gthr, seedload)
     if (qt == 8) SOD_LAUNCH_I8(8); else if (qt == 4) SOD_LAUNCH_I8(4); else SOD_LAUNCH_I8(2);
 #undef SOD_LAUNCH_I8
   }
