@@ -244,6 +244,9 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_SEED
 #define SOD_I8_SEED 1      // seed pass over a chunk's first stage instead of the dense phase
 #endif
+#ifndef SOD_I8_SEEDSUB
+#define SOD_I8_SEEDSUB SPS // subtiles of the first stage the seed pass covers
+#endif
 #ifndef SOD_I8_SEEDPUB
 #define SOD_I8_SEEDPUB 1   // publish the seed thresholds to the other chunks right away
 #endif
@@ -594,7 +597,7 @@ __device__ __forceinline__ void match_unit(
 #pragma unroll
       for (int t = 0; t < QT; ++t) sm[t] = INT_MIN;
 #pragma unroll 1
-      for (int u = 0; u < SPS; ++u) {
+      for (int u = 0; u < SOD_I8_SEEDSUB; ++u) {
         const uint8_t* nb = sb + u * kSub + lane * 16;
         const i32x4 a0 = *reinterpret_cast<const i32x4*>(nb);
         const i32x4 a1 = *reinterpret_cast<const i32x4*>(nb + 1024);
