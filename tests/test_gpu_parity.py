@@ -78,7 +78,8 @@ def test_matcher_query_tiles_shared_thresholds(ctx, monkeypatch, qt):
     """int8 matcher with each query-tile count per wave (SOD_MATCH_QT) over a DB split into
     many chunks, so the chunks exchange prefilter thresholds mid-run: DB rows duplicated far
     apart (other chunks) make exact distance ties ACROSS chunks -- a shared threshold must
-    keep them (lowest trainIdx wins), and queries equal to a DB row (d1 = 0) or near one."""
+    keep them (lowest trainIdx wins), and queries equal to a DB row (d1 = 0) or near one,
+    including runs of equal rows inside a chunk's seed stage."""
     monkeypatch.setenv("SOD_MATCH_QT", qt)
     rng = np.random.default_rng(31)
     ndb, nq = 150000, 2000
@@ -88,6 +89,12 @@ def test_matcher_query_tiles_shared_thresholds(ctx, monkeypatch, qt):
     q = synthetic.sift_like_descriptors(rng, nq)
     q[:600] = np.clip(db[:600].astype(int) + rng.integers(-2, 3, (600, 128)), 0, 255)
     q[600:900] = db[50000:50300]                       # d1 = d2 = 0, two equal rows
+    # equal rows inside a chunk's first stage (where the seed pass takes its bound) and
+    # mid-DB: the seed equals both winners' value, which must still pass (>=)
+    db[1:8] = db[0]
+    db[75001:75005] = db[75000]
+    q[900:950] = db[0]
+    q[950:1000] = db[75000]
     ctx.set_impl("i8")
     ctx.upload_db(db)
     ctx.upload_queries(q)
