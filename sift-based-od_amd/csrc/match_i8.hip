@@ -276,7 +276,10 @@ __device__ __forceinline__ constexpr bool share_apply(int u) { return u == 20 ||
 #define SOD_I8_XEVERY 4
 #endif
 constexpr int64_t kPublishDense = 4, kPublishEvery = SOD_I8_PUB_EVERY;
-constexpr int64_t kXDense = 4, kXEvery = SOD_I8_XEVERY;
+#ifndef SOD_I8_XDENSE
+#define SOD_I8_XDENSE 8    // leading stages that exchange thresholds every stage (4: C2 +1.8 %)
+#endif
+constexpr int64_t kXDense = SOD_I8_XDENSE, kXEvery = SOD_I8_XEVERY;
 __device__ __forceinline__ constexpr bool share_load(int u) { return u == 8; }
 __device__ __forceinline__ constexpr bool share_apply(int u) { return u == 24; }
 #endif
