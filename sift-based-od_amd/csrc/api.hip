@@ -351,7 +351,8 @@ int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n) {
   const bool st = ctx->stage_timing;
   const bool rec[6] = {ctx->matched, ctx->matched, st && ctx->houghed, st && ctx->houghed,
                        st && ctx->selected, st && ctx->affined};
-  // the last matcher launch's begin / end events (sod_match_mark) bound stages 0 and 1
+  // the last matcher launch's begin / end events (sod_match_events, or sod_match_mark on
+  // the bf16 path) bound stages 0 and 1
   hipEvent_t evs[6];
   for (int i = 0; i < 6; ++i) evs[i] = ctx->ev[i];
   if (ctx->nmatch > 0) {
