@@ -280,8 +280,12 @@ constexpr int64_t kPublishDense = 4, kPublishEvery = SOD_I8_PUB_EVERY;
 #define SOD_I8_XDENSE 8    // leading stages that exchange thresholds every stage (4: C2 +1.8 %)
 #endif
 constexpr int64_t kXDense = SOD_I8_XDENSE, kXEvery = SOD_I8_XEVERY;
-__device__ __forceinline__ constexpr bool share_load(int u) { return u == 8; }
-__device__ __forceinline__ constexpr bool share_apply(int u) { return u == 24; }
+#ifndef SOD_I8_SHARE_AT
+#define SOD_I8_SHARE_AT 4, 20   // subtile of the threshold load, of its application (8, 24: C3 +0.2 %)
+#endif
+constexpr int kShareAt[2] = {SOD_I8_SHARE_AT};
+__device__ __forceinline__ constexpr bool share_load(int u) { return u == kShareAt[0]; }
+__device__ __forceinline__ constexpr bool share_apply(int u) { return u == kShareAt[1]; }
 #endif
 #ifndef SOD_SHARED_T
 #define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
