@@ -375,12 +375,8 @@ def main():
         overlap = 1                 # the split runs the matcher on its own stream
     comm = None
     if world > 1 and a.comm == "rccl":
-        # created under the split: sod_comm_init caps NCCL_MAX_NCHANNELS at the reserved CU
-        # count (8 * reserve), so every block of an RCCL kernel is resident at once; set here
-        # too, before the first RCCL call of the process (ncclGetUniqueId), in case RCCL
-        # reads its parameters once at library init
-        if reserve:
-            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(8 * reserve))
+        # created under the split: sod_comm_init gives the communicator maxCTAs = the
+        # reserved CU count (8 * reserve), so every block of an RCCL kernel is resident at once
         comm = RcclComm(ctx, world, rank, D.bcast_bytes)
     elif world > 1:
         comm = TorchHostComm()

@@ -138,9 +138,9 @@ int sod_match_set_overlap(sod_ctx* ctx, int on);
  * Results are unchanged.  (No reference counterpart: an MI355X scheduling knob.)
  * SOD_EINVAL on a device other than a whole MI355X (gfx950, 8 XCDs, 256 CUs: the CU-mask
  * layout it relies on was measured there).  With an RCCL communicator every block of a
- * collective must fit the reserved CUs: sod_comm_init under an active split caps
- * NCCL_MAX_NCHANNELS at the reserved CU count (sets it if unset, SOD_ESTATE if larger),
- * and this call fails with SOD_ESTATE on a communicator created without such a cap. */
+ * collective must fit the reserved CUs: sod_comm_init under an active split creates the
+ * communicator with ncclConfig_t.maxCTAs = the reserved CU count, and this call fails with
+ * SOD_ESTATE on a communicator created with more (or RCCL's default) blocks per collective. */
 int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd);
 /* multi-GPU: RCCL all-gather of every rank's per-query (d1^2, idx1, d2^2) and the
  * global merge.  No-op on a single rank. */

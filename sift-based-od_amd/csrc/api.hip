@@ -189,14 +189,6 @@ static int db_writable(sod_ctx* ctx) {
   return SOD_OK;
 }
 
-// NCCL_MAX_NCHANNELS as RCCL will read it at communicator creation (0 = unset / default)
-static int env_max_channels() {
-  const char* e = std::getenv("NCCL_MAX_NCHANNELS");
-  if (!e || !*e) return 0;
-  const long v = std::strtol(e, nullptr, 10);
-  return v > 0 && v < (1 << 20) ? (int)v : 0;
-}
-
 extern "C" {
 
 int sod_abi_version(void) { return 1; }
@@ -271,7 +263,7 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->d1); sod_release(ctx->d2); sod_release(ctx->idx1); sod_release(ctx->good);
   sod_release(ctx->flags); sod_release(ctx->sig_lut); sod_release(ctx->counts);
   sod_release(ctx->first); sod_release(ctx->basekey); sod_release(ctx->vmask);
-  sod_release(ctx->pose); sod_release(ctx->selstat); sod_release(ctx->scal); sod_release(ctx->vbin);
+  sod_release(ctx->pose); sod_release(ctx->selstat); sod_release(ctx->selticket); sod_release(ctx->scal); sod_release(ctx->vbin);
   sod_release(ctx->voff); sod_release(ctx->members); sod_release(ctx->means);
   sod_release(ctx->vidx); sod_release(ctx->cursor);
   sod_release(ctx->rtab); sod_release(ctx->msize);
@@ -659,7 +651,7 @@ int sod_valid_images_get(sod_ctx* ctx, int32_t* image) {
 int sod_match_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
-  ctx->ratio_fused = -1.0;   // set again by a final merge that applies the pipeline's ratio
+  ctx->ratio_fused_valid = false;   // set again by a final merge that applies the pipeline's ratio
   SOD_TRY(ctx->impl != 0 ? launch_match_i8(ctx) : launch_match(ctx));
   ctx->matched = true;
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
@@ -675,6 +667,7 @@ int sod_match_set_overlap(sod_ctx* ctx, int on) {
   if (!on && ctx->cu_reserve)
     return sod_fail(ctx, SOD_ESTATE, "the CU split (sod_set_cu_reserve) needs the matcher stream");
   ctx->overlap = on != 0;
+  ctx->gthr_n = 0;   // the next int8 launch re-initialises both threshold slots
   return SOD_OK;
 }
 
@@ -709,17 +702,16 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
     if (per_xcd * nx * 2 > ctx->num_cus)
       return sod_fail(ctx, SOD_EINVAL, "cu reserve per XCD must be in [0, CUs per XCD / 2]");
     // a collective whose blocks do not all fit the reserved CUs could wait on a block that
-    // never gets a CU: the communicator must have been created with at most that many
-    // channels
+    // never gets a CU: the communicator must have been created (sod_comm_init under a split)
+    // with at most that many blocks per collective
     if (ctx->comm && (ctx->comm_max_channels == 0 || ctx->comm_max_channels > per_xcd * nx))
       return sod_fail(ctx, SOD_ESTATE,
                       "the RCCL communicator was created with " +
                           (ctx->comm_max_channels ? "up to " + std::to_string(ctx->comm_max_channels)
                                                   : std::string("the default number of")) +
-                          " channels; the CU split runs collectives on " +
+                          " blocks per collective (maxCTAs); the CU split runs collectives on " +
                           std::to_string(per_xcd * nx) +
-                          " CUs: set NCCL_MAX_NCHANNELS <= that before sod_comm_init, or call "
-                          "sod_set_cu_reserve first");
+                          " CUs: call sod_set_cu_reserve before sod_comm_init");
   }
   SOD_HIP(ctx, hipStreamSynchronize(ctx->side));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
@@ -750,6 +742,7 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
   ctx->cu_reserve = per_xcd;
   ctx->reserved_cus = r;
   if (per_xcd > 0) ctx->overlap = true;
+  ctx->gthr_n = 0;   // the next int8 launch re-initialises both threshold slots
   return SOD_OK;
 }
 
@@ -793,7 +786,10 @@ int sod_match_allgather_enqueue(sod_ctx* ctx) {
 int sod_ratio_enqueue(sod_ctx* ctx, double ratio) {
   SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
-  if (ctx->ratio_fused != ratio) SOD_TRY(launch_ratio(ctx, ratio));   // else the merge did it
+  if (!(ratio >= 0.0) || !std::isfinite(ratio))
+    return sod_fail(ctx, SOD_EINVAL, "ratio must be a finite number >= 0");
+  // skipped only when the final merge of this very launch applied this very ratio
+  if (!ctx->ratio_fused_valid || ctx->ratio_fused != ratio) SOD_TRY(launch_ratio(ctx, ratio));
   ctx->ratio_done = true;
   return SOD_OK;
 }
@@ -824,7 +820,7 @@ int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t
   SOD_HIP(ctx, hipMemsetAsync(ctx->d1.p, 0, (size_t)nq * 4, ctx->stream));
   SOD_HIP(ctx, hipMemsetAsync(ctx->d2.p, 0, (size_t)nq * 4, ctx->stream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  ctx->ratio_fused = -1.0;
+  ctx->ratio_fused_valid = false;
   ctx->matched = ctx->ratio_done = true;
   ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
@@ -999,7 +995,9 @@ int sod_affine_get(sod_ctx* ctx, uint8_t* survived, int32_t* votes, double* para
 int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* a) {
   SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!a) return sod_fail(ctx, SOD_EINVAL, "null args");
-  ctx->fuse_ratio = a->ratio >= 0.0 ? a->ratio : -1.0;   // the final merge applies it too
+  if (!(a->ratio >= 0.0) || !std::isfinite(a->ratio))
+    return sod_fail(ctx, SOD_EINVAL, "ratio must be a finite number >= 0");
+  ctx->fuse_ratio = a->ratio;   // the final merge applies it too
   int rc = sod_match_enqueue(ctx);
   if (rc == SOD_OK) rc = sod_match_allgather_enqueue(ctx);
   ctx->fuse_ratio = -1.0;
@@ -1195,26 +1193,23 @@ int sod_comm_init(sod_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[S
   ctx->nranks = nranks;
   ctx->rank = rank;
   // nranks == 1 also builds a communicator: the collectives then run (as copies), which is
-  // how the RCCL path is exercised on a one-GPU machine
-  int cap = env_max_channels();
-  if (ctx->reserved_cus > 0) {   // collectives will run on the reserved CUs only
-    if (cap == 0) {
-      // RCCL reads the variable when the communicator is created
-      setenv("NCCL_MAX_NCHANNELS", std::to_string(ctx->reserved_cus).c_str(), 1);
-      cap = ctx->reserved_cus;
-    } else if (cap > ctx->reserved_cus) {
-      return sod_fail(ctx, SOD_ESTATE,
-                      "NCCL_MAX_NCHANNELS=" + std::to_string(cap) + " exceeds the " +
-                          std::to_string(ctx->reserved_cus) +
-                          " CUs reserved by sod_set_cu_reserve for the collectives");
-    }
+  // how the RCCL path is exercised on a one-GPU machine.  Under a CU split the collectives
+  // run on the reserved CUs only, so the communicator is created with at most that many
+  // blocks per collective (ncclConfig_t.maxCTAs: a per-communicator setting, unlike the
+  // NCCL_MAX_NCHANNELS environment variable, which RCCL reads once per process)
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  int cap = 0;
+  if (ctx->reserved_cus > 0) {
+    cap = ctx->reserved_cus;
+    cfg.minCTAs = 1;
+    cfg.maxCTAs = cap;
   }
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
-  const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
+  const ncclResult_t r = ncclCommInitRankConfig(&ctx->comm, nranks, uid, rank, &cfg);
   if (r != ncclSuccess) {
     ctx->comm = nullptr;
-    return sod_fail(ctx, SOD_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    return sod_fail(ctx, SOD_ECOMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
   }
   ctx->comm_max_channels = cap;
   return SOD_OK;

@@ -367,16 +367,24 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
 // preceding blocks' published words until one carries an inclusive prefix.  A status word is
 // (epoch * 4 + flag) << 32 | value, flag 1 = aggregate, 2 = inclusive prefix; a word of an
 // older call (other epoch) reads as "not yet published", so the array needs no reset.
-// Blocks are dispatched in blockIdx order, so every block waited on is resident or done.
+// A block's position in the scan is a ticket drawn from a device counter when it starts
+// (HIP does not promise dispatch in blockIdx order, and the stream may be CU-masked beside
+// a full-chip matcher): every block waited on has already started, so it is resident or
+// done.  The counter is never reset: the host passes the number of tickets drawn by earlier
+// launches (stream order: they have all drawn theirs).
 __global__ __launch_bounds__(kSelThreads) void select_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
     const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b,
     const int* __restrict__ qimg, int64_t nbins1, uint32_t thr, uint64_t* __restrict__ status,
-    uint32_t epoch, uint32_t* __restrict__ out, uint32_t* __restrict__ vidx,
-    uint32_t* __restrict__ total) {
+    uint32_t epoch, unsigned long long* __restrict__ ticket, unsigned long long ticket_base,
+    uint32_t* __restrict__ out, uint32_t* __restrict__ vidx, uint32_t* __restrict__ total) {
   __shared__ uint32_t sh[kSelThreads / 64];
   __shared__ uint32_t excl_s;
-  const int64_t q = (int64_t)blockIdx.x * kSelThreads + threadIdx.x;
+  __shared__ int blk_s;
+  if (threadIdx.x == 0) blk_s = (int)(atomicAdd(ticket, 1ULL) - ticket_base);
+  __syncthreads();
+  const int blk = blk_s;
+  const int64_t q = (int64_t)blk * kSelThreads + threadIdx.x;
   uint32_t tmp[16];
   const uint32_t qb = (qimg && q < nq) ? (uint32_t)(qimg[q] * nbins1) : 0u;
   const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, qb, thr, tmp) : 0;
@@ -384,7 +392,6 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(
   const uint32_t loc = block_excl_scan(n, sh, &tot);
   if (threadIdx.x == 0) {
     const uint64_t e4 = (uint64_t)(epoch << 2);
-    const int blk = (int)blockIdx.x;
     uint32_t ex = 0;
     if (blk > 0) {
       __hip_atomic_store(&status[blk], ((e4 | 1u) << 32) | tot, __ATOMIC_RELEASE,
@@ -1164,11 +1171,18 @@ static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* t
     SOD_TRY(sod_reserve(ctx, ctx->selstat, (size_t)nblk));
     SOD_HIP(ctx, hipMemsetAsync(ctx->selstat.p, 0, ctx->selstat.n * 8, ctx->stream));
   }
+  if (!ctx->selticket.p) {   // block tickets: a counter that is never reset
+    SOD_TRY(sod_reserve(ctx, ctx->selticket, 1));
+    SOD_HIP(ctx, hipMemsetAsync(ctx->selticket.p, 0, 8, ctx->stream));
+    ctx->sel_tickets = 0;
+  }
   ctx->sel_epoch = ctx->sel_epoch >= (1u << 30) - 1 ? 1u : ctx->sel_epoch + 1;
   hipLaunchKernelGGL(select_kernel, dim3((unsigned)nblk), dim3(kSelThreads), 0, ctx->stream, nq,
                      ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
-                     qimg_p(ctx), ctx->nbins1, thr, ctx->selstat.p, ctx->sel_epoch, out, vidx,
+                     qimg_p(ctx), ctx->nbins1, thr, ctx->selstat.p, ctx->sel_epoch,
+                     ctx->selticket.p, (unsigned long long)ctx->sel_tickets, out, vidx,
                      total_slot);
+  ctx->sel_tickets += (uint64_t)nblk;
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }

@@ -453,6 +453,7 @@ int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float*
                      d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p, ctx->cd2.p, reset,
                      fuse ? ctx->fuse_ratio : -1.0, (int64_t)ctx->nq, ctx->d1.p, ctx->d2.p,
                      ctx->idx1.p, ctx->good.p);
+  ctx->ratio_fused_valid = fuse;
   if (fuse) ctx->ratio_fused = ctx->fuse_ratio;
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;

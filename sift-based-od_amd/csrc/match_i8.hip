@@ -1166,17 +1166,19 @@ int launch_match_i8(sod_ctx* ctx) {
   SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
   // shared thresholds, one array per partial-result slot: "nothing known" is bytes 0x80 (below
   // every reachable t2); the merge that releases a slot resets its array for the next launch,
-  // a new query count (slot layout) resets both here (stream_begin waited for both merges)
+  // a new query count (slot layout) resets BOTH slots here (stream_begin waited for both
+  // merges) -- also the one an overlap-off context never uses, so switching overlap on later
+  // (sod_match_set_overlap / sod_set_cu_reserve, which also clear gthr_n) never reads
+  // uninitialised thresholds
   int32_t* gthr = nullptr;
   if (!wide) {
-    const int64_t nslot = ctx->overlap ? 2 : 1;
     if (ctx->gthr.n < (size_t)(2 * nq_pad) || ctx->gthr_n != nq_pad) {
       if (ctx->gthr.n < (size_t)(2 * nq_pad)) {
         SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
         SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
         SOD_TRY(sod_reserve(ctx, ctx->gthr, (size_t)(2 * nq_pad)));
       }
-      SOD_HIP(ctx, hipMemsetAsync(ctx->gthr.p, 0x80, (size_t)(nslot * nq_pad) * 4, ks));
+      SOD_HIP(ctx, hipMemsetAsync(ctx->gthr.p, 0x80, (size_t)(2 * nq_pad) * 4, ks));
       ctx->gthr_n = nq_pad;
     }
     gthr = ctx->gthr.p + ctx->pslot * nq_pad;

@@ -92,8 +92,10 @@ struct sod_ctx {
   DevBuf<uint32_t> flags;       // [0]=invalid descriptor count, [1]=max dn bits, [2]=max qn bits
   bool matched = false, ratio_done = false;
   // sod_pipeline_enqueue: the ratio its final merge applies in the same kernel (-1 = none),
-  // and the ratio that merge applied (-1 = not fused), which sod_ratio_enqueue then skips
-  double fuse_ratio = -1.0, ratio_fused = -1.0;
+  // and the ratio that merge applied (valid only while ratio_fused_valid: the last merge
+  // fused it), which sod_ratio_enqueue then skips
+  double fuse_ratio = -1.0, ratio_fused = 0.0;
+  bool ratio_fused_valid = false;
 
   // ---- hough ----
   int32_t bins[4] = {0, 0, 0, 0};
@@ -112,6 +114,8 @@ struct sod_ctx {
   // ---- select / CSR / means ----
   DevBuf<uint64_t> selstat;     // look-back words of select_kernel (one per block)
   uint32_t sel_epoch = 0;       // select_kernel call count: tags the look-back words
+  DevBuf<unsigned long long> selticket;   // select_kernel block tickets (never reset)
+  uint64_t sel_tickets = 0;     // tickets drawn by the launches enqueued so far
   DevBuf<uint32_t> scal;        // device scalars: [0]=V, [1]=total members, [2]=B (all bins)
   DevBuf<uint32_t> vbin;        // [vmax] linear bin id, first-touch order
   DevBuf<int64_t> voff;         // [vmax+1]
@@ -150,9 +154,9 @@ struct sod_ctx {
   // ---- comm ----
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-  // channel cap the communicator was created under (NCCL_MAX_NCHANNELS at sod_comm_init,
-  // 0 = RCCL's default): the CU split needs every block of a collective resident on the
-  // reserved CUs at once (sod_set_cu_reserve checks it)
+  // blocks per collective the communicator was created with (ncclConfig_t.maxCTAs at
+  // sod_comm_init under a CU split, 0 = RCCL's default): the split needs every block of a
+  // collective resident on the reserved CUs at once (sod_set_cu_reserve checks it)
   int comm_max_channels = 0;
 
   // ---- DB sharing (sod_db_share): a source counts the contexts that alias its DB buffers

@@ -64,13 +64,23 @@ def _image(seed, image_id, kp_per_image, descriptors=True):
     return des, x, y, ang, pack_octave(octv, layer, xi), (w, h)
 
 
-def make_database(n_images, kp_per_image=1000, seed=0, first_image=0, descriptors=True):
+def make_database(n_images, kp_per_image=1000, seed=0, first_image=0, descriptors=True,
+                  workers=1):
     """Images ``[first_image, first_image + n_images)`` of the seeded DB.  With
     ``descriptors=False`` only the keypoints / image table are generated (the other ranks'
-    part of the replicated keypoint table); ``des`` is then an empty [0,128] array."""
+    part of the replicated keypoint table); ``des`` is then an empty [0,128] array.
+    ``workers`` > 1 generates images on that many threads (numpy releases the GIL in the
+    per-image generators and ufuncs); every image has its own seed, so the result is the
+    same bit for bit."""
+    ids = range(first_image, first_image + n_images)
+    if workers > 1 and n_images > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(workers) as ex:
+            parts = list(ex.map(lambda i: _image(seed, i, kp_per_image, descriptors), ids))
+    else:
+        parts = [_image(seed, i, kp_per_image, descriptors) for i in ids]
     des, xs, ys, angs, octs, imgs, cents, sizes = [], [], [], [], [], [], [], []
-    for i in range(first_image, first_image + n_images):
-        d, x, y, a, o, wh = _image(seed, i, kp_per_image, descriptors)
+    for i, (d, x, y, a, o, wh) in zip(ids, parts):
         des.append(d); xs.append(x); ys.append(y); angs.append(a); octs.append(o)
         imgs.append(np.full(kp_per_image, i - first_image, np.int32))
         cents.append(centroid_of(x, y))

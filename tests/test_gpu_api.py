@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from conftest import golden
-from helpers import ThreadComm, kp, kp_dict
+from helpers import ThreadComm, assert_stages_equal_oracle, kp, kp_dict, oracle_inputs
 from oracle import oracle as orc
 from sift_based_od_amd import _lib, synthetic
 import sift_based_od_amd as sod
@@ -225,6 +225,15 @@ def test_packed_db_roundtrip(tmp_path, impl):
         assert np.array_equal(x, y)
     for k in ("keys", "votes", "offsets", "members"):
         assert np.array_equal(ref[1][k], got[1][k])
+    # oracle leg: the packed-image upload's pipeline against the oracle run on the raw
+    # descriptors (main.py:50-86 flattening + match, then main.py:89-132)
+    dbkp, qkp, images = oracle_inputs(db, qs.kp)
+    o = orc.run_pipeline(qs.des, qkp, db.des, dbkp, images, 15, qs.shape)
+    i1, d1, d2, g = got[0]
+    assert np.array_equal(i1, o["idx1"]) and np.array_equal(g, o["good"])
+    assert np.array_equal(d1, o["d1"]) and np.array_equal(d2, o["d2"])
+    assert len(o["valid"]) > 0
+    assert_stages_equal_oracle(got[1], None, o["table"], o["valid"], None)
 
 
 @pytest.mark.parametrize("fused", [False, True])
@@ -259,6 +268,18 @@ def test_query_batch_equals_per_image(fused):
             np.testing.assert_array_equal(a["params"], b["affine"]["params"])
             p = c.postprocess()
             np.testing.assert_array_equal(p["final_pose"], b["post"]["final_pose"])
+            # oracle leg: the batch's per-image results against the oracle's pipeline of
+            # that image alone (main.py:68-157 per query image, main.py:178-188)
+            dbkp, qkp, images = oracle_inputs(db, kp_)
+            o = orc.run_pipeline(des, qkp, db.des, dbkp, images, 15, shape)
+            assert np.array_equal(b["idx1"], o["idx1"]) and np.array_equal(b["good"], o["good"])
+            assert np.array_equal(b["d1"], o["d1"]) and np.array_equal(b["d2"], o["d2"])
+            assert_stages_equal_oracle(b["valid"], b["affine"], o["table"], o["valid"],
+                                       o["affine"])
+            ref = orc.post_process(b["valid"]["means"][b["post"]["bin_index"]])
+            fp = np.array([[q[0][0], q[0][1], q[1], q[2], q[3][0], q[3][1]]
+                           for q in ref["final_pose"]]).reshape(-1, 6)
+            np.testing.assert_allclose(b["post"]["final_pose"], fp, rtol=1e-12, atol=1e-9)
 
 
 def test_shared_db_contexts():
@@ -395,23 +416,72 @@ def test_matcher_overlap_equals_serial(use_comm, reserve, affine):
             assert np.array_equal(a0["params"], a1["params"])
 
 
-def test_cu_reserve_channel_cap(monkeypatch):
+def test_cu_reserve_channel_cap():
     """The CU split runs collectives on the reserved CUs only, so every block of an RCCL
-    kernel must fit there: a communicator created with more channels than reserved CUs is
-    refused in either order (split then comm, comm then split)."""
-    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "16")
+    kernel must fit there: a communicator created under the split gets maxCTAs = the reserved
+    CU count (per communicator, ncclConfig_t); one created without a split, or with more
+    blocks than a later, smaller split reserves, is refused.  The environment is not used."""
     with _lib.Context(0) as c:
-        c.comm_init(1, 0, _lib.unique_id())
-        with pytest.raises(_lib.SodError, match="NCCL_MAX_NCHANNELS"):
-            c.set_cu_reserve(1)                       # 8 reserved CUs < 16 channels
-        c.set_cu_reserve(2)                           # 16 reserved CUs: fits
+        c.comm_init(1, 0, _lib.unique_id())           # RCCL's default block count
+        with pytest.raises(_lib.SodError, match="maxCTAs"):
+            c.set_cu_reserve(1)
+    with _lib.Context(0) as c:
+        c.set_cu_reserve(2)                           # 16 reserved CUs
+        c.comm_init(1, 0, _lib.unique_id())           # maxCTAs 16
+        with pytest.raises(_lib.SodError, match="maxCTAs"):
+            c.set_cu_reserve(1)                       # 8 CUs < 16 blocks
+        c.set_cu_reserve(2)
         c.set_cu_reserve(0)
     with _lib.Context(0) as c:
         c.set_cu_reserve(1)
-        with pytest.raises(_lib.SodError, match="NCCL_MAX_NCHANNELS"):
-            c.comm_init(1, 0, _lib.unique_id())
-    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "8")
-    with _lib.Context(0) as c:
-        c.comm_init(1, 0, _lib.unique_id())
+        c.comm_init(1, 0, _lib.unique_id())           # maxCTAs 8
         c.set_cu_reserve(1)
         c.set_cu_reserve(0)
+
+
+@pytest.mark.parametrize("switch", ["overlap", "cu_reserve"])
+def test_threshold_slots_after_overlap_switch(switch):
+    """The int8 matcher's shared-threshold slots: a context matches once with overlap off
+    (one slot in use), then switches the matcher stream on with the SAME query count -- the
+    second slot must start from "nothing known", never from uninitialised memory."""
+    rng = np.random.default_rng(91)
+    db = synthetic.sift_like_descriptors(rng, 120000)
+    q = synthetic.sift_like_descriptors(rng, 3000)
+    e1, f1, f2 = orc.knn2_match(q, db)
+    with _lib.Context(0) as c:
+        c.upload_db(db)
+        c.upload_queries(q)
+        c.match()
+        c.ratio(0.75)
+        if switch == "overlap":
+            c.set_overlap(True)
+        else:
+            c.set_cu_reserve(1)
+        for _ in range(3):          # slots 1, 0, 1
+            c.match()
+            c.ratio(0.75)
+            idx1, d1, d2, _ = c.match_result()
+            assert np.array_equal(idx1, e1)
+            assert np.array_equal(d1, f1) and np.array_equal(d2, f2)
+
+
+def test_ratio_argument_validation():
+    """A negative or NaN ratio is refused (it used to collide with the 'not fused' marker)."""
+    db = synthetic.make_database(2, 300, seed=93)
+    qs = synthetic.make_queries(400, seed=94, db_seed=93, kp_per_image=300)
+    with _lib.Context(0) as c:
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        c.upload_queries(qs.des, qs.kp)
+        c.match()
+        for bad in (-1.0, float("nan"), float("inf")):
+            with pytest.raises(_lib.SodError, match="ratio"):
+                c.ratio(bad)
+            with pytest.raises(_lib.SodError, match="ratio"):
+                c.pipeline(qs.shape, 15, ratio=bad)
+        c.pipeline(qs.shape, 15, ratio=0.75)
+        good = c.match_result()[3]
+        c.ratio(0.5)                 # a different ratio after a fused one is re-applied
+        _, d1, d2, g2 = c.match_result()
+        assert np.array_equal(g2, orc.ratio_test(d1, d2, 0.5))
+        assert g2.sum() <= good.sum()
