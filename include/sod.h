@@ -152,6 +152,12 @@ int sod_match_get(sod_ctx* ctx, int32_t* idx1, float* d1, float* d2, uint8_t* go
  * main.py:29,85): idx1[q] = trainIdx (global row), good[q] = keep.  nq must equal the
  * uploaded query count.  Hough/select/affine then run on these matches. */
 int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t* good);
+/* knnMatch's second DMatch (main.py:71: n.trainIdx, which OpenCV fills although main.py
+ * reads only n.distance): per query the lowest trainIdx other than idx1 whose distance is
+ * the second-best one -- what OpenCV's strict-'<' k=2 insertion keeps -- found by a second
+ * MFMA pass over the DB after a bf16 match (sod_match_set_impl(ctx, 0)); -1 with a
+ * single DB row.  Single context (no shards). */
+int sod_match_second_get(sod_ctx* ctx, int32_t* idx2);
 /* 1 if every distance is provably < 2048 (sqrtf then injective on the squared
  * distances, so squared-distance ordering == OpenCV's float ordering), else 0. */
 int sod_match_exact_order(sod_ctx* ctx, int* exact);
@@ -177,6 +183,14 @@ int sod_valid_get(sod_ctx* ctx, int32_t* keys /* [V*4] */, int32_t* votes /* [V]
 /* all occupied bins (counts), first-touch order: keys[B*4], votes[B] */
 int sod_bins_count(sod_ctx* ctx, int64_t* n_bins);
 int sod_bins_get(sod_ctx* ctx, int32_t* keys, int32_t* votes);
+/* Boundary guard of HTHF:31-35,49-58 (x, y through cos / sin): the device lists every
+ * match whose x or y bin could depend on the last ulp of cos / sin and the library redoes
+ * it with the host's libm (the calls math.cos / math.sin make), then, if a bin changed, the
+ * histogram and the stages after it -- before any Hough result is read.  Reports the last
+ * Hough launch's (or sod_pose_batch's) listed matches and changed bins, and the running
+ * totals of this context. */
+int sod_hough_guard_stats(sod_ctx* ctx, int64_t* flagged, int64_t* changed,
+                          int64_t* flagged_total, int64_t* changed_total);
 
 /* ---- A11-A13: AffineParameters / remove_outliers / apply_affine_parameters -------
  * AffineParameters.py:89-160, main.py:139-157: per valid bin, fixed point of
@@ -256,6 +270,16 @@ int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets,
  * [n*128].  detect_bgr takes an interleaved 8-bit BGR image (cvtColor BGR2GRAY first). */
 int sod_sift_set_params(sod_ctx* ctx, int32_t n_octave_layers, double contrast_threshold,
                         double edge_threshold, double sigma);
+/* Orientation / descriptor histogram adds.  OpenCV sums each bin in sample order
+ * (calcOrientationHist / calcSIFTDescriptor); the device keeps that order either with one
+ * lane per sample (ordered) or with whole-wave adds whose same-bin lanes gfx950 applies in
+ * lane order -- an undocumented property, so the context checks it on the device at its
+ * first SIFT call (one wave, 512 order-sensitive trials) and uses the wave adds only when
+ * it holds (and only on gfx950).  mode -1 = that automatic choice (default), 0 = always
+ * the ordered adds.  sod_sift_lane_order reports the active path (1 = wave adds) and the
+ * self-check result (1 = lane order held, 0 = not, -1 = not run). */
+int sod_sift_set_lane_order(sod_ctx* ctx, int mode);
+int sod_sift_lane_order(sod_ctx* ctx, int* active, int* probe_ok);
 int sod_sift_detect(sod_ctx* ctx, const uint8_t* gray /* [h*w] */, int32_t width,
                     int32_t height, int32_t* n_keypoints);
 int sod_sift_detect_bgr(sod_ctx* ctx, const uint8_t* bgr /* [h*w*3] */, int32_t width,

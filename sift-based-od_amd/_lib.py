@@ -70,6 +70,7 @@ SIGNATURES = {
     "sod_match_get": (C.c_int, [c_ctx, c_i32p, c_f32p, c_f32p, c_u8p]),
     "sod_matches_set": (C.c_int, [c_ctx, C.c_int32, c_i32p, c_u8p]),
     "sod_match_exact_order": (C.c_int, [c_ctx, C.POINTER(C.c_int)]),
+    "sod_match_second_get": (C.c_int, [c_ctx, c_i32p]),
     "sod_hough_enqueue": (C.c_int, [c_ctx, C.c_int32, C.c_int32, c_i32p, C.c_int64, C.c_int64]),
     "sod_hough_allreduce_enqueue": (C.c_int, [c_ctx]),
     "sod_select_enqueue": (C.c_int, [c_ctx, C.c_int32]),
@@ -77,6 +78,7 @@ SIGNATURES = {
     "sod_valid_get": (C.c_int, [c_ctx, c_i32p, c_i32p, c_i64p, c_i32p, c_f64p]),
     "sod_bins_count": (C.c_int, [c_ctx, c_i64p]),
     "sod_bins_get": (C.c_int, [c_ctx, c_i32p, c_i32p]),
+    "sod_hough_guard_stats": (C.c_int, [c_ctx, c_i64p, c_i64p, c_i64p, c_i64p]),
     "sod_affine_enqueue": (C.c_int, [c_ctx, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                      C.c_int32]),
     "sod_affine_get": (C.c_int, [c_ctx, c_u8p, c_i32p, c_f64p, c_u8p]),
@@ -98,6 +100,8 @@ SIGNATURES = {
     "sod_hough_partial_get": (C.c_int, [c_ctx, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "sod_hough_partial_set": (C.c_int, [c_ctx, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "sod_sift_set_params": (C.c_int, [c_ctx, C.c_int32, C.c_double, C.c_double, C.c_double]),
+    "sod_sift_set_lane_order": (C.c_int, [c_ctx, C.c_int]),
+    "sod_sift_lane_order": (C.c_int, [c_ctx, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "sod_sift_detect": (C.c_int, [c_ctx, c_u8p, C.c_int32, C.c_int32, c_i32p]),
     "sod_sift_detect_bgr": (C.c_int, [c_ctx, c_u8p, C.c_int32, C.c_int32, c_i32p]),
     "sod_sift_detect_batch": (C.c_int, [c_ctx, C.c_int32, C.POINTER(c_u8p), c_i32p, c_i32p,
@@ -288,6 +292,12 @@ class Context:
                                         ptr(d2, C.c_float), ptr(good, C.c_uint8)))
         return idx1, d1, d2, good.astype(bool)
 
+    def second_index(self):
+        """knnMatch's n.trainIdx per query (sod_match_second_get; bf16 matcher only)."""
+        out = np.empty(self.nq, np.int32)
+        self._chk(self._L.sod_match_second_get(self._h, ptr(out, C.c_int32)))
+        return out
+
     def exact_order(self):
         v = C.c_int()
         self._chk(self._L.sod_match_exact_order(self._h, C.byref(v)))
@@ -330,6 +340,13 @@ class Context:
         votes = np.empty(n.value, np.int32)
         self._chk(self._L.sod_bins_get(self._h, ptr(keys, C.c_int32), ptr(votes, C.c_int32)))
         return keys, votes
+
+    def guard_stats(self):
+        """Boundary guard of the last Hough launch / pose batch (sod_hough_guard_stats):
+        (listed matches, changed bins, listed total, changed total)."""
+        v = [C.c_int64() for _ in range(4)]
+        self._chk(self._L.sod_hough_guard_stats(self._h, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
 
     def affine(self, query_size, x_factor=128.0, y_factor=128.0, threshold=4):
         self._chk(self._L.sod_affine_enqueue(self._h, int(query_size[0]), int(query_size[1]),
@@ -488,6 +505,17 @@ class Context:
         self._chk(self._L.sod_sift_set_params(self._h, int(n_octave_layers),
                                               float(contrast_threshold), float(edge_threshold),
                                               float(sigma)))
+
+    def sift_set_lane_order(self, mode=-1):
+        """Histogram adds: -1 = wave adds when the device self-check holds, 0 = ordered
+        single-lane adds (sod_sift_set_lane_order)."""
+        self._chk(self._L.sod_sift_set_lane_order(self._h, int(mode)))
+
+    def sift_lane_order(self):
+        """(active path: 1 wave adds / 0 ordered, self-check: 1 held / 0 failed / -1 not run)."""
+        a, p = C.c_int(), C.c_int()
+        self._chk(self._L.sod_sift_lane_order(self._h, C.byref(a), C.byref(p)))
+        return a.value, p.value
 
     def sift_detect(self, image, descriptors=True):
         """detectAndCompute on an 8-bit gray [h, w] or BGR [h, w, 3|4] image: SoA keypoints

@@ -806,6 +806,30 @@ int sod_match_get(sod_ctx* ctx, int32_t* idx1, float* d1, float* d2, uint8_t* go
   return SOD_OK;
 }
 
+int sod_match_second_get(sod_ctx* ctx, int32_t* idx2) {
+  SOD_TRY(set_dev(ctx));
+  if (!idx2) return sod_fail(ctx, SOD_EINVAL, "null idx2");
+  if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
+  if (ctx->impl != 0)
+    return sod_fail(ctx, SOD_ESTATE, "the second neighbour's index needs the bf16 matcher "
+                                     "(sod_match_set_impl(ctx, 0) before the uploads)");
+  if (ctx->nranks > 1 || ctx->comm || ctx->row_offset != 0)
+    return sod_fail(ctx, SOD_ESTATE, "the second neighbour's index is single-context only");
+  DevBuf<int32_t> d;
+  const size_t n = (size_t)ctx->nq;
+  int rc = sod_reserve(ctx, d, (size_t)sod_nq_pad(ctx));
+  if (rc == SOD_OK) rc = launch_second_index(ctx, d.p);
+  if (rc == SOD_OK) rc = download(ctx, idx2, d.p, n);
+  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "second neighbour pass failed");
+  (void)hipStreamSynchronize(ctx->stream);
+  sod_release(d);
+  SOD_TRY(rc);
+  for (size_t q = 0; q < n; ++q)
+    if (idx2[q] == 0x7f7f7f7f) idx2[q] = -1;   // a single DB row: no second neighbour
+  return SOD_OK;
+}
+
 int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t* good) {
   SOD_TRY(set_dev(ctx));
   if (!idx1 || !good || nq != ctx->nq || nq < 1)
@@ -894,6 +918,7 @@ int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold) {
 int sod_valid_counts(sod_ctx* ctx, int64_t* n_valid, int64_t* n_members) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->selected) return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
+  SOD_TRY(sod_guard_resolve(ctx));
   uint32_t s[2];
   SOD_HIP(ctx, hipMemcpyAsync(s, ctx->scal.p, 8, hipMemcpyDeviceToHost, ctx->stream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -934,6 +959,7 @@ int sod_valid_get(sod_ctx* ctx, int32_t* keys, int32_t* votes, int64_t* offsets,
 int sod_bins_count(sod_ctx* ctx, int64_t* n_bins) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  SOD_TRY(sod_guard_resolve(ctx));
   SOD_TRY(launch_all_bins(ctx));
   uint32_t b = 0;
   SOD_HIP(ctx, hipMemcpyAsync(&b, ctx->scal.p + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -957,12 +983,28 @@ int sod_bins_get(sod_ctx* ctx, int32_t* keys, int32_t* votes) {
   return SOD_OK;
 }
 
+int sod_hough_guard_stats(sod_ctx* ctx, int64_t* flagged, int64_t* changed,
+                          int64_t* flagged_total, int64_t* changed_total) {
+  SOD_TRY(set_dev(ctx));
+  SOD_TRY(sod_guard_resolve(ctx));
+  if (flagged) *flagged = ctx->guard_flagged;
+  if (changed) *changed = ctx->guard_patched;
+  if (flagged_total) *flagged_total = ctx->guard_flagged_total;
+  if (changed_total) *changed_total = ctx->guard_patched_total;
+  return SOD_OK;
+}
+
 // ---- affine ---------------------------------------------------------------------------
 int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_factor,
                        double y_factor, int32_t threshold) {
   SOD_TRY(set_dev(ctx, false));   // runs beside the means on the side stream
   if (!ctx->selected) return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
   if (!(x_factor != 0.0) || !(y_factor != 0.0)) return sod_fail(ctx, SOD_EINVAL, "zero factor");
+  ctx->aff_qw = query_w;
+  ctx->aff_qh = query_h;
+  ctx->aff_xf = x_factor;
+  ctx->aff_yf = y_factor;
+  ctx->aff_thr = threshold;
   SOD_TRY(launch_affine_gather(ctx));
   SOD_TRY(sod_reserve(ctx, ctx->surv, (size_t)ctx->vmax));
   SOD_TRY(sod_reserve(ctx, ctx->fvotes, (size_t)ctx->vmax));
@@ -1027,8 +1069,9 @@ int sod_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my, co
   ctx->qw = query_w;
   DevBuf<float> f[6];
   DevBuf<int32_t> o[2];
-  DevBuf<double> c[2], dp;
+  DevBuf<double> c[2], dp, grec;
   DevBuf<int32_t> di;
+  DevBuf<uint32_t> gst;
   int rc = SOD_OK;
   const float* fs[6] = {mx, my, mangle, qx, qy, qangle};
   for (int i = 0; i < 6 && rc == SOD_OK; ++i) rc = upload(ctx, f[i], fs[i], (size_t)n);
@@ -1038,19 +1081,48 @@ int sod_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my, co
   if (rc == SOD_OK) rc = upload(ctx, c[1], cy, (size_t)n);
   if (rc == SOD_OK) rc = sod_reserve(ctx, dp, (size_t)n * 4);
   if (rc == SOD_OK) rc = sod_reserve(ctx, di, (size_t)n * 4);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, grec, (size_t)n * 8);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, gst, 1);
+  if (rc == SOD_OK && hipMemsetAsync(gst.p, 0, 4, ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "guard counter reset failed");
   if (rc == SOD_OK)
     rc = launch_pose_batch(ctx, n, f[0].p, f[1].p, f[2].p, o[0].p, f[3].p, f[4].p, f[5].p, o[1].p,
-                           c[0].p, c[1].p, dp.p, di.p);
+                           c[0].p, c[1].p, dp.p, di.p, grec.p, gst.p);
   if (rc == SOD_OK) rc = download(ctx, pose, dp.p, (size_t)n * 4);
   if (rc == SOD_OK) rc = download(ctx, idx, di.p, (size_t)n * 4);
+  uint32_t ng = 0;
+  if (rc == SOD_OK) rc = download(ctx, &ng, gst.p, 1);
   if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
     rc = sod_fail(ctx, SOD_EHIP, "pose batch failed");
   (void)hipStreamSynchronize(ctx->stream);
+  // boundary guard (hough.hip): the listed elements' x, y and x / y bins with glibc cos / sin
+  if (rc == SOD_OK && ng) {
+    std::vector<double> rec((size_t)ng * 8);
+    rc = download(ctx, rec.data(), grec.p, rec.size());
+    if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+      rc = sod_fail(ctx, SOD_EHIP, "guard records download failed");
+    int64_t changed = 0;
+    for (uint32_t i = 0; rc == SOD_OK && i < ng; ++i) {
+      const double* r = &rec[(size_t)i * 8];
+      const int64_t e = (int64_t)r[0];
+      const int32_t ox = idx[4 * e], oy = idx[4 * e + 1];
+      sod_guard_host_pose(r, ctx->bins, &pose[4 * e], &pose[4 * e + 1], &idx[4 * e], &idx[4 * e + 1]);
+      changed += (ox != idx[4 * e]) || (oy != idx[4 * e + 1]);
+    }
+    ctx->guard_flagged = ng;
+    ctx->guard_patched = changed;
+    ctx->guard_flagged_total += ng;
+    ctx->guard_patched_total += changed;
+  } else if (rc == SOD_OK) {
+    ctx->guard_flagged = ctx->guard_patched = 0;
+  }
   for (auto& b : f) sod_release(b);
   for (auto& b : o) sod_release(b);
   for (auto& b : c) sod_release(b);
   sod_release(dp);
   sod_release(di);
+  sod_release(grec);
+  sod_release(gst);
   return rc;
 }
 

@@ -25,6 +25,7 @@
 //   affine_kernel    one wave per bin: decoupled 3x3 normal equations, pinv by Jacobi,
 //                    outlier rejection, fixed point (AffineParameters.py:89-160)
 #include <algorithm>
+#include <cmath>
 #include <utility>
 
 #include "sod_internal.h"
@@ -45,7 +46,7 @@ __device__ __forceinline__ int unpack_octave(int packed) {  // SiftHelperFunctio
 }
 
 // Python int() of a float that is then clamped to [0, b-1] after a -1 (HTHF:49-58).
-__device__ __forceinline__ int xy_index(double v, int b) {
+__host__ __device__ __forceinline__ int xy_index(double v, int b) {
   long long i;
   if (!(v == v)) i = 0;                 // NaN: unreachable for finite inputs
   else if (v > 1e9) i = 1000000000LL;
@@ -66,11 +67,12 @@ __device__ __forceinline__ void bin_index(double x, double y, double a, int k, i
   idx[3] = lut[k + kSigmaLutHalf];
 }
 
-// estimate_object_pose (HTHF:4-37) + calculate_bin_index (HTHF:39-72)
+// estimate_object_pose (HTHF:4-37) + calculate_bin_index (HTHF:39-72); t = the translation
+// (tx, ty) the rotation acts on, for the boundary guard below
 __device__ __forceinline__ void pose_bins(float mx, float my, float ma, int mo, float qx, float qy,
                                           float qa, int qo, double cx, double cy, int H, int W,
                                           Bins b, const int* __restrict__ lut, double pose[4],
-                                          int idx[4]) {
+                                          int idx[4], double t[2]) {
   const int k = unpack_octave(qo) - unpack_octave(mo);  // m_scale / q_scale = 2^(oQ-oM), exact
   const double s = ldexp(1.0, k);
   const double tx = (cx - (double)mx) * s;
@@ -84,7 +86,49 @@ __device__ __forceinline__ void pose_bins(float mx, float my, float ma, int mo, 
   pose[1] = y;
   pose[2] = a;
   pose[3] = s;
+  t[0] = tx;
+  t[1] = ty;
   bin_index(x, y, a, k, H, W, b, lut, idx);
+}
+
+// ---- boundary guard (SURVEY 7 "Hough parity") -------------------------------------------
+// Every step of the pose is one correctly rounded IEEE operation, the same on both sides,
+// except cos/sin: the device's (ocml) and glibc's (math.cos / math.sin of the reference,
+// HTHF:31-32) may round differently by an ulp or two.  The x / y bin indices are then still
+// exact unless v = (x*b)/W lies within that error of an integer where int(v)-1 clamped to
+// [0, b-1] (HTHF:49-58) steps -- 2..b.  Such matches are listed (guard records) and done
+// again on the host with glibc (guard_resolve in api.hip), so bin counts are exact by
+// construction.  Error bound: with trig off by <= 4 ulp, |dx| <= 2e-15 (|tx|+|ty|+|qx|+|x|);
+// the tolerance below is 50x that in units of v.  theta and sigma use no transcendental
+// (theta: exact fmod; sigma: the LUT).
+constexpr int kGuardRec = 8;    // doubles per record: q, tx, ty, alpha, qx, qy, H, W
+
+__device__ __forceinline__ bool near_edge(double v, int b, double mag) {
+  const double n = rint(v);
+  if (!(n >= 2.0 && n <= (double)b)) return false;   // NaN / inf / clamped: no step
+  return fabs(v - n) <= 1e-13 * (mag + fabs(v) + 1.0);
+}
+
+__device__ __forceinline__ bool guard_flag(const double p[4], const double t[2], double qx,
+                                           double qy, int H, int W, Bins b) {
+  const double ax = fabs(t[0]) + fabs(t[1]);
+  return near_edge((p[0] * b.x) / W, b.x, (ax + fabs(qx) + fabs(p[0])) * b.x / W) ||
+         near_edge((p[1] * b.y) / H, b.y, (ax + fabs(qy) + fabs(p[1])) * b.y / H);
+}
+
+__device__ __forceinline__ void guard_push(double* __restrict__ rec, uint32_t* __restrict__ n,
+                                           int64_t q, const double p[4], const double t[2],
+                                           double qx, double qy, int H, int W) {
+  const uint32_t i = atomicAdd(n, 1u);   // capacity = queries: every query fits
+  double* r = rec + (int64_t)kGuardRec * i;
+  r[0] = (double)q;
+  r[1] = t[0];
+  r[2] = t[1];
+  r[3] = p[2];
+  r[4] = qx;
+  r[5] = qy;
+  r[6] = (double)H;
+  r[7] = (double)W;
 }
 
 // scale_factor -> k with s == 2^k exactly (estimate_object_pose only produces powers of 2);
@@ -98,6 +142,19 @@ __device__ __forceinline__ int sigma_from_scale(double s, Bins b, const int* lut
   }
   *generic = true;
   return 0;
+}
+
+// main.py:105-110: 16 votes (w, x, y, z in {0,1}, lexicographic), kept when every index is
+// < bins (no theta wrap)
+__device__ __forceinline__ uint32_t vote_mask(const int ix[4], Bins b) {
+  uint32_t mask = 0;
+#pragma unroll
+  for (int slot = 0; slot < 16; ++slot) {
+    const int w = (slot >> 3) & 1, x = (slot >> 2) & 1, y = (slot >> 1) & 1, z = slot & 1;
+    if (ix[0] + w < b.x && ix[1] + x < b.y && ix[2] + y < b.t && ix[3] + z < b.s)
+      mask |= 1u << slot;
+  }
+  return mask;
 }
 
 __device__ __forceinline__ uint32_t lin_bin(int ix, int iy, int it, int is, Bins b) {
@@ -116,7 +173,8 @@ __global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
                             double* __restrict__ pose, uint32_t* __restrict__ basekey,
                             uint32_t* __restrict__ vmask, int64_t nbins,
                             uint32_t* __restrict__ counts, uint32_t* __restrict__ first,
-                            const int* __restrict__ isize, int2* __restrict__ msize) {
+                            const int* __restrict__ isize, int2* __restrict__ msize,
+                            double* __restrict__ grec, uint32_t* __restrict__ gstat) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // the histogram the next kernel fills starts empty: count 0, first touch "none" (folded
   // in here instead of two memset launches on the tail's critical path)
@@ -135,10 +193,12 @@ __global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
   }
   const int m = idx1[q];
   const int im = mimg[m];
-  double p[4];
+  double p[4], t[2];
   int ix[4];
-  pose_bins(mx[m], my[m], ma[m], mo[m], qx[q], qy[q], qa[q], qo[q], cent[2 * im], cent[2 * im + 1],
-            H, W, b, lut, p, ix);
+  const float fqx = qx[q], fqy = qy[q];
+  pose_bins(mx[m], my[m], ma[m], mo[m], fqx, fqy, qa[q], qo[q], cent[2 * im], cent[2 * im + 1],
+            H, W, b, lut, p, ix, t);
+  if (guard_flag(p, t, fqx, fqy, H, W, b)) guard_push(grec, gstat, q, p, t, fqx, fqy, H, W);
   pose[4 * q + 0] = p[0];
   pose[4 * q + 1] = p[1];
   pose[4 * q + 2] = p[2];
@@ -146,16 +206,34 @@ __global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
   msize[q] = make_int2(isize[2 * im], isize[2 * im + 1]);   // PoseBin img_size input
   basekey[q] = (uint32_t)ix[0] | ((uint32_t)ix[1] << 8) | ((uint32_t)ix[2] << 16) |
                ((uint32_t)ix[3] << 24);
-  // main.py:105-110: 16 votes, kept when every index is < bins (no theta wrap)
-  uint32_t mask = 0;
-#pragma unroll
-  for (int slot = 0; slot < 16; ++slot) {
-    const int w = (slot >> 3) & 1, x = (slot >> 2) & 1, y = (slot >> 1) & 1, z = slot & 1;
-    if (ix[0] + w < b.x && ix[1] + x < b.y && ix[2] + y < b.t && ix[3] + z < b.s)
-      mask |= 1u << slot;
-  }
   const bool own = (m >= own_lo) && (m < own_hi);
-  vmask[q] = mask | (own ? 0x10000u : 0u);
+  vmask[q] = vote_mask(ix, b) | (own ? 0x10000u : 0u);
+}
+
+// guard fix-up (api.hip guard_resolve): the host's (glibc) x, y and base key for the listed
+// queries; their vote masks follow the new keys and keep the shard bit
+__global__ void guard_patch_kernel(int n, const int32_t* __restrict__ pq,
+                                   const uint32_t* __restrict__ pkey, const double* __restrict__ pxy,
+                                   Bins b, uint32_t* __restrict__ basekey,
+                                   uint32_t* __restrict__ vmask, double* __restrict__ pose) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t q = pq[i];
+  const uint32_t key = pkey[i];
+  const int ix[4] = {(int)(key & 0xFF), (int)((key >> 8) & 0xFF), (int)((key >> 16) & 0xFF),
+                     (int)(key >> 24)};
+  basekey[q] = key;
+  vmask[q] = vote_mask(ix, b) | (vmask[q] & 0x10000u);
+  pose[4 * q + 0] = pxy[2 * i];
+  pose[4 * q + 1] = pxy[2 * i + 1];
+}
+
+// the re-done histogram holds every rank's votes (the all-reduce is not repeated): every
+// voting query counts here
+__global__ void own_all_kernel(int64_t nq, uint32_t* __restrict__ vmask) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+       q += (int64_t)gridDim.x * blockDim.x)
+    if (vmask[q] & 0xFFFFu) vmask[q] |= 0x10000u;
 }
 
 __global__ void pose_batch_kernel(int64_t n, const float* __restrict__ mx,
@@ -165,12 +243,15 @@ __global__ void pose_batch_kernel(int64_t n, const float* __restrict__ mx,
                                   const int* __restrict__ qo, const double* __restrict__ cx,
                                   const double* __restrict__ cy, int H, int W, Bins b,
                                   const int* __restrict__ lut, double* __restrict__ pose,
-                                  int* __restrict__ idx) {
+                                  int* __restrict__ idx, double* __restrict__ grec,
+                                  uint32_t* __restrict__ gstat) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double p[4];
+  double p[4], t[2];
   int ix[4];
-  pose_bins(mx[i], my[i], ma[i], mo[i], qx[i], qy[i], qa[i], qo[i], cx[i], cy[i], H, W, b, lut, p, ix);
+  pose_bins(mx[i], my[i], ma[i], mo[i], qx[i], qy[i], qa[i], qo[i], cx[i], cy[i], H, W, b, lut, p,
+            ix, t);
+  if (guard_flag(p, t, qx[i], qy[i], H, W, b)) guard_push(grec, gstat, i, p, t, qx[i], qy[i], H, W);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     pose[4 * i + j] = p[j];
@@ -209,7 +290,13 @@ constexpr int kHistThreads = 1024;
 __global__ __launch_bounds__(kHistThreads) void hist_kernel(
     int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask, Bins b,
     int64_t nbins, const int* __restrict__ qimg, int64_t nbins1, const int* __restrict__ rng,
-    uint32_t* __restrict__ gcount, uint32_t* __restrict__ gfirst) {
+    uint32_t* __restrict__ gcount, uint32_t* __restrict__ gfirst, uint32_t* __restrict__ gstat) {
+  // the guard records pose_kernel listed: their count moves to the slot the host reads, and
+  // the append counter starts the next launch at 0 (stream order: pose_kernel is done)
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    gstat[1] = gstat[0];
+    gstat[0] = 0u;
+  }
   // 64 KiB: two work-groups per CU
   __shared__ uint32_t cnt2[kSlab / 2];     // two u16 counts per word (<= kChunk votes per bin)
   __shared__ uint32_t fst[kSlab];
@@ -1070,11 +1157,11 @@ int sod_build_sigma_lut(sod_ctx* ctx, int32_t bs) {
 int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my, const float* ma,
                       const int32_t* mo, const float* qx, const float* qy, const float* qa,
                       const int32_t* qo, const double* cx, const double* cy, double* pose,
-                      int32_t* idx) {
+                      int32_t* idx, double* grec, uint32_t* gstat) {
   const int bs = 256;
   hipLaunchKernelGGL(pose_batch_kernel, dim3((unsigned)cdiv(n, bs)), dim3(bs), 0, ctx->stream, n,
                      mx, my, ma, mo, qx, qy, qa, qo, cx, cy, ctx->qh, ctx->qw, ctx_bins(ctx),
-                     ctx->sig_lut.p, pose, idx);
+                     ctx->sig_lut.p, pose, idx, grec, gstat);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
@@ -1109,29 +1196,9 @@ static int mark_read(sod_ctx* ctx, hipStream_t s, int par, hipEvent_t (&ev)[2], 
   return SOD_OK;
 }
 
-int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
-  const int64_t nq = sod_win_n(ctx), q0 = sod_win0(ctx);
-  std::swap(ctx->pose, ctx->pose_b);
-  std::swap(ctx->msize, ctx->msize_b);
-  SOD_TRY(next_parity(ctx, ctx->hpar, ctx->ev_hread, ctx->hread_id));
-  SOD_TRY(sod_reserve(ctx, ctx->pose, (size_t)nq * 4));
-  SOD_TRY(sod_reserve(ctx, ctx->basekey, (size_t)nq));
-  SOD_TRY(sod_reserve(ctx, ctx->vmask, (size_t)nq));
-  SOD_TRY(sod_reserve(ctx, ctx->msize, (size_t)nq * 2));
-  SOD_TRY(sod_reserve(ctx, ctx->counts, (size_t)ctx->nbins));
-  SOD_TRY(sod_reserve(ctx, ctx->first, (size_t)ctx->nbins));
-  const int bs = 256;
-  // one thread per query, and enough of them to clear the histogram in a few passes
-  const int64_t pgrid = std::max<int64_t>(cdiv(nq, bs), std::min<int64_t>(cdiv(ctx->nbins, 4 * bs), 4096));
-  hipLaunchKernelGGL(pose_kernel, dim3((unsigned)pgrid), dim3(bs), 0, ctx->stream, nq,
-                     ctx->good.p + q0, ctx->idx1.p + q0, ctx->qx.p + q0, ctx->qy.p + q0,
-                     ctx->qang.p + q0, ctx->qoct.p + q0,
-                     ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p,
-                     ctx->qh, ctx->qw, qimg_p(ctx), ctx->n_qimg ? ctx->qshape.p : nullptr,
-                     ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
-                     ctx->basekey.p, ctx->vmask.p, ctx->nbins, ctx->counts.p, ctx->first.p,
-                     ctx->isize.p, reinterpret_cast<int2*>(ctx->msize.p));
-  SOD_HIP(ctx, hipGetLastError());
+// hist_kernel over the current window: one work-group per (bin slab, query chunk)
+static int launch_hist(sod_ctx* ctx) {
+  const int64_t nq = sod_win_n(ctx);
   const int64_t nchunk = cdiv(nq, kChunk);
   dim3 grid((unsigned)cdiv(ctx->nbins, kSlab), (unsigned)nchunk);
   const int* rng = nullptr;
@@ -1158,8 +1225,145 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
   }
   hipLaunchKernelGGL(hist_kernel, grid, dim3(kHistThreads), 0, ctx->stream, nq, ctx->basekey.p,
                      ctx->vmask.p, ctx_bins(ctx), ctx->nbins, qimg_p(ctx), ctx->nbins1, rng,
-                     ctx->counts.p, ctx->first.p);
+                     ctx->counts.p, ctx->first.p, ctx->gstat.p);
   SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+static int guard_reserve(sod_ctx* ctx, int64_t n) {
+  SOD_TRY(sod_reserve(ctx, ctx->grec, (size_t)n * kGuardRec));
+  if (!ctx->gstat.p) {   // append counter + handed-over count: zero before the first launch
+    SOD_TRY(sod_reserve(ctx, ctx->gstat, 2));
+    SOD_HIP(ctx, hipMemsetAsync(ctx->gstat.p, 0, 8, ctx->stream));
+  }
+  return SOD_OK;
+}
+
+int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
+  const int64_t nq = sod_win_n(ctx), q0 = sod_win0(ctx);
+  std::swap(ctx->pose, ctx->pose_b);
+  std::swap(ctx->msize, ctx->msize_b);
+  SOD_TRY(next_parity(ctx, ctx->hpar, ctx->ev_hread, ctx->hread_id));
+  SOD_TRY(sod_reserve(ctx, ctx->pose, (size_t)nq * 4));
+  SOD_TRY(sod_reserve(ctx, ctx->basekey, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->vmask, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->msize, (size_t)nq * 2));
+  SOD_TRY(sod_reserve(ctx, ctx->counts, (size_t)ctx->nbins));
+  SOD_TRY(sod_reserve(ctx, ctx->first, (size_t)ctx->nbins));
+  SOD_TRY(guard_reserve(ctx, nq));
+  const int bs = 256;
+  // one thread per query, and enough of them to clear the histogram in a few passes
+  const int64_t pgrid = std::max<int64_t>(cdiv(nq, bs), std::min<int64_t>(cdiv(ctx->nbins, 4 * bs), 4096));
+  hipLaunchKernelGGL(pose_kernel, dim3((unsigned)pgrid), dim3(bs), 0, ctx->stream, nq,
+                     ctx->good.p + q0, ctx->idx1.p + q0, ctx->qx.p + q0, ctx->qy.p + q0,
+                     ctx->qang.p + q0, ctx->qoct.p + q0,
+                     ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p,
+                     ctx->qh, ctx->qw, qimg_p(ctx), ctx->n_qimg ? ctx->qshape.p : nullptr,
+                     ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
+                     ctx->basekey.p, ctx->vmask.p, ctx->nbins, ctx->counts.p, ctx->first.p,
+                     ctx->isize.p, reinterpret_cast<int2*>(ctx->msize.p), ctx->grec.p,
+                     ctx->gstat.p);
+  SOD_HIP(ctx, hipGetLastError());
+  SOD_TRY(launch_hist(ctx));
+  ctx->guard_done = false;
+  return SOD_OK;
+}
+
+void sod_guard_host_pose(const double r[8], const int32_t bins[4], double* x, double* y,
+                         int32_t* ix, int32_t* iy) {
+  // HTHF:31-35 with the libm cos / sin CPython's math module calls (glibc), then HTHF:49-58;
+  // one rounding per operation (this file is built with -ffp-contract=off)
+  const double tx = r[1], ty = r[2], a = r[3];
+  const double ca = std::cos(a), sa = std::sin(a);
+  *x = (ca * tx - sa * ty) + r[4];
+  *y = (sa * tx + ca * ty) + r[5];
+  const int H = (int)r[6], W = (int)r[7];
+  *ix = xy_index((*x * bins[0]) / W, bins[0]);
+  *iy = xy_index((*y * bins[1]) / H, bins[1]);
+}
+
+int sod_guard_resolve(sod_ctx* ctx) {
+  if (ctx->guard_done || !ctx->houghed) return SOD_OK;
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  uint32_t n = 0;
+  SOD_HIP(ctx, hipMemcpy(&n, ctx->gstat.p + 1, 4, hipMemcpyDeviceToHost));
+  ctx->guard_flagged = n;
+  ctx->guard_patched = 0;
+  ctx->guard_flagged_total += n;
+  if (n == 0) {
+    ctx->guard_done = true;
+    return SOD_OK;
+  }
+  const int64_t nq = sod_win_n(ctx);
+  std::vector<double> rec((size_t)n * kGuardRec);
+  std::vector<uint32_t> key((size_t)nq);
+  SOD_HIP(ctx, hipMemcpy(rec.data(), ctx->grec.p, rec.size() * 8, hipMemcpyDeviceToHost));
+  SOD_HIP(ctx, hipMemcpy(key.data(), ctx->basekey.p, key.size() * 4, hipMemcpyDeviceToHost));
+  std::vector<int32_t> pq(n);
+  std::vector<uint32_t> pkey(n);
+  std::vector<double> pxy(2 * (size_t)n);
+  int64_t changed = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const double* r = &rec[(size_t)i * kGuardRec];
+    const int64_t q = (int64_t)r[0];
+    int32_t ix, iy;
+    sod_guard_host_pose(r, ctx->bins, &pxy[2 * i], &pxy[2 * i + 1], &ix, &iy);
+    pq[i] = (int32_t)q;
+    pkey[i] = (key[q] & 0xFFFF0000u) | (uint32_t)ix | ((uint32_t)iy << 8);
+    changed += pkey[i] != key[q];
+  }
+  // every listed match takes the host's x, y (and key); the histogram and the stages after
+  // it are done again only when a bin changed
+  DevBuf<int32_t> dq;
+  DevBuf<uint32_t> dk;
+  DevBuf<double> dxy;
+  int rc = sod_reserve(ctx, dq, n);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, dk, n);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, dxy, 2 * (size_t)n);
+  if (rc == SOD_OK && (hipMemcpy(dq.p, pq.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                       hipMemcpy(dk.p, pkey.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                       hipMemcpy(dxy.p, pxy.data(), (size_t)n * 16, hipMemcpyHostToDevice) != hipSuccess))
+    rc = sod_fail(ctx, SOD_EHIP, "guard patch upload failed");
+  if (rc == SOD_OK) {
+    hipLaunchKernelGGL(guard_patch_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, ctx->stream,
+                       (int)n, dq.p, dk.p, dxy.p, ctx_bins(ctx), ctx->basekey.p, ctx->vmask.p,
+                       ctx->pose.p);
+    if (hipGetLastError() != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, "guard_patch_kernel launch");
+  }
+  if (rc == SOD_OK && changed) {
+    // the all-reduced histogram of a sharded run is rebuilt here from every rank's votes
+    // (each rank holds every good match and the whole keypoint table)
+    hipLaunchKernelGGL(own_all_kernel, dim3((unsigned)std::min<int64_t>(cdiv(nq, 256), 1024)),
+                       dim3(256), 0, ctx->stream, nq, ctx->vmask.p);
+    if (hipGetLastError() != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, "own_all_kernel launch");
+    if (rc == SOD_OK &&
+        (hipMemsetAsync(ctx->counts.p, 0, (size_t)ctx->nbins * 4, ctx->stream) != hipSuccess ||
+         hipMemsetAsync(ctx->first.p, 0xFF, (size_t)ctx->nbins * 4, ctx->stream) != hipSuccess))
+      rc = sod_fail(ctx, SOD_EHIP, "guard histogram reset failed");
+    if (rc == SOD_OK) rc = launch_hist(ctx);
+    if (rc == SOD_OK && ctx->selected) rc = launch_select(ctx, ctx->vote_thr);
+    if (rc == SOD_OK && ctx->affined) rc = launch_affine_gather(ctx);
+    if (rc == SOD_OK && ctx->affined)
+      rc = launch_affine(ctx, 0, true, ctx->voff.p, ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p,
+                         ctx->aisig.p, ctx->aff_qw, ctx->aff_qh, ctx->n_qimg ? ctx->bwh.p : nullptr,
+                         ctx->aff_xf, ctx->aff_yf, ctx->aff_thr, 1 << 30, nullptr, ctx->surv.p,
+                         ctx->fvotes.p, ctx->params.p, ctx->alive.p, ctx->scal.p);
+  }
+  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "guard re-run failed");
+  (void)hipStreamSynchronize(ctx->stream);
+  sod_release(dq);
+  sod_release(dk);
+  sod_release(dxy);
+  SOD_TRY(rc);
+  if (ctx->side_pending) {   // the re-done PoseBin means: joined like every result read
+    SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+    ctx->side_pending = false;
+    ctx->means_waited = ctx->means_id;
+  }
+  ctx->guard_patched = changed;
+  ctx->guard_patched_total += changed;
+  ctx->guard_done = true;
   return SOD_OK;
 }
 

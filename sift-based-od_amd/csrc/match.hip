@@ -164,11 +164,19 @@ __device__ __forceinline__ Frag read_frag(const uint8_t* sb, int u, int lane) {
   return f;
 }
 
+// kFind = false: the k=2 search.  kFind = true: the second neighbour's trainIdx for the
+// BFMatcher.knnMatch drop-in -- the same pass over the DB, looking for the LOWEST row other
+// than idx1 whose exact value dn - 2 q.d equals the known second-best one (cd2 - |q|^2):
+// OpenCV's strict-'<' insertion keeps the lowest trainIdx among equal distances, so that row
+// is its n.trainIdx.  Rows are found per lane in increasing order, then min-merged over the
+// lanes and (atomicMin) over the DB splits into idx2[q].
+template <bool kFind>
 __global__ __launch_bounds__(NT, 2) void match_kernel(
     const uint8_t* __restrict__ dbpack, const float* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const float* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
-    int* __restrict__ pidx, float* __restrict__ pd2) {
+    int* __restrict__ pidx, float* __restrict__ pd2, const float* __restrict__ cd2,
+    const int* __restrict__ cidx, int* __restrict__ idx2) {
   // ONE __shared__ array (a second one can make hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageSlot];
 
@@ -205,6 +213,14 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
     v1[t] = kInit;
     v2[t] = kInit;
     id[t] = 0x7fffffff;
+    if constexpr (kFind) {   // v2 = the target value, v1 = the excluded row (idx1)
+      const int qt = qt0 + t;
+      const int64_t q = (int64_t)qt * 16 + (lane & 15);
+      if (qt < nqt && cd2[q] < 1.0e29f) {   // no second row: padding norm -> nothing to find
+        v2[t] = cd2[q] - qn[q];             // integers < 2^24: exact
+        v1[t] = __int_as_float(cidx[q]);
+      }
+    }
   }
 
   for (int64_t s = 0; s < nst; ++s) {
@@ -236,6 +252,25 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
       for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.a2, bq[t][2], acc[t], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < QT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.a3, bq[t][3], acc[t], 0, 0, 0);
+      if constexpr (kFind) {
+        bool any = false;
+#pragma unroll
+        for (int t = 0; t < QT; ++t)
+          any |= (acc[t][0] == v2[t]) | (acc[t][1] == v2[t]) | (acc[t][2] == v2[t]) |
+                 (acc[t][3] == v2[t]);
+        if (__any(any)) {
+          const int rowb = row_offset + (int)((s_lo + s * SPS + u) * kSubRows) + (lane >> 4) * 4;
+#pragma unroll
+          for (int t = 0; t < QT; ++t) {
+#pragma unroll
+            for (int r = 3; r >= 0; --r) {   // the lowest matching row of the four wins
+              const bool eq = (acc[t][r] == v2[t]) && (rowb + r != __float_as_int(v1[t]));
+              id[t] = (eq && rowb + r < id[t]) ? rowb + r : id[t];
+            }
+          }
+        }
+        continue;
+      }
       // prefilter: can any of this lane's 4 x QT candidates beat its running 2nd best?
       bool hit[QT];
       bool any = false;
@@ -264,6 +299,17 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
     }
   }
 
+  if constexpr (kFind) {
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+#pragma unroll
+      for (int m = 16; m <= 32; m <<= 1) id[t] = min(id[t], __shfl_xor(id[t], m));
+      const int qt = qt0 + t;
+      if (lane < 16 && qt < nqt && id[t] != 0x7fffffff)
+        atomicMin(&idx2[(int64_t)qt * 16 + lane], id[t]);
+    }
+    return;
+  }
   // merge the 4 row groups of each query (lanes l, l^16, l^32, l^48)
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
@@ -426,15 +472,35 @@ int launch_match(sod_ctx* ctx) {
   int32_t* pidx;
   SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
   SOD_TRY(sod_match_mark(ctx, ks, 0));
-  hipLaunchKernelGGL(match_kernel, dim3((unsigned)grid), dim3(NT), 0, ks,
+  hipLaunchKernelGGL(match_kernel<false>, dim3((unsigned)grid), dim3(NT), 0, ks,
                      ctx->dbpack.p, ctx->dn.p, ctx->nsub, ctx->qpack.p, ctx->qn.p, ctx->nqt,
-                     nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset, pd1, pidx, pd2);
+                     nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset, pd1, pidx, pd2,
+                     nullptr, nullptr, nullptr);
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(sod_match_mark(ctx, ks, 1));
   SOD_TRY(sod_match_stream_end(ctx));
   SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, nullptr,
                        ctx->nranks <= 1 && !ctx->comm));
   return sod_partials_merged(ctx);   // the slot is free again
+}
+
+// the second neighbour's trainIdx of every query after a bf16 match (kFind pass): idx2 is
+// [nq_pad], set to 0x7f7f7f7f first (no row found stays that)
+int launch_second_index(sod_ctx* ctx, int32_t* idx2) {
+  const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
+  const int64_t qblocks = ceil_div(ctx->nqt, NW * QT);
+  const int64_t nstages = ctx->nsub / SPS;
+  int64_t split = std::max<int64_t>(1, 2LL * ctx->match_cus() / qblocks);
+  split = std::min<int64_t>(split, nstages);
+  const int64_t st_per_split = ceil_div(nstages, split);
+  split = ceil_div(nstages, st_per_split);
+  SOD_HIP(ctx, hipMemsetAsync(idx2, 0x7f, (size_t)nq_pad * 4, ctx->stream));
+  hipLaunchKernelGGL(match_kernel<true>, dim3((unsigned)(qblocks * split)), dim3(NT), 0,
+                     ctx->stream, ctx->dbpack.p, ctx->dn.p, ctx->nsub, ctx->qpack.p, ctx->qn.p,
+                     ctx->nqt, nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset,
+                     nullptr, nullptr, nullptr, ctx->cd2.p, ctx->cidx.p, idx2);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
 }
 
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2, int nparts,

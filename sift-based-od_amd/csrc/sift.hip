@@ -29,8 +29,16 @@
 
 namespace {
 
-#ifndef SOD_SIFT_LANE_ORDER
-#define SOD_SIFT_LANE_ORDER 1   // histogram adds by a whole wave, same-bin lanes in lane order
+// Histogram adds (orientation and descriptor): by a whole wave with same-bin lanes applied
+// in lane order (wave_order, fast) or by one lane per sample in sample order (ordered, the
+// fallback).  The first relies on a property gfx950 shows but does not document -- the
+// same-address lanes of one ds_add_f32 are applied in lane order -- so it is compiled for
+// gfx950 only and used only after the context's self-check (lds_order_probe_kernel, on the
+// first SIFT call) confirmed it on this device; sod_sift_set_lane_order forces the fallback.
+#if defined(__gfx950__)
+#define SOD_SIFT_WAVE_ORDER_ARCH 1
+#else
+#define SOD_SIFT_WAVE_ORDER_ARCH 0
 #endif
 #ifndef SOD_SIFT_EXP
 #define SOD_SIFT_EXP 0   // timing experiments only (wrong results): 1 no descriptor adds,
@@ -692,7 +700,12 @@ __global__ __launch_bounds__(kOT) void orient_kernel(const float* __restrict__ g
                                                      const Surv* __restrict__ surv,
                                                      const unsigned* __restrict__ nsurv, int cap,
                                                      Kp* __restrict__ kps, unsigned* __restrict__ nkp,
-                                                     int kcap) {
+                                                     int kcap, int lane_order) {
+#if SOD_SIFT_WAVE_ORDER_ARCH
+  const bool wave_order = lane_order != 0;
+#else
+  const bool wave_order = false;
+#endif
   __shared__ float tmp[kOriBins + 4 + 1];   // + a dummy bin for the padding samples
   __shared__ __attribute__((aligned(16))) int sbin[kOT + 16];
   __shared__ __attribute__((aligned(16))) float sval[kOT + 16];
@@ -741,17 +754,17 @@ __global__ __launch_bounds__(kOT) void orient_kernel(const float* __restrict__ g
         sval[nv + tid] = 0.f;
       }
       __syncthreads();
-#if SOD_SIFT_LANE_ORDER
+      if (wave_order) {
       // wave 0 adds 64 samples per LDS atomic instruction, sample k on lane k: lanes of one
       // ds_add_f32 that hit the same bin are applied in lane order on gfx950 (probed:
-      // tools/lds_atomic_order.hip, 2000 order-sensitive trials), and the instructions of a
-      // wave in program order -- so every bin still sums in OpenCV's sample order
+      // tools/lds_atomic_order.hip, 2000 order-sensitive trials; checked again per context by
+      // lds_order_probe_kernel), and the instructions of a wave in program order -- so every
+      // bin still sums in OpenCV's sample order
       if (tid < 64 && !(SOD_SIFT_EXP & 2)) {
         for (int t0 = 0; t0 < nv; t0 += 64)
           if (t0 + tid < nv) atomicAdd(&temphist[sbin[t0 + tid]], sval[t0 + tid]);
       }
-#else
-      if (tid == 0 && !(SOD_SIFT_EXP & 2)) {
+      } else if (tid == 0 && !(SOD_SIFT_EXP & 2)) {
         for (int t0 = 0; t0 < nv; t0 += 16) {
           int4 b4[4];
           float4 v4[4];
@@ -769,7 +782,6 @@ __global__ __launch_bounds__(kOT) void orient_kernel(const float* __restrict__ g
           }
         }
       }
-#endif
       __syncthreads();
     }
     if (tid == 0) {
@@ -884,7 +896,7 @@ constexpr int kDT = 256;
 __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
                                                          const Kp* __restrict__ sorted,
                                                          const unsigned* __restrict__ nfinal,
-                                                         float* __restrict__ desc) {
+                                                         float* __restrict__ desc, int lane_order) {
   __shared__ float hist[kHistLen + 72];   // + a dummy region for the padding samples
   __shared__ __attribute__((aligned(16))) int sidx[kDT + 16];
   __shared__ __attribute__((aligned(16))) float svalT[8][kDT + 16];
@@ -893,12 +905,15 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
   __shared__ int wcnt[kDT / 64];
   const int tid = threadIdx.x;
   const int nf = (int)*nfinal;
-#if !SOD_SIFT_LANE_ORDER
-  // the eight bins of a sample relative to its first (lanes 0-7)
+#if SOD_SIFT_WAVE_ORDER_ARCH
+  const bool wave_order = lane_order != 0;
+#else
+  const bool wave_order = false;
+#endif
+  // the eight bins of a sample relative to its first (lanes 0-7 of the ordered adds)
   const int off = tid == 0 ? 0 : tid == 1 ? 1 : tid == 2 ? kN + 2 : tid == 3 ? kN + 3
                 : tid == 4 ? (kD + 2) * (kN + 2) : tid == 5 ? (kD + 2) * (kN + 2) + 1
                 : tid == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
-#endif
   for (int id = blockIdx.x; id < nf; id += gridDim.x) {
     const Kp k = sorted[id];
     int octave = k.octave & 255;
@@ -982,7 +997,7 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
         for (int e = 0; e < 8; ++e) svalT[e][nv + tid] = 0.f;
       }
       __syncthreads();
-#if SOD_SIFT_LANE_ORDER
+      if (wave_order) {
       // wave 0 adds 8 samples per LDS atomic instruction: lane 8 s + e carries contribution
       // e of sample s (same-bin lanes apply in lane order = sample order, see orient_kernel)
       if (tid < 64 && !(SOD_SIFT_EXP & 1)) {
@@ -993,8 +1008,7 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
         for (int t0 = 0; t0 < nv; t0 += 8)
           if (t0 + s8 < nv) atomicAdd(&hist[sidx[t0 + s8] + offe], svalT[e][t0 + s8]);
       }
-#else
-      if (tid < 8 && !(SOD_SIFT_EXP & 1)) {
+      } else if (tid < 8 && !(SOD_SIFT_EXP & 1)) {
         // 16 samples' indices and this lane's values read as 128-bit vectors, then the
         // 16 adds (in order, fire-and-forget)
         for (int t0 = 0; t0 < nv; t0 += 16) {
@@ -1014,7 +1028,6 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
           }
         }
       }
-#endif
       __syncthreads();
     }
     // finalize: fold the circular orientation bins, then OpenCV's sequential norms
@@ -1047,6 +1060,25 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
       dst[tid] = (float)(v < 0 ? 0 : v > 255 ? 255 : v);
     }
     __syncthreads();   // LDS reused by the next keypoint
+  }
+}
+
+// Self-check of the property the wave-order histogram adds rely on: one wave's ds_add_f32
+// with same-address lanes, applied in lane order.  Per trial 64 values whose float sum
+// depends on the order (large / small / cancelling magnitudes) go to 1, 2 or 8 LDS
+// addresses with one atomic instruction; the host compares with the lane-order sums.
+__global__ __launch_bounds__(64) void lds_order_probe_kernel(const float* __restrict__ vals,
+                                                             const int* __restrict__ addr,
+                                                             float* __restrict__ out, int trials) {
+  __shared__ float h[8];
+  const int l = threadIdx.x;
+  for (int t = 0; t < trials; ++t) {
+    if (l < 8) h[l] = 0.f;
+    __syncthreads();
+    atomicAdd(&h[addr[t * 64 + l]], vals[t * 64 + l]);
+    __syncthreads();
+    if (l < 8) out[t * 8 + l] = h[l];
+    __syncthreads();
   }
 }
 
@@ -1108,6 +1140,9 @@ struct SiftSlot {
 };
 
 struct SiftWork {
+  // histogram adds: 1 = wave order, 0 = ordered single lane; -1 = not decided yet (the
+  // self-check runs on the first SIFT call); mode = sod_sift_set_lane_order's request
+  int lane_order = -1, lane_mode = -1, probe_ok = -1;
   int L = 3;
   double contrast = 0.04, edge = 10.0, sigma = 1.6;
   int radius[kMaxLayers] = {};
@@ -1179,7 +1214,67 @@ int get_slot(sod_ctx* ctx, SiftWork& W, int i, SiftSlot** out) {
   return SOD_OK;
 }
 
+// lds_order_probe_kernel over 512 trials (a fixed LCG: the same on every run); 1 when every
+// trial came out in lane order, 0 otherwise
+int lds_order_probe(sod_ctx* ctx, int* ok) {
+  constexpr int kTrials = 512;
+  std::vector<float> v((size_t)kTrials * 64);
+  std::vector<int> a((size_t)kTrials * 64);
+  uint32_t st = 12345u;
+  auto rnd = [&st]() { st = st * 1664525u + 1013904223u; return st >> 8; };
+  for (int t = 0; t < kTrials; ++t) {
+    const int nb = t % 3 == 0 ? 1 : t % 3 == 1 ? 2 : 8;
+    for (int l = 0; l < 64; ++l) {
+      const uint32_t k = rnd() % 4;
+      v[(size_t)t * 64 + l] = k == 0 ? 1.0e8f * (rnd() % 2 ? 1.f : -1.f)
+                            : k == 1 ? 1.0f + (float)(rnd() % 1000) * 1e-3f
+                            : k == 2 ? 3.1e-5f * (float)(rnd() % 100) : 7.7e7f;
+      a[(size_t)t * 64 + l] = (int)(rnd() % nb);
+    }
+  }
+  DevBuf<float> dv, dout;
+  DevBuf<int> da;
+  std::vector<float> o((size_t)kTrials * 8);
+  int rc = sod_reserve(ctx, dv, v.size());
+  if (rc == SOD_OK) rc = sod_reserve(ctx, da, a.size());
+  if (rc == SOD_OK) rc = sod_reserve(ctx, dout, o.size());
+  if (rc == SOD_OK && (hipMemcpy(dv.p, v.data(), v.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                       hipMemcpy(da.p, a.data(), a.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+    rc = sod_fail(ctx, SOD_EHIP, "lds order probe upload failed");
+  if (rc == SOD_OK) {
+    hipLaunchKernelGGL(lds_order_probe_kernel, dim3(1), dim3(64), 0, ctx->stream, dv.p, da.p,
+                       dout.p, kTrials);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(o.data(), dout.p, o.size() * 4, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      rc = sod_fail(ctx, SOD_EHIP, "lds order probe failed");
+  }
+  sod_release(dv);
+  sod_release(da);
+  sod_release(dout);
+  SOD_TRY(rc);
+  int good = 1;
+  for (int t = 0; t < kTrials && good; ++t) {
+    float ref[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int l = 0; l < 64; ++l) ref[a[(size_t)t * 64 + l]] += v[(size_t)t * 64 + l];
+    for (int b = 0; b < 8; ++b) good &= o[(size_t)t * 8 + b] == ref[b];
+  }
+  *ok = good;
+  return SOD_OK;
+}
+
+int set_lane_order(sod_ctx* ctx, SiftWork& W) {
+  if (W.lane_order >= 0) return SOD_OK;
+  if (W.probe_ok < 0) {
+    if (ctx->gfx950) SOD_TRY(lds_order_probe(ctx, &W.probe_ok));
+    else W.probe_ok = 0;   // the wave-order adds are compiled for gfx950 only
+  }
+  W.lane_order = (W.lane_mode != 0 && W.probe_ok == 1) ? 1 : 0;
+  return SOD_OK;
+}
+
 int set_kernels(sod_ctx* ctx, SiftWork& W) {
+  SOD_TRY(set_lane_order(ctx, W));
   if (W.kern_ok) return SOD_OK;
   // sig[0] = the base blur sqrt(max(sigma^2 - 4 * 0.5^2, 0.01)) in float (createInitialImage);
   // sig[i] as buildGaussianPyramid (double)
@@ -1310,7 +1405,7 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                      S.cand.p, S.cnt.p, cap, (float)W.contrast, (float)W.edge, (float)W.sigma, S.surv.p,
                      S.cnt.p + 3);
   hipLaunchKernelGGL(orient_kernel, dim3(kOrientGrid), dim3(kOT), 0, st, S.gauss.p, P, S.surv.p,
-                     S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap);
+                     S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap, W.lane_order);
   SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)cap * 4, st));
   SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)cap * 4, st));
   for (int pass = 0; pass < 2; ++pass)
@@ -1319,7 +1414,7 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
   hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, S.kps.p,
                      S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2);
   hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, P, S.sorted.p,
-                     S.cnt.p + 2, S.desc.p);
+                     S.cnt.p + 2, S.desc.p, W.lane_order);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipMemcpyAsync(S.hcnt, S.cnt.p, 16, hipMemcpyDeviceToHost, st));
   return SOD_OK;
@@ -1436,6 +1531,27 @@ int sod_sift_set_params(sod_ctx* ctx, int32_t n_octave_layers, double contrast_t
   W.sigma = sigma;
   W.kern_ok = false;
   W.valid = false;
+  return SOD_OK;
+}
+
+int sod_sift_set_lane_order(sod_ctx* ctx, int mode) {
+  if (!ctx) return SOD_EINVAL;
+  if (mode != -1 && mode != 0) return sod_fail(ctx, SOD_EINVAL, "lane order mode must be -1 or 0");
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  SiftWork& W = *work(ctx);
+  W.lane_mode = mode;
+  W.lane_order = -1;   // decided again (the self-check result is kept)
+  W.valid = false;
+  return SOD_OK;
+}
+
+int sod_sift_lane_order(sod_ctx* ctx, int* active, int* probe_ok) {
+  if (!ctx) return SOD_EINVAL;
+  SOD_HIP(ctx, hipSetDevice(ctx->device));
+  SiftWork& W = *work(ctx);
+  SOD_TRY(set_lane_order(ctx, W));
+  if (active) *active = W.lane_order;
+  if (probe_ok) *probe_ok = W.probe_ok;
   return SOD_OK;
 }
 

@@ -110,6 +110,14 @@ struct sod_ctx {
   DevBuf<double> pose_b;        // the other step parity of pose / msize
   DevBuf<int32_t> msize_b;
   bool houghed = false;
+  // boundary guard (hough.hip): records of the matches whose x / y bin may depend on the
+  // last ulp of cos / sin [nq * 8], their count ([0] appended by pose_kernel, [1] handed over
+  // by hist_kernel); resolved once per Hough launch, before any result is read
+  DevBuf<double> grec;
+  DevBuf<uint32_t> gstat;
+  bool guard_done = true;
+  int64_t guard_flagged = 0, guard_patched = 0;   // the last launch's records / changed bins
+  int64_t guard_flagged_total = 0, guard_patched_total = 0;
 
   // ---- select / CSR / means ----
   DevBuf<uint64_t> selstat;     // look-back words of select_kernel (one per block)
@@ -142,6 +150,8 @@ struct sod_ctx {
   DevBuf<double> params;        // [vmax*6]
   DevBuf<uint8_t> alive;        // [mmax]
   bool affined = false;
+  int32_t aff_qw = 0, aff_qh = 0, aff_thr = 0;   // the last sod_affine_enqueue's arguments
+  double aff_xf = 0.0, aff_yf = 0.0;             // (a guard re-run repeats it)
 
   // ---- post-processing (post.hip) ----
   DevBuf<double> post_m;        // [n*6] bin means
@@ -261,6 +271,7 @@ inline int64_t sod_nq_pad(const sod_ctx* ctx) { return (int64_t)ctx->nqt * (ctx-
 int launch_pack_db(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n);
 int launch_pack_queries(sod_ctx* ctx, const void* dsrc, int dtype, int32_t nq);
 int launch_match(sod_ctx* ctx);
+int launch_second_index(sod_ctx* ctx, int32_t* idx2);
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db);
 int launch_match_i8(sod_ctx* ctx);
 // matcher-input writers call these around their writes; the match launchers around the
@@ -280,6 +291,9 @@ int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float*
                  int nparts, int64_t stride, int32_t* reset = nullptr, bool final_merge = false);
 int launch_ratio(sod_ctx* ctx, double ratio);
 int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi);
+// boundary guard: redo the listed matches' x / y bins with glibc cos / sin and, when one
+// changes, the histogram and every stage after it (call before reading any Hough result)
+int sod_guard_resolve(sod_ctx* ctx);
 int launch_select(sod_ctx* ctx, int32_t thr);
 int launch_all_bins(sod_ctx* ctx);
 int launch_affine_gather(sod_ctx* ctx);
@@ -294,6 +308,9 @@ int launch_bin_index_batch(sod_ctx* ctx, int64_t n, const double* pose, int32_t*
 int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
                       const float* ma, const int32_t* mo, const float* qx, const float* qy,
                       const float* qa, const int32_t* qo, const double* cx, const double* cy,
-                      double* pose, int32_t* idx);
+                      double* pose, int32_t* idx, double* grec, uint32_t* gstat);
+// host side of the boundary guard: one record's x, y (glibc cos / sin) and x / y bin index
+void sod_guard_host_pose(const double rec[8], const int32_t bins[4], double* x, double* y,
+                         int32_t* ix, int32_t* iy);
 int sod_build_sigma_lut(sod_ctx* ctx, int32_t bins_sigma);
 void sod_sift_free(sod_ctx* ctx);

@@ -58,7 +58,14 @@ def ratio_match(des_query, des_train, ratio=0.75, ctx=None):
 
 
 class BFMatcher:
-    """``cv2.BFMatcher(normType=NORM_L2, crossCheck=False)``: brute force, L2 only."""
+    """``cv2.BFMatcher(normType=NORM_L2, crossCheck=False)``: brute force, L2 only.
+
+    ``knnMatch(k=2)`` returns both DMatch objects complete, the second one's ``trainIdx``
+    included (OpenCV fills it; main.py:81-86 reads only its distance): the lowest trainIdx
+    other than the first's at the second-best distance, which is what OpenCV's strict-'<'
+    k=2 insertion keeps.  That index comes from a second MFMA pass over the DB
+    (``sod_match_second_get``, bf16 matcher), so this object runs on a bf16 context of its
+    own unless one is given."""
 
     def __init__(self, normType=NORM_L2, crossCheck=False, ctx=None):
         if normType != NORM_L2:
@@ -67,21 +74,31 @@ class BFMatcher:
             raise NotImplementedError("crossCheck is not used by the reference")
         self._ctx = ctx
 
+    def _context(self):
+        if self._ctx is None:
+            self._ctx = _lib.Context(0)
+            self._ctx.set_impl("bf16")
+        return self._ctx
+
     def knnMatch(self, queryDescriptors, trainDescriptors, k=2):
         if k not in (1, 2):
             raise NotImplementedError("k must be 1 or 2 (main.py uses k=2)")
-        ntrain = np.asarray(trainDescriptors).shape[0]
+        q = np.asarray(queryDescriptors)
+        d = np.asarray(trainDescriptors)
+        ntrain = d.shape[0]
         if ntrain == 0:   # OpenCV: no neighbours for any query
-            return [[] for _ in range(np.asarray(queryDescriptors).shape[0])]
-        idx1, d1, d2 = knn2(queryDescriptors, trainDescriptors, self._ctx)
-        out = []
+            return [[] for _ in range(q.shape[0])]
+        if q.shape[0] == 0:
+            return []
+        ctx = self._context()
+        ctx.set_impl("bf16")
+        ctx.upload_db(d)
+        ctx.upload_queries(q)
+        ctx.match()
+        ctx.ratio(0.75)
+        idx1, d1, d2, _ = ctx.match_result()
         if k == 1 or ntrain == 1:
-            for q in range(len(idx1)):
-                out.append([DMatch(q, int(idx1[q]), 0, float(d1[q]))])
-            return out
-        # the second neighbour's index is never read by main.py (main.py:81-86); the
-        # kernel keeps only its distance, so trainIdx is -1 here
-        for q in range(len(idx1)):
-            out.append([DMatch(q, int(idx1[q]), 0, float(d1[q])),
-                        DMatch(q, -1, 0, float(d2[q]))])
-        return out
+            return [[DMatch(i, int(idx1[i]), 0, float(d1[i]))] for i in range(len(idx1))]
+        idx2 = ctx.second_index()
+        return [[DMatch(i, int(idx1[i]), 0, float(d1[i])),
+                 DMatch(i, int(idx2[i]), 0, float(d2[i]))] for i in range(len(idx1))]

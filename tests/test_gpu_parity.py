@@ -108,6 +108,34 @@ def test_matcher_query_tiles_shared_thresholds(ctx, monkeypatch, qt):
     assert np.array_equal(good, orc.ratio_test(f1, f2))
 
 
+@pytest.mark.parametrize("case", ["edges", "dups"])
+def test_knnmatch_second_train_idx(case):
+    """BFMatcher.knnMatch returns OpenCV's full pair: n.trainIdx = the lowest trainIdx other
+    than m's at the second-best distance (sod_match_second_get), against the oracle; exact
+    duplicate rows make the ties (inside one DB split and across splits)."""
+    from sift_based_od_amd.matcher import BFMatcher
+    if case == "edges":
+        g = golden("matcher_edges")
+        q, db = g["q_des"], g["db_des"]
+    else:
+        rng = np.random.default_rng(17)
+        db = synthetic.sift_like_descriptors(rng, 70000)
+        db[60000:60500] = db[100:600]              # twins far apart (other DB splits)
+        db[30000:30100] = db[100:200]              # triplets
+        db[101] = db[100]                          # twins next to each other
+        q = synthetic.sift_like_descriptors(rng, 1500)
+        q[:500] = db[100:600]                      # d1 == d2 == 0
+        q[500:1000] = np.clip(db[100:600].astype(int) + rng.integers(-2, 3, (500, 128)), 0, 255)
+    bf = BFMatcher()
+    res = bf.knnMatch(q.astype(np.float32), db.astype(np.float32), k=2)
+    i1, e1, e2, i2 = orc.knn2_match(q, db, with_idx2=True)
+    assert [m.trainIdx for m, _ in res] == i1.tolist()
+    assert [n.trainIdx for _, n in res] == i2.tolist()
+    assert np.array_equal(np.array([m.distance for m, _ in res], np.float32), e1)
+    assert np.array_equal(np.array([n.distance for _, n in res], np.float32), e2)
+    assert all(m.queryIdx == i and n.queryIdx == i for i, (m, n) in enumerate(res))
+
+
 @pytest.mark.parametrize("impl", IMPLS)
 def test_matcher_f32_input_and_validation(ctx, impl):
     rng = np.random.default_rng(11)
@@ -138,6 +166,25 @@ def test_pose_sweep(ctx):
         np.testing.assert_allclose(pose, g["poses"], rtol=1e-13, atol=1e-10)
         # alpha and scale use no transcendental: bit-exact
         assert np.array_equal(pose[:, 2:], g["poses"][:, 2:])
+
+
+def test_pose_near_edge_guard(ctx):
+    """Poses within a few ulps of an x AND a y bin edge (make_golden.near_edge_sweep): the
+    boundary guard lists every one, redoes x, y with the host's libm cos / sin, so indices AND
+    x, y equal the reference's bit for bit (without it, an index follows the device's last
+    ulp of cos / sin)."""
+    g = golden("near_edge_sweep")
+    shape = tuple(int(v) for v in g["shape"])
+    for b in g["bins"]:
+        f = {k: g["b%d_%s" % (b, k)] for k in ("mx", "my", "ma", "mo", "qx", "qy", "qa", "qo",
+                                                "cx", "cy", "poses", "idx")}
+        pose, idx = ctx.pose_batch(f["mx"], f["my"], f["ma"], f["mo"], f["qx"], f["qy"], f["qa"],
+                                   f["qo"], f["cx"], f["cy"], shape, int(b))
+        flagged, changed, _, _ = ctx.guard_stats()
+        assert flagged == len(f["mx"])
+        assert np.array_equal(idx, f["idx"])
+        assert np.array_equal(pose.view(np.uint64), f["poses"].view(np.uint64))
+        print("bins %d: %d listed, %d bins changed by the guard" % (b, flagged, changed))
 
 
 def _check_hough(ctx, g):
@@ -174,7 +221,7 @@ def test_pipeline_golden(ctx, name, impl):
     _check_hough(ctx, g)
 
 
-@pytest.mark.parametrize("name", ["edge_b15", "edge_b6"])
+@pytest.mark.parametrize("name", ["edge_b15", "edge_b6", "near_edge_b15", "near_edge_b32"])
 def test_hough_affine_edges(ctx, name):
     g = golden(name)
     ctx.set_keypoints(kp(g, "db_"), g["db_img"], g["centroid"], g["size"])
@@ -189,6 +236,12 @@ def test_hough_affine_edges(ctx, name):
     ctx.select(5)
     ctx.affine((shape[1], shape[0]), 128.0, 128.0, 4)
     _check_hough(ctx, g)
+    flagged, changed, _, _ = ctx.guard_stats()
+    if name.startswith("near_edge"):      # every match sits on an x and a y edge
+        assert flagged == len(g["match_q"])
+        print("%s: %d listed, %d bins changed by the guard" % (name, flagged, changed))
+    else:
+        assert changed == 0
 
 
 @pytest.mark.parametrize("nq", [40000, 530000])

@@ -26,6 +26,22 @@ def test_pose_sweep_bit_exact():
             assert orc.calculate_bin_index(p, int(b), shape) == tuple(g["idx"][j][i])
 
 
+def test_near_edge_sweep_bit_exact():
+    """Poses within a few ulps of an x and a y bin edge (the boundary guard's cases)."""
+    g = golden("near_edge_sweep")
+    shape = tuple(int(v) for v in g["shape"])
+    for b in g["bins"]:
+        f = {k: g["b%d_%s" % (b, k)] for k in ("mx", "my", "ma", "mo", "qx", "qy", "qa", "qo",
+                                                "cx", "cy", "poses", "idx")}
+        for i in range(len(f["mx"])):
+            p = orc.estimate_object_pose(float(f["mx"][i]), float(f["my"][i]), float(f["ma"][i]),
+                                         int(f["mo"][i]), float(f["qx"][i]), float(f["qy"][i]),
+                                         float(f["qa"][i]), int(f["qo"][i]), float(f["cx"][i]),
+                                         float(f["cy"][i]))
+            assert p == tuple(f["poses"][i]), i
+            assert orc.calculate_bin_index(p, int(b), shape) == tuple(f["idx"][i])
+
+
 def test_per_axis_bins_reduce_to_scalar():
     g = golden("pose_sweep")
     shape = tuple(int(v) for v in g["shape"])
@@ -83,7 +99,7 @@ def test_matcher_and_pipeline_golden(name):
     _run_case(g)
 
 
-@pytest.mark.parametrize("name", ["edge_b15", "edge_b6"])
+@pytest.mark.parametrize("name", ["edge_b15", "edge_b6", "near_edge_b15", "near_edge_b32"])
 def test_edges_golden(name):
     g = golden(name)
     matches = list(zip(g["match_q"].tolist(), g["match_m"].tolist()))
@@ -98,6 +114,17 @@ def test_matcher_edges_golden():
     # ties keep the lowest trainIdx (rows 20, 150, 151 are identical)
     assert (idx1[:10] == 20).all() and (d1[:10] == 0).all() and (d2[:10] == 0).all()
     assert not orc.ratio_test(d1, d2)[:10].any()
+
+
+def test_matcher_second_index_two_ways():
+    """knnMatch's n.trainIdx: the GEMM restatement and the int64 brute force agree on the
+    second neighbour's index, ties included (rows 20 / 150 / 151 are identical)."""
+    g = golden("matcher_edges")
+    a = orc.knn2_match(g["q_des"], g["db_des"], with_idx2=True)
+    b = orc.knn2_match_int(g["q_des"], g["db_des"], with_idx2=True)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert (a[3][:10] == 150).all()          # d1 == d2 == 0: the next-lowest equal row
 
 
 def test_matcher_needs_two_rows():

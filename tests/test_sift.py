@@ -139,6 +139,29 @@ def test_sift_parity_images(ctx):
 
 
 @pytest.mark.gpu
+def test_sift_lane_order_paths(ctx):
+    """Both histogram-add paths bit-exact against the C oracle on the reference's images
+    (their orientation / descriptor bins collide inside one wave all the time, so the sums
+    are order-sensitive): the ordered single-lane adds (forced) and the automatic choice,
+    which is the wave adds only when the device self-check held."""
+    imgs = _images()
+    active, probe = ctx.sift_lane_order()
+    assert probe in (0, 1)
+    assert active == probe               # auto mode: wave adds exactly when the check held
+    print("LDS lane-order self-check:", "held" if probe else "FAILED (ordered adds in use)")
+    try:
+        ctx.sift_set_lane_order(0)
+        assert ctx.sift_lane_order() == (0, probe)
+        for name, img in imgs.items():
+            _assert_same(ctx.sift_detect(img), osift.detect_and_compute(img), name + "/ordered")
+    finally:
+        ctx.sift_set_lane_order(-1)
+    assert ctx.sift_lane_order() == (probe, probe)
+    for name, img in imgs.items():
+        _assert_same(ctx.sift_detect(img), osift.detect_and_compute(img), name + "/auto")
+
+
+@pytest.mark.gpu
 def test_sift_parity_edges(ctx):
     imgs = {"blank": np.full((64, 64), 128, np.uint8), "tiny": np.zeros((8, 8), np.uint8),
             "one": np.zeros((1, 1), np.uint8),
