@@ -51,6 +51,9 @@ CONFIGS = {
     "c3": (50000, 1000, 1000, (32, 32, 8, 12), True),
     "c2": (10000, 100, 1000, (15, 15, 15, 15), False),
     "c5": (50000, 1000, 1000, (32, 32, 8, 12), True),
+    # C4 / C5's whole 8M-row DB on ONE GPU (1.1 GB of int8 rows): the matcher's fraction at
+    # the per-job DB size of the 8-GPU configs (not a scaling number)
+    "c4x1": (50000, 8000, 1000, (32, 32, 8, 12), True),
     "tiny": (2000, 20, 1000, (15, 15, 15, 15), True),
 }
 
@@ -101,9 +104,9 @@ def parse():
 
 
 class Dist:
-    """torch.distributed (gloo, host side) for rendezvous, barriers, the RCCL unique-id
-    broadcast and the max-over-ranks of the timings.  The data path uses RCCL inside
-    libsod; torch is only this plumbing."""
+    """Rendezvous, barriers, the RCCL unique-id broadcast and the max over ranks through
+    sharded.FileStore (the ranks of one node share a directory; standard library only).
+    The data path uses RCCL inside libsod."""
 
     def __init__(self, n):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,51 +115,27 @@ class Dist:
         if self.world != n:
             if n != 1 or self.world != 1:
                 raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (n, self.world))
-        self.pg = None
+        self.store = None
         if self.world > 1:
-            import torch.distributed as dist
-            dist.init_process_group("gloo")
-            self.dist = dist
+            from sift_based_od_amd.sharded import FileStore
+            self.store = FileStore(self.world, self.rank)
 
     def barrier(self):
-        if self.world > 1:
-            self.dist.barrier()
+        if self.store:
+            self.store.barrier()
 
     def bcast_bytes(self, b):
-        if self.world == 1:
-            return b
-        import torch
-        t = torch.zeros(len(b) if b is not None else _lib.UNIQUE_ID_BYTES, dtype=torch.uint8)
-        if self.rank == 0:
-            t[:] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
-        self.dist.broadcast(t, 0)
-        return bytes(t.numpy().tobytes())
+        return self.store.broadcast_bytes(b) if self.store else b
 
     def max(self, x):
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return self.store.max(x) if self.store else x
 
     def sum(self, x):
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return self.store.sum(x) if self.store else x
 
-
-def device_sync(world, dev):
-    # the whole step runs on libsod's own streams (ctx.synchronize() waits for them); with
-    # several ranks torch is loaded anyway and a device-wide sync of THIS rank's GPU is added
-    # on top (torch's default device 0 would open a context on GPU 0 in every rank)
-    if world > 1:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.synchronize(dev)
+    def close(self):
+        if self.store:
+            self.store.close()
 
 
 def cpu_baseline(queries, db_des, nq_sample):
@@ -292,6 +271,62 @@ def sift_extras(c, bins, n_batch=16, h=800, w=1000):
             "image_to_pose_images_per_s": n_batch / (t_e2e / 1000.0)}
 
 
+def main_path_extras(dev, impl, c3_data):
+    """main.py's stage-by-stage driver (pipeline.Main: run_matcher ->
+    apply_hough_transform -> get_valid_bins -> apply_affine_parameters -> post_process, the
+    calls main.py:182-186 makes, PoseBin objects materialised lazily) timed at C1, C2 and
+    C3 beside the fused one-enqueue ``Main.run`` on the same inputs (host wall clock per
+    call, outside the timed region).  C3 reuses the bench's DB and queries."""
+    from sift_based_od_amd import Main, SiftDatabase
+    out = {}
+    cases = {
+        "C1": lambda: (synthetic.make_database(1, 500, seed=0),
+                       synthetic.make_queries(500, seed=1, db_seed=0, kp_per_image=500,
+                                              n_objects=1), 15),
+        "C2": lambda: (synthetic.make_database(100, 1000, seed=0),
+                       synthetic.make_queries(10000, seed=1, db_seed=0, kp_per_image=1000), 15),
+        "C3": lambda: c3_data,
+    }
+    for name, make in cases.items():
+        db, qs, bins = make()
+        c = _lib.Context(dev)
+        c.set_impl(impl)
+        m = Main(c)
+        m.set_database(SiftDatabase(db.des, db.kp, db.img, db.centroid, db.size))
+        m.get_query_features(qs.des, qs.kp, qs.shape)
+        stages = {}
+
+        def staged():
+            t = {}
+            for k, fn in (("run_matcher", m.run_matcher),
+                          ("apply_hough_transform", lambda: m.apply_hough_transform(bins)),
+                          ("get_valid_bins", lambda: m.get_valid_bins(5)),
+                          ("apply_affine_parameters", lambda: m.apply_affine_parameters(4)),
+                          ("post_process", m.post_process)):
+                t0 = time.perf_counter()
+                fn()
+                t[k] = (time.perf_counter() - t0) * 1000.0
+            c.synchronize()
+            m.valid_bins = []      # main.py builds a new Main per image
+            return t
+        staged()                   # warm-up (code objects, buffers)
+        reps = 3
+        for _ in range(reps):
+            for k, v in staged().items():
+                stages[k] = stages.get(k, 0.0) + v / reps
+        m.run(bins)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            m.run(bins)
+        fused = (time.perf_counter() - t0) * 1000.0 / reps
+        out[name] = {"queries": len(qs.des), "db_rows": len(db.des), "bins": bins,
+                     "stage_ms": stages, "staged_total_ms": sum(stages.values()),
+                     "fused_run_ms": fused, "affine_path": m.affine_path,
+                     "surviving_bins": len(m.valid_bins) if m.valid_bins else None}
+        c.close()
+    return out
+
+
 def cpu_sift_baseline(h=800, w=1000):
     """oracle/sift_oracle.c (C, one thread) on the same 1000 x 800 image."""
     from oracle import sift as osift
@@ -350,9 +385,7 @@ def main():
 
     dev = D.local
     if world > 1:
-        import torch
-        ndev = max(1, torch.cuda.device_count())   # counting does not initialise HIP
-        dev = D.local % ndev                       # >1 rank per GPU only with --comm host
+        dev = D.local % max(1, _lib.device_count())   # >1 rank per GPU only with --comm host
     ctx = _lib.Context(dev)
     ctx.set_impl(a.impl)
     kernel, dtype, peak, peak_unit = IMPLS[a.impl]
@@ -361,7 +394,7 @@ def main():
     n_shard = shard.shape[0]
     ctx.upload_db(shard, row_offset=rank * n_shard)
     ctx.upload_queries(qs.des, qs.kp)
-    from sift_based_od_amd.sharded import RcclComm, TorchHostComm, run_sharded
+    from sift_based_od_amd.sharded import FileHostComm, RcclComm, run_sharded
     # auto: split the chip for the int8 matcher from 1e9 pairs per GPU up (C3 / C5: ~3.8 ms
     # against a ~0.8 ms tail on the 8 reserved CUs; C2: 0.209 vs 0.218 ms per step with two
     # contexts, measured; 2 reserved CUs per XCD 0.258 ms)
@@ -379,7 +412,7 @@ def main():
         # reserved CU count (8 * reserve), so every block of an RCCL kernel is resident at once
         comm = RcclComm(ctx, world, rank, D.bcast_bytes)
     elif world > 1:
-        comm = TorchHostComm()
+        comm = FileHostComm(D.store)
     own = (rank * n_shard, (rank + 1) * n_shard)
     ncontexts = a.contexts if a.contexts > 0 else (2 if world == 1 and not overlap else 1)
     ctxs = [ctx]
@@ -415,7 +448,6 @@ def main():
     stage = []
     D.barrier()
     sync_all()
-    device_sync(world, dev)
     t0 = time.perf_counter()
     host = 0.0                      # host time spent enqueueing (the calls return unsynced)
     for _ in range(a.steps):
@@ -423,7 +455,6 @@ def main():
         step()
         host += time.perf_counter() - h0
     sync_all()
-    device_sync(world, dev)
     D.barrier()
     t1 = time.perf_counter()
     el = D.max(t1 - t0)
@@ -449,8 +480,18 @@ def main():
         stage.append(ctx.stage_ms())
     match_iso = float(np.mean(match_iso))
     stage = np.mean(np.array(stage), axis=0)
+    stage_full = None
     if reserve:
         ctx.set_cu_reserve(0)      # post-processing and extras below on the whole chip
+        # the same stages on the whole chip (the timed run keeps them on the reserved CUs,
+        # beside the next query's matcher)
+        full = []
+        for _ in range(5):
+            turn[0] = 0
+            step()
+            ctx.synchronize()
+            full.append(ctx.stage_ms())
+        stage_full = np.mean(np.array(full), axis=0)
 
     # post-processing (main.py:159-168) over the surviving bins: timed
     # separately (it ends in a host DFS, so it is not inside the stream-ordered step)
@@ -468,6 +509,29 @@ def main():
     aff = ctx.affine_result() if run_affine else None
     idx1, d1, d2, good = ctx.match_result()
 
+    # Hough stage roofline: algorithmic bytes 52 per good match (query kp 16 +
+    # model kp 16 + idx 4 + centroid 16) + 4 per bin (the count written out) over the
+    # device time of pose_kernel + hist_kernel (stage events)
+    n_good = int(good.sum())
+    nbins = int(np.prod(bins))
+    hough_bytes = 52 * n_good + 4 * nbins
+    t_hough = float(stage[2])
+    t_hough_full = float(stage_full[2]) if stage_full is not None else t_hough
+    roofline_hough = {
+        "bound": "hbm", "achieved": hough_bytes / (t_hough * 1e-3) / 1e9, "peak": 8000.0,
+        "unit": "GB/s", "frac": hough_bytes / (t_hough * 1e-3) / 1e9 / 8000.0, "traffic": None,
+        "algorithmic_bytes": hough_bytes, "kernels": "pose_kernel + hist_kernel",
+        "stage_ms": t_hough,
+        "cus": 8 * reserve if reserve else "all",
+        "whole_chip": {"stage_ms": t_hough_full,
+                       "achieved": hough_bytes / (t_hough_full * 1e-3) / 1e9,
+                       "frac": hough_bytes / (t_hough_full * 1e-3) / 1e9 / 8000.0},
+        "note": "latency-bound, not bandwidth-bound: %d good matches and %d bins move %.1f MB; "
+                "the two launches (their fixed cost and one pass of dependent loads / LDS "
+                "atomics per work-group) set the time%s" % (
+                    n_good, nbins, hough_bytes / 1e6,
+                    ", here on the %d CUs the CU split reserves for the tail" % (8 * reserve)
+                    if reserve else "")}
     pmc, traffic_src = pmc_traffic(kernel, a.config)
     traffic = pmc.get("hbm_bytes") if pmc else None
     pairs = float(world) * nq * n_shard
@@ -500,14 +564,19 @@ def main():
             "cu_reserve_per_xcd": reserve,
             "comm": a.comm if world > 1 else None},
         "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
-        "hough_stage_votes_per_s": n_votes / ((float(stage[2]) + float(stage[3])) / 1000.0),
+        "hough_stage_votes_per_s": n_votes / (t_hough / 1000.0),
         "hough_votes": n_votes,
         "good_matches": int(good.sum()),
         "valid_bins": V,
         "surviving_bins": int(aff["survived"].sum()) if aff else None,
-        "stage_ms": {"match_kernel": match_ms, "match_kernel_isolated": match_iso, "merge_gather_ratio": float(stage[1]),
-                     "hough_vote": float(stage[2]), "select": float(stage[3]),
-                     "affine": float(stage[4]), "post_process": post_ms},
+        # device time of each stage's own launches (sod_last_stage_ms: per rank, host waits
+        # between the calls excluded), isolated steps after the timed region
+        "stage_ms": dict({"match_kernel": match_ms, "match_kernel_isolated": match_iso},
+                         **{k: float(v) for k, v in zip(_lib.Context.STAGES[1:], stage[1:])},
+                         post_process=post_ms),
+        "stage_ms_whole_chip": ({k: float(v) for k, v in zip(_lib.Context.STAGES, stage_full)}
+                                if stage_full is not None else None),
+        "roofline_hough": roofline_hough,
         "final_poses": int(len(post["final_pose"])) if post is not None else None,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
                      "unit": peak_unit, "frac": achieved / peak, "traffic": traffic,
@@ -540,6 +609,10 @@ def main():
             ec.set_impl(a.impl)
             ec.share_db(ctx)
         out["extras"] = extras(ec, ctx, shard, bins)
+        if a.config in ("c3", "c5"):
+            from sift_based_od_amd import SiftDatabase
+            c3db = SiftDatabase(shard, Keypoints(x, y, ang, octv), img, cent, size)
+            out["extras"]["main_path"] = main_path_extras(dev, a.impl, (c3db, qs, bins))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(qs.des, shard, a.cpu_queries)
         out["cpu_baseline_hough"] = cpu_hough_baseline(qs, (x, y, ang, octv), img, cent, size,
@@ -555,8 +628,7 @@ def main():
     for c in ctxs[1:]:
         c.close()
     ctx.close()
-    if world > 1:
-        D.dist.destroy_process_group()
+    D.close()
 
 
 if __name__ == "__main__":

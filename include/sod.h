@@ -45,6 +45,8 @@ typedef struct sod_ctx sod_ctx;
 
 /* ---- lifetime --------------------------------------------------------------------- */
 int sod_abi_version(void);
+/* HIP devices visible to this process (a launcher maps one rank to each). */
+int sod_device_count(int* n);
 int sod_create(int device, sod_ctx** out);
 void sod_destroy(sod_ctx* ctx);
 const char* sod_last_error(const sod_ctx* ctx);
@@ -56,7 +58,13 @@ int sod_last_match_ms(sod_ctx* ctx, float* ms);
  * so far), from begin/end HIP events recorded on the matcher's stream around each launch:
  * the kernel timed inside a pipelined run.  Waits for those launches. */
 int sod_match_times(sod_ctx* ctx, int n, float* ms);
-int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n); /* match,merge,hough,select,affine */
+/* Device time (ms) of each stage of the last step (since the last sod_match_enqueue /
+ * sod_matches_set), from begin / end events recorded on the stream around the stage's own
+ * launches -- host work and waits between two calls (a host-staged exchange, other ranks)
+ * are not counted: [0 matcher kernel, 1 merge + ratio kernels, 2 Hough pose + vote,
+ * 3 select + members (+ PoseBin means fork), 4 affine, 5 all-reduce of the bin counts (or
+ * the host exchange's upload), 6 all-gather of the candidates (or its upload)]. */
+int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n);
 /* Stage events (the bounds sod_last_stage_ms reads) on (1, the default) or off (0): each is
  * a marker packet on the tail's critical path, so a timed loop turns them off.  With them
  * off, sod_last_stage_ms reports 0 for the stages after the matcher. */

@@ -41,6 +41,7 @@ class PipelineArgs(C.Structure):
 # name -> (restype, argtypes); must mirror include/sod.h exactly (tests check the symbols)
 SIGNATURES = {
     "sod_abi_version": (C.c_int, []),
+    "sod_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "sod_create": (C.c_int, [C.c_int, C.POINTER(c_ctx)]),
     "sod_destroy": (None, [c_ctx]),
     "sod_last_error": (C.c_char_p, [c_ctx]),
@@ -392,9 +393,14 @@ class Context:
         """Record the per-stage events read by stage_ms (default on; off in timed loops)."""
         self._chk(self._L.sod_set_stage_timing(self._h, 1 if on else 0))
 
+    STAGES = ("match_kernel", "merge_ratio", "hough_vote", "select", "affine", "allreduce",
+              "allgather")
+
     def stage_ms(self):
-        out = np.zeros(5, np.float32)
-        self._chk(self._L.sod_last_stage_ms(self._h, ptr(out, C.c_float), 5))
+        """Device time (ms) of each stage's own launches in the last step, in STAGES order
+        (sod_last_stage_ms): host work and waits between the calls are not counted."""
+        out = np.zeros(len(self.STAGES), np.float32)
+        self._chk(self._L.sod_last_stage_ms(self._h, ptr(out, C.c_float), len(out)))
         return out
 
     # -- stateless batch forms --
@@ -660,6 +666,15 @@ def bins4(bins):
 
 
 _default = {}
+
+
+def device_count():
+    """HIP devices visible to this process (sod_device_count)."""
+    n = C.c_int()
+    rc = lib().sod_device_count(C.byref(n))
+    if rc != SOD_OK:
+        raise SodError(rc, lib().sod_last_error(None).decode())
+    return n.value
 
 
 def default_context(device=0):

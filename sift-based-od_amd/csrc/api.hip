@@ -189,9 +189,37 @@ static int db_writable(sod_ctx* ctx) {
   return SOD_OK;
 }
 
+// ---- stage segments (sod_last_stage_ms) ---------------------------------------------
+int sod_stage_mark(sod_ctx* ctx, int stage, bool end) {
+  if (!ctx->stage_timing) return SOD_OK;
+  if (!end) {
+    if (ctx->nseg >= sod_ctx::kSegs) return SOD_OK;   // a step of more segments: the rest uncounted
+    hipEvent_t* e = ctx->seg_ev[ctx->nseg];
+    for (int k = 0; k < 2; ++k)
+      if (!e[k]) SOD_HIP(ctx, hipEventCreate(&e[k]));
+    ctx->seg_stage[ctx->nseg] = stage;
+    SOD_HIP(ctx, hipEventRecord(e[0], ctx->stream));
+    ctx->nseg++;
+  } else if (ctx->nseg > 0 && ctx->seg_stage[ctx->nseg - 1] == stage) {
+    SOD_HIP(ctx, hipEventRecord(ctx->seg_ev[ctx->nseg - 1][1], ctx->stream));
+  }
+  return SOD_OK;
+}
+
 extern "C" {
 
 int sod_abi_version(void) { return 1; }
+
+int sod_device_count(int* n) {
+  if (!n) return SOD_EINVAL;
+  const hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) {
+    g_err = std::string("hipGetDeviceCount: ") + hipGetErrorString(e);
+    *n = 0;
+    return SOD_EHIP;
+  }
+  return SOD_OK;
+}
 
 int sod_create(int device, sod_ctx** out) {
   if (!out) return SOD_EINVAL;
@@ -280,6 +308,9 @@ void sod_destroy(sod_ctx* ctx) {
   for (auto& pr : ctx->mev)
     for (auto& e : pr)
       if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->seg_ev)
+    for (auto& x : e)
+      if (x) (void)hipEventDestroy(x);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   for (int i = 0; i < 2; ++i) {
@@ -336,30 +367,29 @@ int sod_set_stage_timing(sod_ctx* ctx, int on) {
 }
 
 int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n) {
-  // [match kernel, merge+allgather+ratio, hough vote (+allreduce), select, affine]
+  // [match kernel, merge + ratio, hough vote, select (+ members, means), affine, all-reduce
+  //  (or the host exchange's upload), all-gather (or its upload)]: device time of each
+  // stage's own launches in the last step
   SOD_TRY(set_dev(ctx));
-  if (!ms_out) return sod_fail(ctx, SOD_EINVAL, "null output");
+  if (!ms_out || n < 0) return sod_fail(ctx, SOD_EINVAL, "null output");
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  const bool st = ctx->stage_timing;
-  const bool rec[6] = {ctx->matched, ctx->matched, st && ctx->houghed, st && ctx->houghed,
-                       st && ctx->selected, st && ctx->affined};
-  // the last matcher launch's begin / end events (sod_match_events, or sod_match_mark on
-  // the bf16 path) bound stages 0 and 1
-  hipEvent_t evs[6];
-  for (int i = 0; i < 6; ++i) evs[i] = ctx->ev[i];
-  if (ctx->nmatch > 0) {
+  float acc[kStages] = {};
+  if (ctx->matched && ctx->nmatch > 0) {   // the last matcher launch's own begin / end events
     hipEvent_t* m = ctx->mev[(ctx->nmatch - 1) % sod_ctx::kMatchRing];
-    evs[0] = m[0];
-    evs[1] = m[1];
-  }
-  for (int i = 0; i < n && i < 5; ++i) {
-    float ms = 0.f;
-    if (rec[i] && rec[i + 1] && hipEventElapsedTime(&ms, evs[i], evs[i + 1]) != hipSuccess) {
-      ms = 0.f;
+    if (hipEventElapsedTime(&acc[kStageMatch], m[0], m[1]) != hipSuccess) {
+      acc[kStageMatch] = 0.f;
       (void)hipGetLastError();   // not sticky: the next launch check must not see it
     }
-    ms_out[i] = ms;
   }
+  for (int i = 0; i < ctx->nseg; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->seg_ev[i][0], ctx->seg_ev[i][1]) != hipSuccess) {
+      ms = 0.f;
+      (void)hipGetLastError();
+    }
+    acc[ctx->seg_stage[i]] += ms;
+  }
+  for (int i = 0; i < n; ++i) ms_out[i] = i < kStages ? acc[i] : 0.f;
   return SOD_OK;
 }
 
@@ -652,6 +682,7 @@ int sod_match_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
   ctx->ratio_fused_valid = false;   // set again by a final merge that applies the pipeline's ratio
+  ctx->nseg = 0;                    // a new step for sod_last_stage_ms
   SOD_TRY(ctx->impl != 0 ? launch_match_i8(ctx) : launch_match(ctx));
   ctx->matched = true;
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
@@ -770,6 +801,7 @@ int sod_match_allgather_enqueue(sod_ctx* ctx) {
   SOD_TRY(sod_reserve(ctx, ctx->gd1, tot));
   SOD_TRY(sod_reserve(ctx, ctx->gd2, tot));
   SOD_TRY(sod_reserve(ctx, ctx->gidx, tot));
+  SOD_TRY(sod_stage_mark(ctx, kStageAllgather, false));
   ncclResult_t r = ncclGroupStart();
   if (r == ncclSuccess) r = ncclAllGather(ctx->cd1.p, ctx->gd1.p, nq_pad, ncclFloat32, ctx->comm, ctx->stream);
   if (r == ncclSuccess) r = ncclAllGather(ctx->cidx.p, ctx->gidx.p, nq_pad, ncclInt32, ctx->comm, ctx->stream);
@@ -778,9 +810,12 @@ int sod_match_allgather_enqueue(sod_ctx* ctx) {
   if (r != ncclSuccess || r2 != ncclSuccess)
     return sod_fail(ctx, SOD_ECOMM, std::string("ncclAllGather: ") +
                                         ncclGetErrorString(r != ncclSuccess ? r : r2));
+  SOD_TRY(sod_stage_mark(ctx, kStageAllgather, true));
   // global merge in rank order (lexicographic on (d^2, trainIdx): order-independent anyway)
-  return launch_merge(ctx, ctx->gd1.p, ctx->gidx.p, ctx->gd2.p, ctx->nranks, (int64_t)nq_pad,
-                      nullptr, true);   // the global merge: final
+  SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
+  SOD_TRY(launch_merge(ctx, ctx->gd1.p, ctx->gidx.p, ctx->gd2.p, ctx->nranks, (int64_t)nq_pad,
+                       nullptr, true));   // the global merge: final
+  return sod_stage_mark(ctx, kStageMerge, true);
 }
 
 int sod_ratio_enqueue(sod_ctx* ctx, double ratio) {
@@ -789,7 +824,11 @@ int sod_ratio_enqueue(sod_ctx* ctx, double ratio) {
   if (!(ratio >= 0.0) || !std::isfinite(ratio))
     return sod_fail(ctx, SOD_EINVAL, "ratio must be a finite number >= 0");
   // skipped only when the final merge of this very launch applied this very ratio
-  if (!ctx->ratio_fused_valid || ctx->ratio_fused != ratio) SOD_TRY(launch_ratio(ctx, ratio));
+  if (!ctx->ratio_fused_valid || ctx->ratio_fused != ratio) {
+    SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
+    SOD_TRY(launch_ratio(ctx, ratio));
+    SOD_TRY(sod_stage_mark(ctx, kStageMerge, true));
+  }
   ctx->ratio_done = true;
   return SOD_OK;
 }
@@ -845,6 +884,7 @@ int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t
   SOD_HIP(ctx, hipMemsetAsync(ctx->d2.p, 0, (size_t)nq * 4, ctx->stream));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->ratio_fused_valid = false;
+  ctx->nseg = 0;
   ctx->matched = ctx->ratio_done = true;
   ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
@@ -879,9 +919,9 @@ int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int3
   }
   ctx->qh = query_h;
   ctx->qw = query_w;
-  if (ctx->stage_timing) SOD_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+  SOD_TRY(sod_stage_mark(ctx, kStageHough, false));
   SOD_TRY(launch_hough(ctx, own_lo, own_hi));
-  if (ctx->stage_timing) SOD_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+  SOD_TRY(sod_stage_mark(ctx, kStageHough, true));
   ctx->houghed = true;
   ctx->selected = ctx->affined = false;
   return SOD_OK;
@@ -892,12 +932,14 @@ int sod_hough_allreduce_enqueue(sod_ctx* ctx) {
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
   if (ctx->nranks <= 1 && !ctx->comm) return SOD_OK;   // a 1-rank communicator still runs
   if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
+  SOD_TRY(sod_stage_mark(ctx, kStageAllreduce, false));
   ncclResult_t r = ncclGroupStart();
   if (r == ncclSuccess)
     r = ncclAllReduce(ctx->counts.p, ctx->counts.p, ctx->nbins, ncclUint32, ncclSum, ctx->comm, ctx->stream);
   if (r == ncclSuccess)
     r = ncclAllReduce(ctx->first.p, ctx->first.p, ctx->nbins, ncclUint32, ncclMin, ctx->comm, ctx->stream);
   ncclResult_t r2 = ncclGroupEnd();
+  SOD_TRY(sod_stage_mark(ctx, kStageAllreduce, true));
   if (r != ncclSuccess || r2 != ncclSuccess)
     return sod_fail(ctx, SOD_ECOMM, std::string("ncclAllReduce: ") +
                                         ncclGetErrorString(r != ncclSuccess ? r : r2));
@@ -907,8 +949,9 @@ int sod_hough_allreduce_enqueue(sod_ctx* ctx) {
 int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold) {
   SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  SOD_TRY(sod_stage_mark(ctx, kStageSelect, false));
   SOD_TRY(launch_select(ctx, vote_threshold));
-  if (ctx->stage_timing) SOD_HIP(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+  SOD_TRY(sod_stage_mark(ctx, kStageSelect, true));
   ctx->vote_thr = vote_threshold;
   ctx->selected = true;
   ctx->affined = false;
@@ -1005,6 +1048,7 @@ int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_
   ctx->aff_xf = x_factor;
   ctx->aff_yf = y_factor;
   ctx->aff_thr = threshold;
+  SOD_TRY(sod_stage_mark(ctx, kStageAffine, false));
   SOD_TRY(launch_affine_gather(ctx));
   SOD_TRY(sod_reserve(ctx, ctx->surv, (size_t)ctx->vmax));
   SOD_TRY(sod_reserve(ctx, ctx->fvotes, (size_t)ctx->vmax));
@@ -1015,7 +1059,7 @@ int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_
                         x_factor, y_factor, threshold, 1 << 30,
                         nullptr, ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p,
                         ctx->scal.p));
-  if (ctx->stage_timing) SOD_HIP(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+  SOD_TRY(sod_stage_mark(ctx, kStageAffine, true));
   ctx->affined = true;
   return SOD_OK;
 }
@@ -1213,10 +1257,14 @@ int sod_match_candidates_merge(sod_ctx* ctx, int32_t nparts, const float* d1sq,
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
   if (nparts < 1 || !d1sq || !idx || !d2sq) return sod_fail(ctx, SOD_EINVAL, "bad arguments");
   const size_t n = (size_t)ctx->nq, tot = n * (size_t)nparts;
+  SOD_TRY(sod_stage_mark(ctx, kStageAllgather, false));
   SOD_TRY(upload(ctx, ctx->gd1, d1sq, tot));
   SOD_TRY(upload(ctx, ctx->gidx, idx, tot));
   SOD_TRY(upload(ctx, ctx->gd2, d2sq, tot));
+  SOD_TRY(sod_stage_mark(ctx, kStageAllgather, true));
+  SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
   SOD_TRY(launch_merge(ctx, ctx->gd1.p, ctx->gidx.p, ctx->gd2.p, nparts, (int64_t)n));
+  SOD_TRY(sod_stage_mark(ctx, kStageMerge, true));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
@@ -1235,8 +1283,10 @@ int sod_hough_partial_set(sod_ctx* ctx, const uint32_t* counts, const uint32_t* 
   SOD_TRY(set_dev(ctx));
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
   if (!counts || !first) return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  SOD_TRY(sod_stage_mark(ctx, kStageAllreduce, false));
   SOD_HIP(ctx, hipMemcpyAsync(ctx->counts.p, counts, ctx->nbins * 4, hipMemcpyHostToDevice, ctx->stream));
   SOD_HIP(ctx, hipMemcpyAsync(ctx->first.p, first, ctx->nbins * 4, hipMemcpyHostToDevice, ctx->stream));
+  SOD_TRY(sod_stage_mark(ctx, kStageAllreduce, true));
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->selected = ctx->affined = false;
   return SOD_OK;

@@ -479,8 +479,10 @@ int launch_match(sod_ctx* ctx) {
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(sod_match_mark(ctx, ks, 1));
   SOD_TRY(sod_match_stream_end(ctx));
+  SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
   SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, nullptr,
                        ctx->nranks <= 1 && !ctx->comm));
+  SOD_TRY(sod_stage_mark(ctx, kStageMerge, true));
   return sod_partials_merged(ctx);   // the slot is free again
 }
 

@@ -205,6 +205,14 @@ struct sod_ctx {
   int64_t pslot_n = 0;          // its size (elements per array)
 
   // ---- timing ----
+  // per-stage device time of the last step (sod_last_stage_ms): begin / end events recorded
+  // on the context stream around each stage's own launches, so host work and waits between
+  // two calls (a host exchange, the other ranks) are not counted; segments of one stage add
+  // up; a step starts at sod_match_enqueue / sod_matches_set
+  static constexpr int kSegs = 24;
+  hipEvent_t seg_ev[kSegs][2] = {};
+  int seg_stage[kSegs] = {};
+  int nseg = 0;
   hipEvent_t ev[8] = {};
   // begin/end events of the last kMatchRing matcher launches (sod_match_times), so the
   // kernel is timed inside a pipelined run, not only in isolated launches
@@ -270,6 +278,10 @@ inline int64_t sod_win0(const sod_ctx* ctx) { return ctx->winn < 0 ? 0 : ctx->wi
 inline int64_t sod_nq_pad(const sod_ctx* ctx) { return (int64_t)ctx->nqt * (ctx->impl == 2 ? 32 : kSubRows); }
 int launch_pack_db(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n);
 int launch_pack_queries(sod_ctx* ctx, const void* dsrc, int dtype, int32_t nq);
+// stage segments (api.hip): kStage* ids; mark(begin) ... mark(end) around a stage's launches
+enum { kStageMatch = 0, kStageMerge = 1, kStageHough = 2, kStageSelect = 3, kStageAffine = 4,
+       kStageAllreduce = 5, kStageAllgather = 6, kStages = 7 };
+int sod_stage_mark(sod_ctx* ctx, int stage, bool end);
 int launch_match(sod_ctx* ctx);
 int launch_second_index(sod_ctx* ctx, int32_t* idx2);
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db);

@@ -56,23 +56,26 @@ def calculate_bin_index(object_pose, bins, query_image_shape, ctx=None):
     return int(idx[0]), int(idx[1]), int(idx[2]), int(idx[3])
 
 
-def posebins_from_device(res, pair_of, size_of=None):
+def posebins_from_device(res, pair_of, size_of=None, token=None):
     """PoseBin objects from a device selection (``Context.valid_result()``): ``pair_of(q)``
-    returns the (kpM, kpQ) pair of member query ``q``; ``size_of(q)`` the model image size
-    (ints) used when a bin has a single vote (the reference keeps the int tuple then)."""
+    returns the (kpM, kpQ) pair of member query ``q``, called only when a bin's
+    ``keypoint_pairs`` is first read (the members stay device arrays until then);
+    ``size_of(q)`` the model image size (ints) used when a bin has a single vote (the
+    reference keeps the int tuple then).  ``token`` names the device selection the bins
+    are bound to (``PoseBin.bind_device``)."""
     out = []
     keys, votes, off, mem, means = (res["keys"], res["votes"], res["offsets"], res["members"],
                                     res["means"])
     for i in range(len(keys)):
         m = mem[off[i]:off[i + 1]]
-        pairs = [pair_of(int(q)) for q in m]
         mu = means[i]
         if votes[i] == 1 and size_of is not None:
             size = size_of(int(m[0]))
         else:
             size = (float(mu[4]), float(mu[5]))
-        b = PoseBin(tuple(int(v) for v in keys[i]), size, int(votes[i]), pairs,
+        b = PoseBin(tuple(int(v) for v in keys[i]), size, int(votes[i]), None,
                     (float(mu[0]), float(mu[1]), float(mu[2]), float(mu[3])))
+        b.bind_device(token, i, m, pair_of)
         out.append(b)
     return out
 

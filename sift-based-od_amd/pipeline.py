@@ -54,6 +54,10 @@ class Main:
         self.keypoint_pairs = []
         self.final_pose = []
         self._stage = None
+        self._sel_token = 0            # device selections made (PoseBin.bind_device)
+        self._valid_sel = None         # (token, valid_result) of get_valid_bins' selection
+        self._tuple_ctx = None         # context of the tuple-given Hough path (reused)
+        self.affine_path = None        # how the last apply_affine_parameters ran
 
     # ---------------------------------------------------------------- inputs
     def set_database(self, db):
@@ -151,9 +155,11 @@ class Main:
         self._hough_bins = bins
         self._table = None
         if self._stage == "assigned":
-            # tuples set by the caller: vote over them as given
-            self._tuple_ctx, self._tuple_bins = hough_table_from_tuples(
-                self._matching, shape, bins, 1, _lib.Context(self.ctx.device))
+            # tuples set by the caller: vote over them as given (on a second context, kept)
+            if self._tuple_ctx is None:
+                self._tuple_ctx = _lib.Context(self.ctx.device)
+            _, self._tuple_bins = hough_table_from_tuples(self._matching, shape, bins, 1,
+                                                          self._tuple_ctx)
             self._table = {b.pose: b for b in self._tuple_bins}
             return
         self.ctx.hough(shape, bins)
@@ -164,9 +170,9 @@ class Main:
         if self._table is None:
             if self._hough_bins is None:
                 return {}
-            self.ctx.select(1)
-            res = self.ctx.valid_result()
-            self._table = {b.pose: b for b in posebins_from_device(res, self._pair, self._size_of)}
+            res = self._select(1)
+            self._table = {b.pose: b for b in posebins_from_device(res, self._pair, self._size_of,
+                                                                   self._sel_token)}
             self._selected_thr = 1
         return self._table
 
@@ -178,36 +184,77 @@ class Main:
         im = int(self.db.img[m])
         return (int(self.db.size[im][0]), int(self.db.size[im][1]))
 
+    def _select(self, threshold):
+        self.ctx.select(threshold)
+        self._sel_token += 1
+        return self.ctx.valid_result()
+
     def get_valid_bins(self, threshold=5):
-        """``main.py:121-132``: bins with votes >= threshold, insertion order."""
-        self.keypoint_pairs = []
+        """``main.py:121-132``: bins with votes >= threshold, insertion order.  The bins'
+        members stay on the device (``keypoint_pairs`` is built when first read), and so
+        does ``self.keypoint_pairs`` (a lazy concatenation)."""
         if self._stage == "assigned":
             vb = [b for b in self._table.values() if b.votes >= threshold]
         else:
-            self.ctx.select(threshold)
-            res = self.ctx.valid_result()
+            res = self._select(threshold)
+            tok = self._sel_token
+            off, mem = res["offsets"], res["members"]
             if self._table is not None:
                 vb = [self._table[tuple(int(v) for v in k)] for k in res["keys"]]
+                for i, b in enumerate(vb):
+                    b.bind_device(tok, i, mem[off[i]:off[i + 1]], self._pair)
             else:
-                vb = posebins_from_device(res, self._pair, self._size_of)
+                vb = posebins_from_device(res, self._pair, self._size_of, tok)
+            self._valid_sel = (tok, res)
+        # main.py:131's `not in` scan, by pose (PoseBin.__eq__) through a set: O(V)
+        seen = {b.pose for b in self.valid_bins}
         for b in vb:
-            self.keypoint_pairs.extend(b.keypoint_pairs)
-            if b not in self.valid_bins:
+            if b.pose not in seen:
+                seen.add(b.pose)
                 self.valid_bins.append(b)
+        self.keypoint_pairs = _LazyPairs(self.valid_bins)
         self._valid_thr = threshold
 
     def update_keypoint_pairs(self):
-        """``main.py:134-137``."""
-        self.keypoint_pairs.clear()
-        for posebin in self.valid_bins:
-            self.keypoint_pairs.extend(posebin.keypoint_pairs)
+        """``main.py:134-137`` (the concatenation is built when first read)."""
+        self.keypoint_pairs = _LazyPairs(self.valid_bins)
+
+    def _device_resident(self):
+        """True when ``valid_bins`` is exactly the device's current selection, in its order,
+        and no bin was edited by the caller (members, votes, pose): the affine stage can then
+        run on the members already on the device."""
+        if self._valid_sel is None or self._stage == "assigned":
+            return False
+        tok, res = self._valid_sel
+        if tok != self._sel_token or len(self.valid_bins) != len(res["keys"]):
+            return False
+        return all(b.device_index(tok) == i for i, b in enumerate(self.valid_bins))
 
     def apply_affine_parameters(self, threshold=4):
         """``main.py:139-157``: per-bin fixed point of {AffineParameters;
-        remove_outliers} with factor pos_factor*4, on the device (all bins at once)."""
-        from .affine import verify_bins
-        self.valid_bins = verify_bins(self.valid_bins, self.image_query_size, threshold,
-                                      POS_FACTOR * 4, POS_FACTOR * 4, self.ctx)
+        remove_outliers} with factor pos_factor*4, on the device (all bins at once).  When
+        the valid bins are the device's selection, untouched, the kernel runs on the
+        members resident there (no host gather / upload); otherwise on the bins' own
+        keypoint pairs."""
+        if self._device_resident():
+            self.ctx.affine(self.image_query_size, POS_FACTOR * 4, POS_FACTOR * 4, threshold)
+            a = self.ctx.affine_result()
+            off = self._valid_sel[1]["offsets"]
+            out = []
+            for i, b in enumerate(self.valid_bins):
+                b.keep_device_members(a["alive"][off[i]:off[i + 1]])
+                b.votes = int(a["votes"][i])
+                b.affine_parameters = [float(v) for v in a["params"][i]]
+                if a["survived"][i]:
+                    out.append(b)
+            self.valid_bins = out
+            self._valid_sel = None
+            self.affine_path = "device-resident"
+        else:
+            from .affine import verify_bins
+            self.valid_bins = verify_bins(self.valid_bins, self.image_query_size, threshold,
+                                          POS_FACTOR * 4, POS_FACTOR * 4, self.ctx)
+            self.affine_path = "host-pairs"
         self.update_keypoint_pairs()
 
     def post_process(self):
@@ -239,6 +286,36 @@ class Main:
         self._match = (idx1, good)
         self._hough_bins = bins
         return out
+
+
+class _LazyPairs(list):
+    """``Main.keypoint_pairs`` (main.py:134-137): the valid bins' pairs concatenated, built
+    on first use, so the pairs stay on the device until someone reads them."""
+
+    def __init__(self, bins):
+        super().__init__()
+        self._bins = list(bins)
+        self._built = False
+
+    def _build(self):
+        if not self._built:
+            self._built = True
+            for b in self._bins:
+                super().extend(b.keypoint_pairs)
+
+    for _m in ("__len__", "__getitem__", "__iter__", "__contains__", "__repr__", "__eq__",
+               "__reversed__", "index", "count", "copy", "__add__", "__mul__"):
+        def _f(self, *a, _m=_m, **k):
+            self._build()
+            return getattr(list, _m)(self, *a, **k)
+        locals()[_m] = _f
+    for _m in ("append", "extend", "insert", "remove", "pop", "clear", "sort", "reverse",
+               "__setitem__", "__delitem__", "__iadd__"):
+        def _g(self, *a, _m=_m, **k):
+            self._build()
+            return getattr(list, _m)(self, *a, **k)
+        locals()[_m] = _g
+    del _m, _f, _g
 
 
 class _LazyKeypoints:

@@ -40,11 +40,67 @@ class PoseBin:
                  mean=(0, 0, 0, 0)):
         # the reference's default `keypoint_pairs=[]` is one list shared by every bin
         # built without pairs; main.py always passes its own list, so a fresh one is kept
+        self._lazy = None       # (pair_of, member query indices): pairs built on first read
+        self._dev = None        # device binding, see bind_device
         self.keypoint_pairs = [] if keypoint_pairs is None else keypoint_pairs
         self.pose, self.img_size, self.votes = pose, img_size, votes
         self.centroid = (mean[0], mean[1])
         self.angle, self.scale = mean[2], mean[3]
         self.affine_parameters = []
+
+    # ---- members resident on the device (pipeline.Main) ---------------------------------
+    @property
+    def keypoint_pairs(self):
+        if self._lazy is not None:
+            pair_of, members = self._lazy
+            self._lazy = None
+            self._pairs = [pair_of(int(q)) for q in members]
+            if self._dev is not None:          # what the device holds, to detect edits
+                self._dev = self._dev[:3] + (list(self._pairs),)
+        return self._pairs
+
+    @keypoint_pairs.setter
+    def keypoint_pairs(self, pairs):
+        self._pairs = pairs
+        self._lazy = None
+        self._dev = None        # the caller's own list: the device copy no longer applies
+
+    def bind_device(self, token, index, members, pair_of):
+        """The bin is valid bin ``index`` of the device selection ``token`` with member
+        queries ``members``; its keypoint pairs are built from them on first read."""
+        if self._dev is None and self._lazy is None and self._pairs:
+            snap = list(self._pairs)           # already built: keep the objects
+        else:
+            snap = None
+            self._pairs = []
+            self._lazy = (pair_of, members)
+        self._dev = (token, index, members, snap)
+        self._dev_pose, self._dev_votes = self.pose, len(members)
+
+    def device_index(self, token):
+        """The bin's index in device selection ``token`` when the device copy still equals
+        the bin (members, votes, pose unchanged by the caller), else None."""
+        d = self._dev
+        if d is None or d[0] != token or self.pose != self._dev_pose or self.votes != self._dev_votes:
+            return None
+        if self._lazy is None:                 # built: still exactly those objects?
+            snap = d[3]
+            if snap is None or len(snap) != len(self._pairs) or any(
+                    a is not b for a, b in zip(snap, self._pairs)):
+                return None
+        return d[1]
+
+    def keep_device_members(self, alive):
+        """After a device step on the bound members (the affine outlier removal): keep the
+        members where ``alive`` (bool, member order) -- built objects stay the same objects,
+        unbuilt ones stay lazy."""
+        _, _, members, snap = self._dev
+        alive = np.asarray(alive, bool)
+        if self._lazy is None:
+            self._pairs = [p for p, k in zip(self._pairs, alive) if k]
+        else:
+            self._lazy = (self._lazy[0], np.asarray(members)[alive])
+        self._dev = None
 
     # ---- per-vote updates (PoseBin.py:19-54) --------------------------------------------
     def update_centroid(self, center):

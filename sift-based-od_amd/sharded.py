@@ -19,8 +19,12 @@ Two communicators carry the two exchanges:
 * :class:`RcclComm` -- RCCL over xGMI inside libsod (device buffers, the ctx stream);
   the production path.
 * :class:`HostComm` -- the same exchanges staged through host memory over any object
-  providing ``allgather``/``allreduce`` of numpy arrays (``TorchHostComm`` wraps a
-  torch.distributed gloo group); used where RCCL is unavailable and by the CPU tests.
+  providing ``allgather``/``allreduce`` of numpy arrays (``FileHostComm`` over the
+  stdlib :class:`FileStore` of one node; ``TorchHostComm`` wraps a torch.distributed gloo
+  group for the CPU tests); used where RCCL is unavailable.
+
+The bootstrap (RCCL unique id, barriers, max over ranks) needs nothing but the standard
+library: :class:`FileStore`.
 
 ``run_sharded`` drives either one with the same code, so the multi-rank logic tested
 with gloo on the CPU is the logic the GPUs run.
@@ -77,8 +81,111 @@ class HostComm:
         ctx.set_hough_partial(cnt, fst)
 
 
+class FileStore:
+    """Rendezvous of the ranks of ONE node through a directory (stdlib only): the RCCL
+    unique-id broadcast, barriers, all-gathers of small byte strings.  Keys are files
+    written to a temporary name and renamed into place (atomic), readers poll.
+
+    ``path`` defaults to ``$TMPDIR/sod_store_<MASTER_PORT>_<parent pid>``: the ranks a
+    launcher (torchrun's agent) started share their parent, so a run never meets an older
+    run's files.  ``close()`` removes the directory once every rank is done with it."""
+
+    def __init__(self, world, rank, path=None, timeout=600.0):
+        import os
+        import tempfile
+        self.world, self.rank, self.timeout = world, rank, timeout
+        if path is None:
+            path = os.path.join(tempfile.gettempdir(), "sod_store_%s_%d" % (
+                os.environ.get("MASTER_PORT", "0"), os.getppid()))
+        self.path = path
+        os.makedirs(path, exist_ok=True)
+        self._seq = 0
+
+    def _file(self, key):
+        import os
+        return os.path.join(self.path, key)
+
+    def set(self, key, data):
+        import os
+        tmp = self._file(".%s.%d.tmp" % (key, self.rank))
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, self._file(key))
+
+    def get(self, key):
+        import os
+        import time
+        f = self._file(key)
+        t0 = time.perf_counter()
+        spin = 0
+        while not os.path.exists(f):
+            spin += 1
+            if spin > 200:              # tight for ~the first ms (barriers in timed regions)
+                time.sleep(1e-4)
+            if time.perf_counter() - t0 > self.timeout:
+                raise TimeoutError("FileStore: rank %d waited %.0f s for %s"
+                                   % (self.rank, self.timeout, key))
+        with open(f, "rb") as fh:
+            return fh.read()
+
+    def allgather_bytes(self, data):
+        k = self._seq
+        self._seq += 1
+        self.set("g%d_%d" % (k, self.rank), data)
+        return [self.get("g%d_%d" % (k, r)) for r in range(self.world)]
+
+    def barrier(self):
+        self.allgather_bytes(b"")
+
+    def broadcast_bytes(self, data):
+        """rank 0's bytes on every rank (``data`` is ignored elsewhere)."""
+        k = self._seq
+        self._seq += 1
+        if self.rank == 0:
+            self.set("b%d" % k, data)
+            return data
+        return self.get("b%d" % k)
+
+    def max(self, x):
+        import struct
+        return max(struct.unpack("<d", b)[0] for b in self.allgather_bytes(struct.pack("<d", x)))
+
+    def sum(self, x):
+        import struct
+        return sum(struct.unpack("<d", b)[0] for b in self.allgather_bytes(struct.pack("<d", x)))
+
+    def close(self):
+        import shutil
+        self.barrier()                   # every rank has read everything it will read
+        self.set("done_%d" % self.rank, b"")
+        if self.rank == 0:
+            for r in range(self.world):
+                self.get("done_%d" % r)
+            shutil.rmtree(self.path, ignore_errors=True)
+
+
+class FileHostComm(HostComm):
+    """HostComm over a :class:`FileStore` (no torch, no MPI): the host-staged exchanges of
+    ranks that cannot use RCCL (e.g. several ranks sharing one GPU)."""
+
+    def __init__(self, store):
+        def allgather(a):
+            a = np.ascontiguousarray(a)
+            return [np.frombuffer(b, a.dtype).reshape(a.shape)
+                    for b in store.allgather_bytes(a.tobytes())]
+
+        def allreduce(a, op):
+            parts = allgather(a)
+            out = parts[0].copy()
+            for p in parts[1:]:
+                out = out + p if op == "sum" else np.minimum(out, p)
+            return out
+
+        super().__init__(store.world, store.rank, allgather, allreduce)
+
+
 class TorchHostComm(HostComm):
-    """HostComm over a torch.distributed process group (gloo)."""
+    """HostComm over a torch.distributed process group (gloo): a test adapter."""
 
     def __init__(self, group=None):
         import torch

@@ -109,6 +109,7 @@ def test_main_stages_match_golden():
         np.testing.assert_allclose([b.centroid[0], b.centroid[1], b.angle, b.scale,
                                     b.img_size[0], b.img_size[1]], mu, rtol=1e-12, atol=1e-9)
     m.apply_affine_parameters(4)
+    assert m.affine_path == "device-resident"
     assert [b.pose for b in m.valid_bins] == [tuple(k) for k in g["surv_keys"]]
     assert [b.votes for b in m.valid_bins] == list(g["surv_votes"])
     for b, prm in zip(m.valid_bins, g["surv_params"]):
@@ -117,6 +118,53 @@ def test_main_stages_match_golden():
     m.post_process()                                   # main.py:186
     got = np.array([[p[0][0], p[0][1], p[1], p[2], p[3][0], p[3][1]] for p in m.final_pose])
     np.testing.assert_allclose(got.reshape(-1, 6), g["final_pose"], rtol=1e-12, atol=1e-9)
+
+
+def _main_on(g):
+    db = sod.SiftDatabase(g["db_des"], kp(g, "db_"), g["db_img"], g["centroid"], g["size"])
+    m = sod.Main()
+    m.set_database(db)
+    m.get_query_features(g["q_des"], kp(g, "q_"), tuple(int(v) for v in g["shape"]))
+    m.run_matcher()
+    m.apply_hough_transform(int(g["bins"]))
+    return m
+
+
+def test_main_device_resident_members():
+    """main.py:121-157 without the PoseBin objects' members ever leaving the device: the
+    valid bins' keypoint pairs are not built until read, the affine stage runs on the
+    resident members, and survivors / votes / parameters / surviving members equal the
+    reference's goldens."""
+    g = golden("planted_b12")
+    m = _main_on(g)
+    m.get_valid_bins(5)
+    assert all(b._lazy is not None for b in m.valid_bins)       # nothing materialised yet
+    m.apply_affine_parameters(4)
+    assert m.affine_path == "device-resident"
+    assert [b.pose for b in m.valid_bins] == [tuple(k) for k in g["surv_keys"]]
+    assert [b.votes for b in m.valid_bins] == list(g["surv_votes"])
+    for k, b in enumerate(m.valid_bins):
+        np.testing.assert_allclose(b.affine_parameters, g["surv_params"][k], rtol=0, atol=1e-4)
+        want = g["surv_members"][g["surv_off"][k]:g["surv_off"][k + 1]]
+        assert [p[1] for p in b.keypoint_pairs] == [m.kp_query[int(q)] for q in want]
+    assert len(m.keypoint_pairs) == int(g["surv_votes"].sum())
+
+
+def test_main_edited_bins_take_the_host_path():
+    """A caller that edits the valid bins (drops a member of one bin) gets the affine stage
+    on the bins' own pairs -- the edit counts; every other bin's outcome is the reference's."""
+    g = golden("planted_b12")
+    m = _main_on(g)
+    m.get_valid_bins(5)
+    edited = m.valid_bins[0]
+    edited.keypoint_pairs.pop()
+    edited.votes -= 1
+    others = [b.pose for b in m.valid_bins[1:]]
+    m.apply_affine_parameters(4)
+    assert m.affine_path == "host-pairs"
+    surv = [tuple(k) for k in g["surv_keys"]]
+    got = [b.pose for b in m.valid_bins if b.pose != edited.pose]
+    assert got == [p for p in surv if p in others]
 
 
 @pytest.mark.parametrize("world", [2, 3])

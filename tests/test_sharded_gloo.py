@@ -80,6 +80,64 @@ def test_sharded_equals_single_rank(tmp_path, world, bins):
         assert np.array_equal(z["surv"], surv)
 
 
+def _file_worker(rank, world, store_path, outdir, bins):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    import sod_pkg
+    sod_pkg.load()
+    from fake_ctx import OracleCtx
+    from sift_based_od_amd.sharded import FileHostComm, FileStore, run_sharded, shard_range
+    store = FileStore(world, rank, path=store_path, timeout=120)
+    # the bootstrap primitives bench.py uses: unique-id broadcast, barrier, max / sum
+    uid = store.broadcast_bytes(b"uid-from-rank-0" if rank == 0 else None)
+    assert uid == b"uid-from-rank-0"
+    store.barrier()
+    assert store.max(float(rank)) == world - 1
+    assert store.sum(1.0) == world
+    db, qs = _case()
+    lo, hi = shard_range(len(db), rank, world)
+    ctx = OracleCtx(db, lo, hi, qs.des, qs.kp)
+    run_sharded(ctx, FileHostComm(store), (lo, hi), qs.shape, bins, 0.75, 5, 4, 128.0, 128.0, True)
+    idx1, d1, d2, good = ctx.match_result()
+    v = ctx.valid_result()
+    surv = np.array([r["survived"] for r in ctx.affine_result()], bool)
+    np.savez(os.path.join(outdir, "f%d.npz" % rank), idx1=idx1, d1=d1, d2=d2, good=good,
+             keys=v["keys"], votes=v["votes"], off=v["offsets"], mem=v["members"], surv=surv)
+    store.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_over_file_store_equals_single_rank(tmp_path, world):
+    """bench.py's torch-free multi-rank plumbing: FileStore bootstrap + FileHostComm
+    exchange between real processes, equal to the single-rank result bit for bit; the
+    store directory is gone after close()."""
+    import multiprocessing as mp
+    bins = 15
+    store_path = str(tmp_path / "store")
+    ctxm = mp.get_context("spawn")
+    procs = [ctxm.Process(target=_file_worker, args=(r, world, store_path, str(tmp_path), bins))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert not os.path.exists(store_path)
+    sys.path.insert(0, HERE)
+    from fake_ctx import OracleCtx
+    from sift_based_od_amd.sharded import HostComm, run_sharded
+    db, qs = _case()
+    ref = OracleCtx(db, 0, len(db), qs.des, qs.kp)
+    run_sharded(ref, HostComm(1, 0, lambda a: [a], lambda a, op: a), (0, len(db)), qs.shape,
+                bins, 0.75, 5, 4, 128.0, 128.0, True)
+    idx1, _, _, good = ref.match_result()
+    v = ref.valid_result()
+    for r in range(world):
+        z = np.load(tmp_path / ("f%d.npz" % r))
+        assert np.array_equal(z["idx1"], idx1) and np.array_equal(z["good"], good)
+        assert np.array_equal(z["keys"], v["keys"]) and np.array_equal(z["mem"], v["members"])
+
+
 def test_single_rank_double_matches_oracle_pipeline():
     """The test double itself agrees with the oracle's end-to-end restatement."""
     sys.path.insert(0, HERE)
