@@ -377,22 +377,64 @@ __global__ void ratio_kernel(const float* __restrict__ cd1, const int* __restric
 
 // per query: the partial top-2 of every DB chunk (or rank) merged; when this is the final
 // merge of a pipeline call (one rank, or the global merge after the all-gather) and ratio >=
-// 0, the ratio test of ratio_kernel is applied in the same pass (one launch fewer)
-__global__ void merge_kernel(const float* __restrict__ d1, const int* __restrict__ idx,
-                             const float* __restrict__ d2, int nparts, int64_t stride, int64_t nq,
-                             float* __restrict__ od1, int* __restrict__ oidx,
-                             float* __restrict__ od2, int* __restrict__ reset, double ratio,
-                             int64_t nq_real, float* __restrict__ rd1, float* __restrict__ rd2,
-                             int* __restrict__ ridx, uint8_t* __restrict__ rgood) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// 0, the ratio test of ratio_kernel is applied in the same pass (one launch fewer).
+// A work-group covers 64 queries (one per lane) with kMergeW waves, wave w merging parts
+// w, w + W, ... (their loads issued 8 at a time, independent of the merges), then the W
+// partial results through LDS: the top-2 merge of disjoint row sets is associative and
+// commutative (lexicographic (d^2, trainIdx) on the best, plain min on the second), so any
+// grouping gives the sequential result bit for bit -- and hundreds of DB chunks (one query
+// image over a large DB) cost a few dependent loads per lane instead of one per chunk.
+constexpr int kMergeW = 16;
+__global__ __launch_bounds__(64 * kMergeW) void merge_kernel(
+    const float* __restrict__ d1, const int* __restrict__ idx, const float* __restrict__ d2,
+    int nparts, int64_t stride, int64_t nq, float* __restrict__ od1, int* __restrict__ oidx,
+    float* __restrict__ od2, int* __restrict__ reset, double ratio, int64_t nq_real,
+    float* __restrict__ rd1, float* __restrict__ rd2, int* __restrict__ ridx,
+    uint8_t* __restrict__ rgood) {
+  __shared__ float s1[kMergeW][64], s2[kMergeW][64];
+  __shared__ int si[kMergeW][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nw = min((int)(blockDim.x >> 6), nparts);
+  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  float v1 = 3.0e38f, v2 = 3.0e38f;
+  int i1 = 0x7fffffff;
+  if (q < nq && w < nw) {
+    v1 = d1[(int64_t)w * stride + q];   // the wave's first part as is (as the sequential merge)
+    i1 = idx[(int64_t)w * stride + q];
+    v2 = d2[(int64_t)w * stride + q];
+    int p = w + nw;
+    for (; p + 7 * nw < nparts; p += 8 * nw) {   // 8 parts' loads in flight
+      float a1[8], a2[8];
+      int ai[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int64_t o = (int64_t)(p + k * nw) * stride + q;
+        a1[k] = d1[o];
+        ai[k] = idx[o];
+        a2[k] = d2[o];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) merge2(v1, i1, v2, a1[k], ai[k], a2[k]);
+    }
+    for (; p < nparts; p += nw) {
+      const int64_t o = (int64_t)p * stride + q;
+      merge2(v1, i1, v2, d1[o], idx[o], d2[o]);
+    }
+  }
+  if (nw > 1) {
+    s1[w][lane] = v1;
+    si[w][lane] = i1;
+    s2[w][lane] = v2;
+    __syncthreads();
+    if (w != 0) return;
+    for (int k = 1; k < nw; ++k) merge2(v1, i1, v2, s1[k][lane], si[k][lane], s2[k][lane]);
+  } else if (w != 0) {
+    return;
+  }
   if (q >= nq) return;
   // the matcher's shared thresholds of this partial-result slot: "nothing known" again for
   // the next launch that takes the slot (it waits for this merge)
   if (reset) reset[q] = (int)0x80808080;
-  float v1 = d1[q], v2 = d2[q];
-  int i1 = idx[q];
-  for (int p = 1; p < nparts; ++p)
-    merge2(v1, i1, v2, d1[p * stride + q], idx[p * stride + q], d2[p * stride + q]);
   od1[q] = v1;
   oidx[q] = i1;
   od2[q] = v2;
@@ -508,7 +550,6 @@ int launch_second_index(sod_ctx* ctx, int32_t* idx2) {
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2, int nparts,
                  int64_t stride, int32_t* reset, bool final_merge) {
   const int64_t nq_pad = sod_nq_pad(ctx);
-  const int bs = 256;
   // sod_pipeline_enqueue announces its ratio: the final merge applies it as well
   const bool fuse = final_merge && ctx->fuse_ratio >= 0.0;
   if (fuse) {
@@ -517,10 +558,12 @@ int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float*
     SOD_TRY(sod_reserve(ctx, ctx->idx1, (size_t)ctx->nq));
     SOD_TRY(sod_reserve(ctx, ctx->good, (size_t)ctx->nq));
   }
-  hipLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, bs)), dim3(bs), 0, ctx->stream,
-                     d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p, ctx->cd2.p, reset,
-                     fuse ? ctx->fuse_ratio : -1.0, (int64_t)ctx->nq, ctx->d1.p, ctx->d2.p,
-                     ctx->idx1.p, ctx->good.p);
+  // waves per 64 queries: one per part up to kMergeW (a few parts: one wave, no LDS step)
+  const int wv = std::max(1, std::min(kMergeW, nparts));
+  hipLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, 64)), dim3(64 * wv), 0,
+                     ctx->stream, d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p,
+                     ctx->cd2.p, reset, fuse ? ctx->fuse_ratio : -1.0, (int64_t)ctx->nq, ctx->d1.p,
+                     ctx->d2.p, ctx->idx1.p, ctx->good.p);
   ctx->ratio_fused_valid = fuse;
   if (fuse) ctx->ratio_fused = ctx->fuse_ratio;
   SOD_HIP(ctx, hipGetLastError());
