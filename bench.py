@@ -54,6 +54,8 @@ CONFIGS = {
     # C4 / C5's whole 8M-row DB on ONE GPU (1.1 GB of int8 rows): the matcher's fraction at
     # the per-job DB size of the 8-GPU configs (not a scaling number)
     "c4x1": (50000, 8000, 1000, (32, 32, 8, 12), True),
+    # main.py's own use (main.py:36-86): ONE query image (~500 keypoints) against the DB
+    "img1": (500, 1000, 1000, (32, 32, 8, 12), True),
     "tiny": (2000, 20, 1000, (15, 15, 15, 15), True),
 }
 
@@ -93,7 +95,7 @@ def parse():
                    help="multi-rank exchange: RCCL on the device (default) or staged "
                         "through host memory over gloo (for >1 rank per GPU)")
     a = p.parse_args()
-    short = a.config in ("c2", "tiny")
+    short = a.config in ("c2", "tiny", "img1")
     if a.steps is None:
         a.steps = 200 if short else 50
     if a.warmup is None:
