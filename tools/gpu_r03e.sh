@@ -14,3 +14,5 @@ for cfg in "500 1000" "10000 100" "50000 1000"; do
   SOD_LIB_PATH=$C timeout -k 10 150 python3 tools/ab_match.py $1 $2 i8 > $O/count_$1.log 2>&1 || { tail -5 $O/count_$1.log; exit 1; }
 done
 grep -h "" $O/*.log | grep -v "^$" | cut -c1-220
+CONFIGS=img500x1M,c2,q2kx1M timeout -k 10 400 python3 -u tools/small_q.py > $O/small_q_qt.log 2> $O/small_q_qt.err || { tail -20 $O/small_q_qt.err; exit 1; }
+head -3 $O/small_q_qt.log | cut -c1-400

@@ -15,6 +15,7 @@ src, dst = sys.argv[1], sys.argv[2]
 kernel_ms = float(sys.argv[3]) if len(sys.argv) > 3 and sys.argv[3] != "-" else None
 kernel = sys.argv[4] if len(sys.argv) > 4 else "match_i8_kernel"
 vals = collections.defaultdict(list)
+gui_clock = []   # per dispatch of the pass that holds GRBM_GUI_ACTIVE: cycles / its own duration
 for sub in sorted(os.listdir(src)):
     f = os.path.join(src, sub, "pmc_counter_collection.csv")
     if not os.path.exists(f):
@@ -22,8 +23,14 @@ for sub in sorted(os.listdir(src)):
     for r in csv.DictReader(open(f)):
         if re.search(r"(^|::|\s)%s\b" % kernel, r["Kernel_Name"]):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and r.get("End_Timestamp"):
+                dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+                if dur > 0:
+                    gui_clock.append(float(r["Counter_Value"]) / 8 / dur / 1e9)
 avg = {k: sum(v) / len(v) for k, v in vals.items()}
 out = {"kernel": kernel, "counters_per_launch": avg}
+if gui_clock:   # the profiled dispatches' own clock (MI355X_MICROARCH.md, DVFS)
+    out["clock_ghz_profiled"] = sum(gui_clock) / len(gui_clock)
 if "FETCH_SIZE" in avg:
     out["hbm_read_bytes"] = 2 * avg["FETCH_SIZE"] * 1024
 if "WRITE_SIZE" in avg:
