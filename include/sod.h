@@ -160,12 +160,13 @@ int sod_match_get(sod_ctx* ctx, int32_t* idx1, float* d1, float* d2, uint8_t* go
  * main.py:29,85): idx1[q] = trainIdx (global row), good[q] = keep.  nq must equal the
  * uploaded query count.  Hough/select/affine then run on these matches. */
 int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t* good);
-/* knnMatch's second DMatch (main.py:71: n.trainIdx, which OpenCV fills although main.py
- * reads only n.distance): per query the lowest trainIdx other than idx1 whose distance is
- * the second-best one -- what OpenCV's strict-'<' k=2 insertion keeps -- found by a second
- * MFMA pass over the DB after a bf16 match (sod_match_set_impl(ctx, 0)); -1 with a
- * single DB row.  Single context (no shards). */
-int sod_match_second_get(sod_ctx* ctx, int32_t* idx2);
+/* knnMatch's trainIdx pair as OpenCV returns it (main.py:71: m.trainIdx, n.trainIdx --
+ * main.py reads only n.distance, but OpenCV fills both).  OpenCV orders by the float
+ * distance sqrtf(d^2) with ties to the lower trainIdx: idx1 = the lowest row at the float
+ * d1 (the matcher's own idx1 whenever every distance is < 2048, sod_match_exact_order),
+ * idx2 = the lowest other row at the float d2 (-1 with a single DB row) -- found by MFMA
+ * passes over the DB after a bf16 match (sod_match_set_impl(ctx, 0)), single context. */
+int sod_match_knn_indices(sod_ctx* ctx, int32_t* idx1, int32_t* idx2);
 /* 1 if every distance is provably < 2048 (sqrtf then injective on the squared
  * distances, so squared-distance ordering == OpenCV's float ordering), else 0. */
 int sod_match_exact_order(sod_ctx* ctx, int* exact);

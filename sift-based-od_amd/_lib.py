@@ -71,7 +71,7 @@ SIGNATURES = {
     "sod_match_get": (C.c_int, [c_ctx, c_i32p, c_f32p, c_f32p, c_u8p]),
     "sod_matches_set": (C.c_int, [c_ctx, C.c_int32, c_i32p, c_u8p]),
     "sod_match_exact_order": (C.c_int, [c_ctx, C.POINTER(C.c_int)]),
-    "sod_match_second_get": (C.c_int, [c_ctx, c_i32p]),
+    "sod_match_knn_indices": (C.c_int, [c_ctx, c_i32p, c_i32p]),
     "sod_hough_enqueue": (C.c_int, [c_ctx, C.c_int32, C.c_int32, c_i32p, C.c_int64, C.c_int64]),
     "sod_hough_allreduce_enqueue": (C.c_int, [c_ctx]),
     "sod_select_enqueue": (C.c_int, [c_ctx, C.c_int32]),
@@ -293,11 +293,13 @@ class Context:
                                         ptr(d2, C.c_float), ptr(good, C.c_uint8)))
         return idx1, d1, d2, good.astype(bool)
 
-    def second_index(self):
-        """knnMatch's n.trainIdx per query (sod_match_second_get; bf16 matcher only)."""
-        out = np.empty(self.nq, np.int32)
-        self._chk(self._L.sod_match_second_get(self._h, ptr(out, C.c_int32)))
-        return out
+    def knn_indices(self):
+        """knnMatch's (m.trainIdx, n.trainIdx) per query, OpenCV's float-distance order
+        (sod_match_knn_indices; bf16 matcher only)."""
+        i1 = np.empty(self.nq, np.int32)
+        i2 = np.empty(self.nq, np.int32)
+        self._chk(self._L.sod_match_knn_indices(self._h, ptr(i1, C.c_int32), ptr(i2, C.c_int32)))
+        return i1, i2
 
     def exact_order(self):
         v = C.c_int()

@@ -845,27 +845,80 @@ int sod_match_get(sod_ctx* ctx, int32_t* idx1, float* d1, float* d2, uint8_t* go
   return SOD_OK;
 }
 
-int sod_match_second_get(sod_ctx* ctx, int32_t* idx2) {
+// the integers n whose correctly rounded sqrtf is d (OpenCV's float distance): a short run
+// around d^2 (one value below 2048, a few above); empty (lo > hi) for a d no real distance
+// has -- squared distances of 0..255 descriptors are < 2^24, so d < 4096; the padding rows'
+// 1e30 norm (a single-row DB's "second") is not one
+static void sqrt_preimage(float d, float* lo, float* hi) {
+  *lo = 1.0f;
+  *hi = 0.0f;
+  if (!(d >= 0.0f) || !(d < 4096.0f)) return;
+  const double c = std::floor((double)d * (double)d);
+  bool any = false;
+  for (double n = std::max(0.0, c - 64.0); n <= c + 64.0; n += 1.0) {
+    if (std::sqrt((float)n) != d) continue;   // float sqrt: correctly rounded (IEEE)
+    if (!any) *lo = (float)n;
+    *hi = (float)n;
+    any = true;
+  }
+}
+
+int sod_match_knn_indices(sod_ctx* ctx, int32_t* idx1, int32_t* idx2) {
   SOD_TRY(set_dev(ctx));
-  if (!idx2) return sod_fail(ctx, SOD_EINVAL, "null idx2");
-  if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");
+  if (!idx1 && !idx2) return sod_fail(ctx, SOD_EINVAL, "null outputs");
+  if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue + sod_ratio_enqueue first");
   if (ctx->impl != 0)
-    return sod_fail(ctx, SOD_ESTATE, "the second neighbour's index needs the bf16 matcher "
+    return sod_fail(ctx, SOD_ESTATE, "knnMatch's indices need the bf16 matcher "
                                      "(sod_match_set_impl(ctx, 0) before the uploads)");
   if (ctx->nranks > 1 || ctx->comm || ctx->row_offset != 0)
-    return sod_fail(ctx, SOD_ESTATE, "the second neighbour's index is single-context only");
-  DevBuf<int32_t> d;
-  const size_t n = (size_t)ctx->nq;
-  int rc = sod_reserve(ctx, d, (size_t)sod_nq_pad(ctx));
-  if (rc == SOD_OK) rc = launch_second_index(ctx, d.p);
-  if (rc == SOD_OK) rc = download(ctx, idx2, d.p, n);
-  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
-    rc = sod_fail(ctx, SOD_EHIP, "second neighbour pass failed");
+    return sod_fail(ctx, SOD_ESTATE, "knnMatch's indices are single-context only");
+  int exact = 0;
+  SOD_TRY(sod_match_exact_order(ctx, &exact));
+  const size_t n = (size_t)ctx->nq, np = (size_t)sod_nq_pad(ctx);
+  std::vector<float> d1(n), d2(n), lo(np, 1.0f), hi(np, 0.0f);
+  std::vector<int32_t> i1(n), ex(np, -1), f1(np), f2(np);
+  SOD_TRY(download(ctx, i1.data(), ctx->idx1.p, n));
+  SOD_TRY(download(ctx, d1.data(), ctx->d1.p, n));
+  SOD_TRY(download(ctx, d2.data(), ctx->d2.p, n));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  DevBuf<float> dlo, dhi;
+  DevBuf<int32_t> dex, dfound;
+  int rc = SOD_OK;
+  auto pass = [&](const std::vector<float>& dist, std::vector<int32_t>& out) {
+    for (size_t q = 0; q < n; ++q) sqrt_preimage(dist[q], &lo[q], &hi[q]);
+    if (rc == SOD_OK) rc = upload(ctx, dlo, lo.data(), np);
+    if (rc == SOD_OK) rc = upload(ctx, dhi, hi.data(), np);
+    if (rc == SOD_OK) rc = upload(ctx, dex, ex.data(), np);
+    if (rc == SOD_OK) rc = sod_reserve(ctx, dfound, np);
+    if (rc == SOD_OK) rc = launch_find_rows(ctx, dlo.p, dhi.p, dex.p, dfound.p);
+    if (rc == SOD_OK) rc = download(ctx, out.data(), dfound.p, np);
+    if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+      rc = sod_fail(ctx, SOD_EHIP, "knn index pass failed");
+  };
+  // OpenCV orders by the float distance sqrtf(d^2), ties to the lower trainIdx.  With every
+  // distance < 2048 (exact order) distinct squared distances have distinct floats and the
+  // matcher's idx1 is OpenCV's; otherwise the lowest row at the float d1 is
+  if (exact) {
+    for (size_t q = 0; q < n; ++q) f1[q] = i1[q];
+  } else {
+    pass(d1, f1);
+    for (size_t q = 0; q < n && rc == SOD_OK; ++q)
+      if (f1[q] == 0x7f7f7f7f) f1[q] = i1[q];   // unreachable: the best row is at d1
+  }
+  // the second: the lowest row other than that one at the float d2
+  if (rc == SOD_OK && idx2) {
+    for (size_t q = 0; q < n; ++q) ex[q] = f1[q];
+    pass(d2, f2);
+  }
   (void)hipStreamSynchronize(ctx->stream);
-  sod_release(d);
+  sod_release(dlo);
+  sod_release(dhi);
+  sod_release(dex);
+  sod_release(dfound);
   SOD_TRY(rc);
-  for (size_t q = 0; q < n; ++q)
-    if (idx2[q] == 0x7f7f7f7f) idx2[q] = -1;   // a single DB row: no second neighbour
+  if (idx1) std::memcpy(idx1, f1.data(), n * 4);
+  if (idx2)
+    for (size_t q = 0; q < n; ++q) idx2[q] = f2[q] == 0x7f7f7f7f ? -1 : f2[q];   // single DB row
   return SOD_OK;
 }
 

@@ -164,19 +164,20 @@ __device__ __forceinline__ Frag read_frag(const uint8_t* sb, int u, int lane) {
   return f;
 }
 
-// kFind = false: the k=2 search.  kFind = true: the second neighbour's trainIdx for the
-// BFMatcher.knnMatch drop-in -- the same pass over the DB, looking for the LOWEST row other
-// than idx1 whose exact value dn - 2 q.d equals the known second-best one (cd2 - |q|^2):
-// OpenCV's strict-'<' insertion keeps the lowest trainIdx among equal distances, so that row
-// is its n.trainIdx.  Rows are found per lane in increasing order, then min-merged over the
-// lanes and (atomicMin) over the DB splits into idx2[q].
+// kFind = false: the k=2 search.  kFind = true: a row-finding pass for the BFMatcher.knnMatch
+// drop-in -- the same pass over the DB, looking per query for the LOWEST row other than
+// excl[q] whose exact squared distance lies in [flo[q], fhi[q]] (the integers whose sqrtf is
+// one float distance; a single value when every distance is < 2048).  OpenCV's strict-'<'
+// insertion keeps the lowest trainIdx among equal float distances, so that row is its
+// trainIdx.  Rows are found per lane in increasing order, then min-merged over the lanes
+// and (atomicMin) over the DB splits into found[q].
 template <bool kFind>
 __global__ __launch_bounds__(NT, 2) void match_kernel(
     const uint8_t* __restrict__ dbpack, const float* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const float* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
-    int* __restrict__ pidx, float* __restrict__ pd2, const float* __restrict__ cd2,
-    const int* __restrict__ cidx, int* __restrict__ idx2) {
+    int* __restrict__ pidx, float* __restrict__ pd2, const float* __restrict__ flo,
+    const float* __restrict__ fhi, const int* __restrict__ excl, int* __restrict__ found) {
   // ONE __shared__ array (a second one can make hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageSlot];
 
@@ -208,17 +209,20 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
   }
   float v1[QT], v2[QT];
   int id[QT];
+  float vh[kFind ? QT : 1];
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
     v1[t] = kInit;
     v2[t] = kInit;
     id[t] = 0x7fffffff;
-    if constexpr (kFind) {   // v2 = the target value, v1 = the excluded row (idx1)
+    if constexpr (kFind) {   // [v2, vh] = the target interval in dn - 2 q.d units, v1 = excl
       const int qt = qt0 + t;
       const int64_t q = (int64_t)qt * 16 + (lane & 15);
-      if (qt < nqt && cd2[q] < 1.0e29f) {   // no second row: padding norm -> nothing to find
-        v2[t] = cd2[q] - qn[q];             // integers < 2^24: exact
-        v1[t] = __int_as_float(cidx[q]);
+      vh[t] = -kInit;
+      if (qt < nqt && flo[q] <= fhi[q]) {   // an empty interval: nothing to find
+        v2[t] = flo[q] - qn[q];             // integers < 2^24: exact
+        vh[t] = fhi[q] - qn[q];
+        v1[t] = __int_as_float(excl[q]);
       }
     }
   }
@@ -256,16 +260,17 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
         bool any = false;
 #pragma unroll
         for (int t = 0; t < QT; ++t)
-          any |= (acc[t][0] == v2[t]) | (acc[t][1] == v2[t]) | (acc[t][2] == v2[t]) |
-                 (acc[t][3] == v2[t]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) any |= (acc[t][r] >= v2[t]) & (acc[t][r] <= vh[t]);
         if (__any(any)) {
           const int rowb = row_offset + (int)((s_lo + s * SPS + u) * kSubRows) + (lane >> 4) * 4;
 #pragma unroll
           for (int t = 0; t < QT; ++t) {
 #pragma unroll
             for (int r = 3; r >= 0; --r) {   // the lowest matching row of the four wins
-              const bool eq = (acc[t][r] == v2[t]) && (rowb + r != __float_as_int(v1[t]));
-              id[t] = (eq && rowb + r < id[t]) ? rowb + r : id[t];
+              const bool in = (acc[t][r] >= v2[t]) && (acc[t][r] <= vh[t]) &&
+                              (rowb + r != __float_as_int(v1[t]));
+              id[t] = (in && rowb + r < id[t]) ? rowb + r : id[t];
             }
           }
         }
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(NT, 2) void match_kernel(
       for (int m = 16; m <= 32; m <<= 1) id[t] = min(id[t], __shfl_xor(id[t], m));
       const int qt = qt0 + t;
       if (lane < 16 && qt < nqt && id[t] != 0x7fffffff)
-        atomicMin(&idx2[(int64_t)qt * 16 + lane], id[t]);
+        atomicMin(&found[(int64_t)qt * 16 + lane], id[t]);
     }
     return;
   }
@@ -517,7 +522,7 @@ int launch_match(sod_ctx* ctx) {
   hipLaunchKernelGGL(match_kernel<false>, dim3((unsigned)grid), dim3(NT), 0, ks,
                      ctx->dbpack.p, ctx->dn.p, ctx->nsub, ctx->qpack.p, ctx->qn.p, ctx->nqt,
                      nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset, pd1, pidx, pd2,
-                     nullptr, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, nullptr);
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(sod_match_mark(ctx, ks, 1));
   SOD_TRY(sod_match_stream_end(ctx));
@@ -528,9 +533,11 @@ int launch_match(sod_ctx* ctx) {
   return sod_partials_merged(ctx);   // the slot is free again
 }
 
-// the second neighbour's trainIdx of every query after a bf16 match (kFind pass): idx2 is
-// [nq_pad], set to 0x7f7f7f7f first (no row found stays that)
-int launch_second_index(sod_ctx* ctx, int32_t* idx2) {
+// per query the lowest row other than excl[q] whose exact squared distance lies in
+// [flo[q], fhi[q]] (kFind pass over the bf16-packed DB; all four arrays on the device,
+// [nq_pad]); found[q] = 0x7f7f7f7f where there is none
+int launch_find_rows(sod_ctx* ctx, const float* flo, const float* fhi, const int32_t* excl,
+                     int32_t* found) {
   const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
   const int64_t qblocks = ceil_div(ctx->nqt, NW * QT);
   const int64_t nstages = ctx->nsub / SPS;
@@ -538,11 +545,11 @@ int launch_second_index(sod_ctx* ctx, int32_t* idx2) {
   split = std::min<int64_t>(split, nstages);
   const int64_t st_per_split = ceil_div(nstages, split);
   split = ceil_div(nstages, st_per_split);
-  SOD_HIP(ctx, hipMemsetAsync(idx2, 0x7f, (size_t)nq_pad * 4, ctx->stream));
+  SOD_HIP(ctx, hipMemsetAsync(found, 0x7f, (size_t)nq_pad * 4, ctx->stream));
   hipLaunchKernelGGL(match_kernel<true>, dim3((unsigned)(qblocks * split)), dim3(NT), 0,
                      ctx->stream, ctx->dbpack.p, ctx->dn.p, ctx->nsub, ctx->qpack.p, ctx->qn.p,
                      ctx->nqt, nq_pad, (int)split, st_per_split * SPS, (int)ctx->row_offset,
-                     nullptr, nullptr, nullptr, ctx->cd2.p, ctx->cidx.p, idx2);
+                     nullptr, nullptr, nullptr, flo, fhi, excl, found);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }

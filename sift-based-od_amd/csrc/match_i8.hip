@@ -480,7 +480,10 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
 
 // One work unit: query block qb (NW16*QT tiles) against DB chunk sp (sub_per_split subtiles),
 // writing the chunk's partial top-2 of every query to slot sp of pd1/pidx/pd2.
-template <int QT>
+// PF = subtiles whose A fragments / norm words are read from LDS ahead of their MFMAs: 1
+// hides the LDS latency behind one subtile's MFMAs, which at 2-4 query tiles per wave (8-16
+// MFMAs per wave and subtile) is too short
+template <int QT, int PF>
 __device__ __forceinline__ void match_unit(
     uint8_t* lds, int sp, int qb, const uint8_t* __restrict__ dbpack, const int* __restrict__ dn,
     int64_t nsub, const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt,
@@ -652,23 +655,31 @@ __device__ __forceinline__ void match_unit(
     }
 #endif
     slot = slot + 1 == kRing ? 0 : slot + 1;
-    i32x4 fa0 = *reinterpret_cast<const i32x4*>(sb + lane * 16);
-    i32x4 fa1 = *reinterpret_cast<const i32x4*>(sb + 1024 + lane * 16);
-    i32x4 fc = *reinterpret_cast<const i32x4*>(nb0);
+    i32x4 fa0[PF], fa1[PF], fc[PF];
 #if !SOD_I8_LAZYP
-    i32x4 fp = *reinterpret_cast<const i32x4*>(nb0 + kParOff);
+    i32x4 fp[PF];
 #endif
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      fa0[j] = *reinterpret_cast<const i32x4*>(sb + j * kSub + lane * 16);
+      fa1[j] = *reinterpret_cast<const i32x4*>(sb + j * kSub + 1024 + lane * 16);
+      fc[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j, 0));
+#if !SOD_I8_LAZYP
+      fp[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j, 0) + kParOff);
+#endif
+    }
 #if SOD_I8_UNROLL
 #pragma unroll SOD_I8_UNROLL
 #else
 #pragma clang loop unroll(full)
 #endif
     for (int u = 0; u < SPS; ++u) {
-      const i32x4 a0 = fa0, a1 = fa1, c = fc;   // c = floor(-||d'||^2 / 2)
+      const int js = u % PF;   // a constant after unrolling
+      const i32x4 a0 = fa0[js], a1 = fa1[js], c = fc[js];   // c = floor(-||d'||^2 / 2)
 #if SOD_I8_LAZYP
       const uint8_t* p = nb0 + norm_off(u, 0) + kParOff;   // norm_off(u, g) = norm_off(u, 0) + 16 g
 #else
-      const i32x4 p = fp;
+      const i32x4 p = fp[js];
 #endif
       i32x4 acc[QT];
 #pragma unroll
@@ -682,13 +693,13 @@ __device__ __forceinline__ void match_unit(
 #else
       const bool piece_here = false;
 #endif
-      if (u + 1 < SPS) {   // next subtile's fragments in flight
-        const uint8_t* nb = sb + (u + 1) * kSub + lane * 16;
-        fa0 = *reinterpret_cast<const i32x4*>(nb);
-        fa1 = *reinterpret_cast<const i32x4*>(nb + 1024);
-        fc = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + 1, 0));
+      if (u + PF < SPS) {   // subtile u + PF's fragments in flight
+        const uint8_t* nb = sb + (u + PF) * kSub + lane * 16;
+        fa0[js] = *reinterpret_cast<const i32x4*>(nb);
+        fa1[js] = *reinterpret_cast<const i32x4*>(nb + 1024);
+        fc[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF, 0));
 #if !SOD_I8_LAZYP
-        fp = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + 1, 0) + kParOff);
+        fp[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF, 0) + kParOff);
 #endif
       }
 #pragma unroll
@@ -787,7 +798,7 @@ __device__ __forceinline__ void match_unit(
 __device__ unsigned long long g_stamps[4096][8];
 #endif
 
-template <int QT>
+template <int QT, int PF>
 __global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
@@ -809,10 +820,10 @@ __global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
   // instead of all of them (bijective for any grid size; cdna_hip_programming.md T1)
   const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = blockIdx.x % 8;
   const unsigned u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blockIdx.x / 8;
-  match_unit<QT>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
+  match_unit<QT, PF>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
              sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
 #else
-  match_unit<QT>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
+  match_unit<QT, PF>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
              nq_pad, sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
 #endif
 #ifdef SOD_I8_STAMP
@@ -1136,6 +1147,15 @@ static int pick_qt(int32_t nqt) {
   return 2;
 }
 
+// LDS prefetch distance (subtiles) per query tiles per wave; SOD_MATCH_PF overrides
+static int pick_pf(int qt) {
+  if (const char* e = std::getenv("SOD_MATCH_PF")) {
+    const int v = std::atoi(e);
+    if (v == 1 || v == 2) return v;
+  }
+  return 1;
+}
+
 int launch_match_i8(sod_ctx* ctx) {
   const bool wide = ctx->impl == 2;
   const int rows = wide ? 32 : kSubRows;
@@ -1193,13 +1213,20 @@ int launch_match_i8(sod_ctx* ctx) {
                           ctx->nqt, nq_pad, (int)split, st_per_split * sps,
                           (int)ctx->row_offset, pd1, pidx, pd2, (int)qblocks);
   else {
-#define SOD_LAUNCH_I8(Q)                                                                      \
-  hipExtLaunchKernelGGL(match_i8_kernel<Q>, dim3((unsigned)(qblocks * split)), dim3(NT16), 0,   \
+#define SOD_LAUNCH_I8(Q, P)                                                                   \
+  hipExtLaunchKernelGGL((match_i8_kernel<Q, P>), dim3((unsigned)(qblocks * split)), dim3(NT16), 0, \
                         ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),  \
                         ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),       \
                         ctx->nqt, nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, \
                         pd1, pidx, pd2, (int)qblocks, gthr, seedload)
-    if (qt == 8) SOD_LAUNCH_I8(8); else if (qt == 4) SOD_LAUNCH_I8(4); else SOD_LAUNCH_I8(2);
+    const int pf = pick_pf(qt);
+    if (qt == 8) {
+      if (pf == 2) SOD_LAUNCH_I8(8, 2); else SOD_LAUNCH_I8(8, 1);
+    } else if (qt == 4) {
+      if (pf == 2) SOD_LAUNCH_I8(4, 2); else SOD_LAUNCH_I8(4, 1);
+    } else {
+      if (pf == 2) SOD_LAUNCH_I8(2, 2); else SOD_LAUNCH_I8(2, 1);
+    }
 #undef SOD_LAUNCH_I8
   }
   SOD_HIP(ctx, hipGetLastError());

@@ -283,7 +283,8 @@ enum { kStageMatch = 0, kStageMerge = 1, kStageHough = 2, kStageSelect = 3, kSta
        kStageAllreduce = 5, kStageAllgather = 6, kStages = 7 };
 int sod_stage_mark(sod_ctx* ctx, int stage, bool end);
 int launch_match(sod_ctx* ctx);
-int launch_second_index(sod_ctx* ctx, int32_t* idx2);
+int launch_find_rows(sod_ctx* ctx, const float* flo, const float* fhi, const int32_t* excl,
+                     int32_t* found);
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db);
 int launch_match_i8(sod_ctx* ctx);
 // matcher-input writers call these around their writes; the match launchers around the

@@ -61,11 +61,13 @@ class BFMatcher:
     """``cv2.BFMatcher(normType=NORM_L2, crossCheck=False)``: brute force, L2 only.
 
     ``knnMatch(k=2)`` returns both DMatch objects complete, the second one's ``trainIdx``
-    included (OpenCV fills it; main.py:81-86 reads only its distance): the lowest trainIdx
-    other than the first's at the second-best distance, which is what OpenCV's strict-'<'
-    k=2 insertion keeps.  That index comes from a second MFMA pass over the DB
-    (``sod_match_second_get``, bf16 matcher), so this object runs on a bf16 context of its
-    own unless one is given."""
+    included (OpenCV fills it; main.py:81-86 reads only its distance): OpenCV orders by the
+    float distance with ties to the lower trainIdx, so ``n.trainIdx`` is the lowest row other
+    than ``m``'s at the second float distance -- and, for inputs whose distances reach 2048
+    (not SIFT: its norms are ~512), where two squared distances can share a float,
+    ``m.trainIdx`` is the lowest row at the first.  Those indices come from MFMA passes over
+    the DB (``sod_match_knn_indices``, bf16 matcher), so this object runs on a bf16 context
+    of its own unless one is given."""
 
     def __init__(self, normType=NORM_L2, crossCheck=False, ctx=None):
         if normType != NORM_L2:
@@ -97,8 +99,8 @@ class BFMatcher:
         ctx.match()
         ctx.ratio(0.75)
         idx1, d1, d2, _ = ctx.match_result()
+        idx1, idx2 = ctx.knn_indices()
         if k == 1 or ntrain == 1:
             return [[DMatch(i, int(idx1[i]), 0, float(d1[i]))] for i in range(len(idx1))]
-        idx2 = ctx.second_index()
         return [[DMatch(i, int(idx1[i]), 0, float(d1[i])),
                  DMatch(i, int(idx2[i]), 0, float(d2[i]))] for i in range(len(idx1))]

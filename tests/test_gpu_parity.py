@@ -111,7 +111,7 @@ def test_matcher_query_tiles_shared_thresholds(ctx, monkeypatch, qt):
 @pytest.mark.parametrize("case", ["edges", "dups"])
 def test_knnmatch_second_train_idx(case):
     """BFMatcher.knnMatch returns OpenCV's full pair: n.trainIdx = the lowest trainIdx other
-    than m's at the second-best distance (sod_match_second_get), against the oracle; exact
+    than m's at the second-best distance (sod_match_knn_indices), against the oracle; exact
     duplicate rows make the ties (inside one DB split and across splits)."""
     from sift_based_od_amd.matcher import BFMatcher
     if case == "edges":
@@ -134,6 +134,52 @@ def test_knnmatch_second_train_idx(case):
     assert np.array_equal(np.array([m.distance for m, _ in res], np.float32), e1)
     assert np.array_equal(np.array([n.distance for _, n in res], np.float32), e2)
     assert all(m.queryIdx == i and n.queryIdx == i for i, (m, n) in enumerate(res))
+
+
+def _float_tie_case(seed=23, nq=96, ndb=3000):
+    """Descriptors far apart (distances 2200-2900, beyond 2048): for every query a pair of
+    DB rows whose squared distances differ by 1 but share one float sqrtf -- OpenCV then
+    sees a tie and keeps the LOWER trainIdx, while the exact squared order prefers the
+    other row when it comes later."""
+    rng = np.random.default_rng(seed)
+    q = rng.integers(250, 256, (nq, 128)).astype(np.int64)
+    db = rng.integers(0, 6, (ndb, 128)).astype(np.int64)           # far: ~2860
+    placed = 0
+    for k in range(nq):
+        for _ in range(200):
+            a = np.clip(q[k] - rng.integers(185, 230, 128), 0, 255)
+            a[0] = q[k][0] - 1                                        # B: d0 = q0 -> sq - 1
+            b = a.copy()
+            b[0] = q[k][0]
+            sa, sb = int(((q[k] - a) ** 2).sum()), int(((q[k] - b) ** 2).sum())
+            if np.sqrt(np.float32(sa), dtype=np.float32) == np.sqrt(np.float32(sb), dtype=np.float32):
+                i, j = rng.choice(ndb, 2, replace=False)
+                db[i], db[j] = (a, b) if k % 2 else (b, a)          # the closer one first or last
+                placed += 1
+                break
+    assert placed > nq // 2
+    return q.astype(np.uint8), db.astype(np.uint8)
+
+
+def test_knnmatch_float_distance_ties():
+    """Inputs beyond SIFT's range (distances >= 2048, exact_order False): knnMatch's indices
+    follow OpenCV's float-distance order -- equal float distances keep the lower trainIdx --
+    for m and n, against the oracle (float32 sqrt order) and the int64 brute force."""
+    from sift_based_od_amd.matcher import BFMatcher
+    q, db = _float_tie_case()
+    bf = BFMatcher()
+    res = bf.knnMatch(q.astype(np.float32), db.astype(np.float32), k=2)
+    assert not bf._context().exact_order()
+    i1, e1, e2, i2 = orc.knn2_match(q, db, with_idx2=True)
+    j1, f1, f2, j2 = orc.knn2_match_int(q, db, with_idx2=True)
+    assert np.array_equal(i1, j1) and np.array_equal(i2, j2)
+    assert [m.trainIdx for m, _ in res] == i1.tolist()
+    assert [n.trainIdx for _, n in res] == i2.tolist()
+    assert np.array_equal(np.array([m.distance for m, _ in res], np.float32), e1)
+    assert np.array_equal(np.array([n.distance for _, n in res], np.float32), e2)
+    # the float order mattered: the matcher's exact squared order picks other rows here
+    raw = bf._context().match_result()[0]
+    assert (raw != i1).sum() > 0
 
 
 @pytest.mark.parametrize("impl", IMPLS)
