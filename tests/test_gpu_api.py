@@ -533,3 +533,44 @@ def test_ratio_argument_validation():
         _, d1, d2, g2 = c.match_result()
         assert np.array_equal(g2, orc.ratio_test(d1, d2, 0.5))
         assert g2.sum() <= good.sum()
+
+
+@pytest.mark.parametrize("case", ["no_good_matches", "no_valid_bins", "one_query", "ragged"])
+def test_pipeline_empty_and_ragged(ctx, case):
+    """Edge sizes through the whole device pipeline, against the oracle: no match passes the
+    ratio test (ratio 0), no bin reaches the vote threshold, a single query, and query / DB
+    counts that fill no tile or stage (17 queries, 1 000 + 3 rows)."""
+    nimg, kpi = (1, 1003) if case == "ragged" else (3, 400)
+    nq = {"one_query": 1, "ragged": 17}.get(case, 600)
+    db = synthetic.make_database(nimg, kpi, seed=41)
+    qs = synthetic.make_queries(nq, seed=42, db_seed=41, kp_per_image=kpi, planted_frac=0.6,
+                                n_objects=1)
+    ratio = 0.0 if case == "no_good_matches" else 0.75
+    vthr = 10 ** 6 if case == "no_valid_bins" else 5
+    ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
+    ctx.upload_db(db.des)
+    ctx.upload_queries(qs.des, qs.kp)
+    ctx.pipeline(qs.shape, 15, ratio=ratio, vote_threshold=vthr, affine_threshold=4)
+    idx1, d1, d2, good = ctx.match_result()
+    e1, f1, f2 = orc.knn2_match(qs.des, db.des)
+    assert np.array_equal(idx1, e1) and np.array_equal(d1, f1) and np.array_equal(d2, f2)
+    assert np.array_equal(good, orc.ratio_test(f1, f2, ratio))
+    matches = [(int(q), int(idx1[q])) for q in np.nonzero(good)[0]]
+    dbkp, qkp, images = oracle_inputs(db, qs.kp)
+    table = orc.hough_vote(matches, qkp, dbkp, images, 15, qs.shape)
+    vb = orc.valid_bins(table, vthr)
+    aff = orc.affine_verify(vb, qkp, dbkp, (qs.shape[1], qs.shape[0]), 4)
+    keys, votes = ctx.all_bins()
+    assert [tuple(k) for k in keys] == list(table.keys())
+    assert list(votes) == [b.votes for b in table.values()]
+    v = ctx.valid_result()
+    assert [tuple(k) for k in v["keys"]] == [b.pose for b in vb]
+    a = ctx.affine_result()
+    assert list(a["survived"].astype(bool)) == [r["survived"] for r in aff]
+    if case == "no_good_matches":
+        assert not good.any() and len(keys) == 0 and len(v["keys"]) == 0
+    if case == "no_valid_bins":
+        assert len(keys) > 0 and len(v["keys"]) == 0
+    post = ctx.postprocess()                     # clustering of the survivors: also empty-safe
+    if not any(r["survived"] for r in aff):
+        assert len(post["final_pose"]) == 0
