@@ -439,7 +439,8 @@ __global__ __launch_bounds__(64 * kMergeW) void merge_kernel(
   if (q >= nq) return;
   // the matcher's shared thresholds of this partial-result slot: "nothing known" again for
   // the next launch that takes the slot (it waits for this merge)
-  if (reset) reset[q] = (int)0x80808080;
+  if (reset)
+    for (int r = 0; r < kThrWords; ++r) reset[q * kThrWords + r] = (int)0x80808080;
   od1[q] = v1;
   oidx[q] = i1;
   od2[q] = v2;

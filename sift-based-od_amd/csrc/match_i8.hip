@@ -238,6 +238,12 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_EXP
 #define SOD_I8_EXP 0       // timing experiments only (wrong results): 1 no refill DMA,
 #endif                     // 2 no prefilter, 4 no stage wait/barrier
+#ifndef SOD_I8_SLOTS
+#define SOD_I8_SLOTS 1     // shared bound from the best rows of the even / odd DB chunks
+#endif
+#ifndef SOD_I8_SEEDSLOT
+#define SOD_I8_SEEDSLOT 1  // the seed's best row goes out with the seed's t2
+#endif
 #ifndef SOD_I8_LAZYP
 #define SOD_I8_LAZYP 1     // parity words read from LDS on the slow path only
 #endif
@@ -310,6 +316,13 @@ __device__ __forceinline__ void top2_xor16(int& y1, int& y2) {
   const int a = (int)p[0], b = (int)p[1];
   y1 = max(a, b);
   y2 = max(max(min(a, b), (int)q[0]), (int)q[1]);
+}
+// max of a over the lane quadruple (l, l^16, l^32, l^48): one query's four lane groups
+__device__ __forceinline__ int max_xor3216(int a) {
+  auto p = __builtin_amdgcn_permlane32_swap((unsigned)a, (unsigned)a, false, false);
+  a = max((int)p[0], (int)p[1]);
+  p = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)a, false, false);
+  return max((int)p[0], (int)p[1]);
 }
 
 #if SOD_I8_LAZYP
@@ -539,12 +552,20 @@ __device__ __forceinline__ void match_unit(
   // DMAs the current global values of its 128 queries into LDS, which the next boundary
   // applies -- a value one stage old, or stale across XCDs, is still a valid bound, so
   // nothing waits for it.  The chunk's own top-2 stays exact over the rows it keeps.
+  // SOD_I8_SLOTS: every chunk also publishes its query-wide best h (the value of one of its
+  // rows) into word 1 + (chunk & 1) by atomic max.  The two words then hold rows of two
+  // different chunks, so min(even best, odd best) has two distinct rows at or above it and
+  // is a valid bound too -- close to the second best over ALL rows the chunks have seen so
+  // far, where the max of the chunks' own second bests lags far behind with many chunks.
+  // Layout: gthr[q * kThrWords + {0: t2, 1: even best, 2: odd best}] (h units).
   const int wq = __builtin_amdgcn_readfirstlane(wave);
   const int ntile = max(0, min(QT, nqt - (qb * NW16 + wq) * QT));   // real tiles of the wave
-  int* const gw = gthr + (int64_t)(qb * NW16 + wq) * QT * 16;   // the wave's queries
+  int* const gw = gthr + (int64_t)(qb * NW16 + wq) * QT * 16 * kThrWords;   // the wave's queries
   const __amdgpu_buffer_rsrc_t rg =
-      __builtin_amdgcn_make_buffer_rsrc((void*)gw, (short)0, ntile * 64, kRsrcWord3);
-  uint8_t* const gl = lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64);
+      __builtin_amdgcn_make_buffer_rsrc((void*)gw, (short)0, ntile * 64 * kThrWords, kRsrcWord3);
+  uint8_t* const gl =
+      lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64 * kThrWords);
+  [[maybe_unused]] const int oslot = 1 + (sp & 1);   // this chunk's best-row word
 #endif
 #if SOD_I8_PIPE
   // accumulators, norms and first row of the subtile whose prefilter is pending; the
@@ -604,6 +625,9 @@ __device__ __forceinline__ void match_unit(
       // normally, its rows below the seed skipped, instead of every tile of its 32 subtiles
       // taking the exact update (the dense phase).
       int sm[QT];
+#if SOD_I8_SLOTS
+      int sb1[QT];
+#endif
 #pragma unroll
       for (int t = 0; t < QT; ++t) sm[t] = INT_MIN;
 #pragma unroll 1
@@ -628,9 +652,17 @@ __device__ __forceinline__ void match_unit(
 #if SOD_I8_XCHUNK && SOD_I8_SEEDPUB
         // out to the chunks of the same queries now: their first threshold load (this
         // stage's share_load) then already sees the other chunks' seeds
-        if (lane < 16 && t < ntile)
-          __hip_atomic_fetch_max(gw + 16 * t + lane, t2[t], __ATOMIC_RELAXED,
+        if (lane < 16 && t < ntile) {
+          __hip_atomic_fetch_max(gw + (16 * t + lane) * kThrWords, t2[t], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
+#if SOD_I8_SLOTS && SOD_I8_SEEDSLOT
+          __hip_atomic_fetch_max(gw + (16 * t + lane) * kThrWords + oslot, g1, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        }
+#endif
+#if SOD_I8_SLOTS
+        sb1[t] = g1;   // the chunk's best so far (h), for the seed load below
 #endif
       }
 #if SOD_I8_XCHUNK && SOD_I8_SEEDPUB && SOD_I8_SEEDLOAD
@@ -641,15 +673,24 @@ __device__ __forceinline__ void match_unit(
       // 124 chunks, 0.078 vs 0.070 ms), so the launch enables it up to 64 chunks only, and
       // the one-image kernel (QT 2) does not carry the code (its mere presence cost 2-3 %)
       if (QT >= 4 && seedload) {
-        int gq[QT];
+        int gq[QT][kThrWords];
 #pragma unroll
         for (int t = 0; t < QT; ++t)   // one load per query (lanes 0-15), then to its groups
-          gq[t] = lane < 16 && t < ntile
-                      ? __hip_atomic_load(gw + 16 * t + lane, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT)
-                      : INT_MIN;
 #pragma unroll
-        for (int t = 0; t < QT; ++t) t2[t] = max(t2[t], __shfl(gq[t], lane & 15));
+          for (int r = 0; r < kThrWords; ++r)
+            gq[t][r] = lane < 16 && t < ntile
+                           ? __hip_atomic_load(gw + (16 * t + lane) * kThrWords + r,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : INT_MIN;
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+#if SOD_I8_SLOTS
+          const bool odd = oslot == 2;   // selects, not an indexed register array
+          const int own = max(odd ? gq[t][2] : gq[t][1], sb1[t]), other = odd ? gq[t][1] : gq[t][2];
+          gq[t][0] = max(gq[t][0], min(own, other));
+#endif
+          t2[t] = max(t2[t], __shfl(gq[t][0], lane & 15));
+        }
       }
 #endif
     }
@@ -732,22 +773,49 @@ __device__ __forceinline__ void match_unit(
       // refill pieces went out before the load) it publishes its own t2 where above them and
       // raises t2 to them
       const bool xstage = kXEvery == 1 || s < kXDense || s % kXEvery == 0;   // wave-uniform
-      if (share_load(u) && xstage && lane < QT * 4)   // the wave's QT x 16 values: QT*4 lanes x 16 B
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_void*)gl, 16, (uint32_t)lane * 16u, 0,
-                                                 0, 16 /* sc1: past this XCD's L2 */);
+      // the wave's QT x 16 x kThrWords values: QT*4*kThrWords lanes x 16 B, in pieces of 64
+      constexpr int kGLanes = QT * 4 * kThrWords;
+      if (share_load(u) && xstage) {
+#pragma unroll
+        for (int g = 0; g < kGLanes; g += 64)
+          if (lane < kGLanes - g)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_void*)(gl + g * 16), 16,
+                                                     (uint32_t)(g + lane) * 16u, 0, 0,
+                                                     16 /* sc1: past this XCD's L2 */);
+      }
       if (share_apply(u) && xstage && (SOD_I8_SHARE2 == 0 || u != 12 || s > 0)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15);
+        const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15) * kThrWords;
         // publishing is a device-scope atomic per query (a memory-side transaction each):
         // every stage while the thresholds still move fast, then every kPublishEvery-th
         const bool publish = s < kPublishDense || s % kPublishEvery == 0;
         int gq[QT];
+#if SOD_I8_SLOTS
+        int go[QT], gx[QT];
+#endif
 #pragma unroll
-        for (int t = 0; t < QT; ++t) gq[t] = gv[16 * t];   // all reads, then one wait
+        for (int t = 0; t < QT; ++t) {   // all reads, then one wait
+          gq[t] = gv[16 * kThrWords * t];
+#if SOD_I8_SLOTS
+          go[t] = gv[16 * kThrWords * t + oslot];
+          gx[t] = gv[16 * kThrWords * t + 3 - oslot];
+#endif
+        }
 #pragma unroll
         for (int t = 0; t < QT; ++t) {
+#if SOD_I8_SLOTS
+          // the query-wide best of this wave's rows (y units -> h)
+          const int hb = max_xor3216(y1[t]) >> 1;
+          if (publish && lane < 16 && t < ntile && hb > go[t])
+            __hip_atomic_fetch_max(gw + (16 * t + lane) * kThrWords + oslot, hb,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // t2 goes out only where it beats what every chunk derives from the words itself
+          // (a t2 raised by the slot bound would otherwise be re-published by all chunks at
+          // every exchange: same-address atomics that the vmcnt(0) above then waits for)
+          gq[t] = max(gq[t], min(max(go[t], hb), gx[t]));
+#endif
           if (publish && lane < 16 && t < ntile && t2[t] > gq[t])
-            __hip_atomic_fetch_max(gw + 16 * t + lane, t2[t], __ATOMIC_RELAXED,
+            __hip_atomic_fetch_max(gw + (16 * t + lane) * kThrWords, t2[t], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
           t2[t] = max(t2[t], gq[t]);
         }
@@ -806,7 +874,7 @@ __global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
     int* __restrict__ pidx, float* __restrict__ pd2, int nqb, int* __restrict__ gthr,
     int seedload) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageBytes + kNormRing * kStageNorm +
-                                                     SOD_I8_XCHUNK * NW16 * QT * 64];
+                                                     SOD_I8_XCHUNK * NW16 * QT * 64 * kThrWords];
 #ifdef SOD_I8_STAMP
   unsigned long long t0 = 0, r0 = 0;
   if (threadIdx.x == 0) {
@@ -1192,16 +1260,17 @@ int launch_match_i8(sod_ctx* ctx) {
   // uninitialised thresholds
   int32_t* gthr = nullptr;
   if (!wide) {
-    if (ctx->gthr.n < (size_t)(2 * nq_pad) || ctx->gthr_n != nq_pad) {
-      if (ctx->gthr.n < (size_t)(2 * nq_pad)) {
+    const int64_t gslot = kThrWords * nq_pad;   // words of one slot
+    if (ctx->gthr.n < (size_t)(2 * gslot) || ctx->gthr_n != nq_pad) {
+      if (ctx->gthr.n < (size_t)(2 * gslot)) {
         SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
         SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        SOD_TRY(sod_reserve(ctx, ctx->gthr, (size_t)(2 * nq_pad)));
+        SOD_TRY(sod_reserve(ctx, ctx->gthr, (size_t)(2 * gslot)));
       }
-      SOD_HIP(ctx, hipMemsetAsync(ctx->gthr.p, 0x80, (size_t)(2 * nq_pad) * 4, ks));
+      SOD_HIP(ctx, hipMemsetAsync(ctx->gthr.p, 0x80, (size_t)(2 * gslot) * 4, ks));
       ctx->gthr_n = nq_pad;
     }
-    gthr = ctx->gthr.p + ctx->pslot * nq_pad;
+    gthr = ctx->gthr.p + ctx->pslot * gslot;
   }
   const int seedload = split <= 64 ? 1 : 0;   // see match_unit (SOD_I8_SEEDLOAD)
   hipEvent_t eb, ee;

@@ -16,6 +16,9 @@ constexpr int kDim = 128;
 constexpr int kSubRows = 16;
 constexpr int kSubBytes = kSubRows * kDim * 2;   // 4096
 constexpr float kPadNorm = 1.0e30f;              // ||d||^2 of padding rows: never selected
+// int8 matcher, thresholds shared by the DB chunks of a query: per query {max published t2,
+// max published best of the even chunks, of the odd chunks} (match_i8.hip, SOD_I8_SLOTS)
+constexpr int kThrWords = 3;
 
 // Hough
 constexpr int kSigmaLutHalf = 255;               // i_sigma LUT over k = oQ - oM in [-255,255]
@@ -83,7 +86,7 @@ struct sod_ctx {
   DevBuf<float> cd1, cd2;       // merged (this shard / after allgather: global)  [nq_pad]
   DevBuf<int32_t> cidx;
   DevBuf<int32_t> gthr;         // matcher: prefilter thresholds shared by the DB chunks
-  int64_t gthr_n = 0;           //   [partial-result slot][nq_pad]; reset by the slot's merge
+  int64_t gthr_n = 0;           //   [partial-result slot][nq_pad][kThrWords]; reset by the merge
   DevBuf<float> gd1, gd2;       // allgather landing [nranks * nq_pad]
   DevBuf<int32_t> gidx;
   DevBuf<float> d1, d2;         // sqrt distances [nq]

@@ -61,7 +61,9 @@ def main():
                     st.append(ctx.stage_ms())
                 res[m]["merge"].append(float(np.mean([x[1] for x in st])))
                 got = ctx.match_result()
-                if ref is None:
+                if os.environ.get("SMALLQ_NOCHECK"):   # timing-only builds (SOD_I8_EXP)
+                    pass
+                elif ref is None:
                     ref = [np.asarray(a).copy() for a in got]
                 else:
                     for a, b in zip(ref, got):
