@@ -85,9 +85,9 @@ def parse():
                         "stay on the context stream).  Default: on with several ranks")
     p.add_argument("--cu-reserve", type=int, default=-1,
                    help="CUs per XCD kept off the matcher for the other stages and the RCCL "
-                        "exchanges (sod_set_cu_reserve; implies --overlap 1).  Default: 1 "
-                        "from 1e9 pairs per GPU up (C2, C3, C5), else 0 "
-                        "(and 0 with --contexts > 1 or --overlap 0)")
+                        "exchanges (sod_set_cu_reserve; implies --overlap 1).  Default: 3 "
+                        "below 5e5 DB rows per GPU (C2), else 1 "
+                        "(0 with --contexts > 1 or --overlap 0)")
     p.add_argument("--impl", default="i8", choices=sorted(IMPLS),
                    help="matcher kernel: int8 MFMA 16x16x64 (default, fastest), int8 32x32x32 "
                         "or bf16 MFMA; all bit-exact")
@@ -397,12 +397,16 @@ def main():
     ctx.upload_db(shard, row_offset=rank * n_shard)
     ctx.upload_queries(qs.des, qs.kp)
     from sift_based_od_amd.sharded import FileHostComm, RcclComm, run_sharded
-    # auto: split the chip for the int8 matcher from 1e9 pairs per GPU up (C3 / C5: ~3.8 ms
-    # against a ~0.8 ms tail on the 8 reserved CUs; C2: 0.209 vs 0.218 ms per step with two
-    # contexts, measured; 2 reserved CUs per XCD 0.258 ms)
+    # auto: split the chip for the int8 matcher (tail on reserved CUs beside the next image's
+    # matcher).  The tail's dependent kernel chain grows with the queries, the matcher with
+    # queries x DB rows, so a small DB shard needs more tail CUs: 3 per XCD below 5e5 rows
+    # (C2: 0.125 vs 0.134 ms per step at 1 per XCD, 0.168 with two unsplit contexts), else 1
+    # (C3 / C5: ~3.8 ms against a ~0.7 ms tail on 8 CUs; one query image: 0.092 vs 0.106 ms
+    # with two unsplit contexts).  2 per XCD leaves C2's 240-work-group grid no spare CU
+    # (0.21 ms: a second dispatch round).  profiles/r03t_tail_ab.log
     reserve = a.cu_reserve if a.cu_reserve >= 0 else (
-        0 if a.contexts > 1 or a.overlap == 0 or nq * shard.shape[0] < 10 ** 9
-        or a.impl != "i8" else 1)   # grid sizing measured for the default int8 kernel only
+        0 if a.contexts > 1 or a.overlap == 0
+        or a.impl != "i8" else (3 if shard.shape[0] < 500000 else 1))
     overlap = a.overlap if a.overlap >= 0 else (1 if world > 1 or reserve else 0)
     ctx.set_overlap(bool(overlap))
     if reserve:
