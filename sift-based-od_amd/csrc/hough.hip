@@ -26,6 +26,7 @@
 //                    outlier rejection, fixed point (AffineParameters.py:89-160)
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <utility>
 
 #include "sod_internal.h"
@@ -319,19 +320,21 @@ __global__ __launch_bounds__(kHistThreads) void hist_kernel(
   // all of a thread's queries are loaded before any is listed: one memory latency per
   // work-group instead of one per query (the kernel is latency-bound on a CU split's few
   // reserved CUs)
+  // (unconditional loads from clamped indices: a load under a branch gets a vmcnt(0) at the
+  // branch's join, i.e. one round trip per load)
   constexpr int kPer = kChunk / kHistThreads;
   uint32_t mv[kPer], kv[kPer], bv[kPer];
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     const int64_t q = q0 + threadIdx.x + (int64_t)u * kHistThreads;
-    mv[u] = q < q1 ? vmask[q] : 0u;
+    const int64_t qc = q < q1 ? q : q0;
+    mv[u] = vmask[qc];
+    kv[u] = basekey[qc];
+    bv[u] = qimg ? (uint32_t)qimg[qc] : 0u;
+    if (q >= q1) mv[u] = 0u;
   }
 #pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int64_t q = q0 + threadIdx.x + (int64_t)u * kHistThreads;
-    kv[u] = (mv[u] & 0x10000u) ? basekey[q] : 0u;
-    bv[u] = (qimg && (mv[u] & 0x10000u)) ? (uint32_t)(qimg[q] * nbins1) : 0u;
-  }
+  for (int u = 0; u < kPer; ++u) bv[u] = (mv[u] & 0x10000u) ? bv[u] * (uint32_t)nbins1 : 0u;
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     bool hit = false;
@@ -398,12 +401,24 @@ __device__ __forceinline__ uint32_t first_touch_slots(int64_t q, const uint32_t*
   if (!m) return 0;
   const uint32_t key = basekey[q];
   const int ix = key & 0xFF, iy = (key >> 8) & 0xFF, it = (key >> 16) & 0xFF, is = key >> 24;
+  // all of the query's count / first-touch loads in flight at once, then the compaction
+  // (a load per slot inside the compacting loop was one dependent round trip per vote)
+  uint32_t lbs[16], c[16], f[16];
+#pragma unroll
   for (int slot = 0; slot < 16; ++slot) {
-    if (!((m >> slot) & 1u)) continue;
-    const uint32_t lb = qbase + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
-                                        it + ((slot >> 1) & 1), is + (slot & 1), b);
-    if (gcount[lb] >= thr && gfirst[lb] == (uint32_t)(q * 16 + slot)) bins_out[n++] = lb;
+    lbs[slot] = qbase + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                it + ((slot >> 1) & 1), is + (slot & 1), b);
+    // unconditional loads (slots out of range read bin qbase, a valid address): a load under
+    // a branch gets a vmcnt(0) wait at the branch's join, one round trip per slot again
+    const bool in = (m >> slot) & 1u;
+    const uint32_t a = in ? lbs[slot] : qbase;
+    c[slot] = gcount[a];
+    f[slot] = gfirst[a];
+    if (!in) c[slot] = 0u;
   }
+#pragma unroll
+  for (int slot = 0; slot < 16; ++slot)
+    if (c[slot] >= thr && f[slot] == (uint32_t)(q * 16 + slot)) bins_out[n++] = lbs[slot];
   return n;
 }
 
@@ -614,12 +629,17 @@ __global__ __launch_bounds__(256) void member_fill_lds_kernel(
   __syncthreads();
   const int ix = k & 0xFF, iy = (k >> 8) & 0xFF, it = (k >> 16) & 0xFF, is = k >> 24;
   uint32_t v[16], r[16];
+  // independent loads, one wait: unconditional (a slot without a vote reads entry 0; its
+  // key may be stale -- basekey is written for good matches only) -- a load under a branch
+  // waits at the branch's join
 #pragma unroll
-  for (int slot = 0; slot < 16; ++slot)   // independent loads, one wait
-    v[slot] = ((m >> slot) & 1u)
-                  ? vidx[base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
-                                        it + ((slot >> 1) & 1), is + (slot & 1), b)]
-                  : 0xFFFFFFFFu;
+  for (int slot = 0; slot < 16; ++slot) {
+    const bool vin = (m >> slot) & 1u;
+    v[slot] = vidx[vin ? base + lin_bin(ix + ((slot >> 3) & 1), iy + ((slot >> 2) & 1),
+                                        it + ((slot >> 1) & 1), is + (slot & 1), b)
+                       : 0u];
+    if (!vin) v[slot] = 0xFFFFFFFFu;
+  }
 #pragma unroll
   for (int slot = 0; slot < 16; ++slot)
     r[slot] = v[slot] != 0xFFFFFFFFu ? atomicAdd(&cnt[v[slot]], 1u) : 0u;
@@ -820,6 +840,142 @@ __global__ __launch_bounds__(256) void members_kernel(
         }
         got += __popcll(bal);
       }
+    }
+  }
+}
+
+// Small query windows (<= kSmallQ): select + member offsets + ordered member lists in ONE
+// work-group, one launch instead of five (select, offsets, fill, two orderings).  On the
+// few reserved CUs a one-image tail is a chain of dependent launches of a few microseconds
+// each whatever their work; here the phases are separated by work-group barriers.
+//   1. the window's queries are copied to LDS while the valid bins are compacted in
+//      first-touch order (first_touch_slots, as select_kernel; a running carry replaces the
+//      look-back: the work-group walks the queries in order)
+//   2. voff = exclusive scan of the bins' vote counts (as member_offsets_kernel)
+//   3. one wave per bin scans the queries in LDS from the bin's first touch until it has
+//      found all its votes, in query order by construction (the test of members_kernel)
+// Same outputs as the multi-kernel path: vbin, scal[0] = V, voff, scal[1], members.
+constexpr int kSmallT = 1024;
+constexpr int kSmallQ = 2048;
+constexpr int kSmallV = 2048;   // valid bins whose (bin, count, first touch, offset) stay in LDS
+
+__global__ __launch_bounds__(kSmallT) void select_small_kernel(
+    int64_t nq, const uint32_t* __restrict__ basekey, const uint32_t* __restrict__ vmask,
+    const uint32_t* __restrict__ gcount, const uint32_t* __restrict__ gfirst, Bins b,
+    const int* __restrict__ qimg, int64_t nbins1, uint32_t thr, uint32_t* __restrict__ vbin,
+    uint32_t* __restrict__ scal, int64_t* __restrict__ voff, int32_t* __restrict__ members) {
+  __shared__ uint32_t skey[kSmallQ], smask[kSmallQ];
+  __shared__ int simg[kSmallQ];
+  __shared__ uint32_t sh[kSmallT / 64];
+  __shared__ uint32_t vb_lb[kSmallV], vb_need[kSmallV], vb_first[kSmallV], vb_off[kSmallV];
+  __shared__ uint32_t carry_s;
+  __shared__ int64_t carry64_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int kW = kSmallT / 64;
+  if (tid == 0) {
+    carry_s = 0;
+    carry64_s = 0;
+  }
+  __syncthreads();
+  // 1. valid bins in first-touch order
+  for (int64_t q0 = 0; q0 < nq; q0 += kSmallT) {
+    const int64_t q = q0 + tid;
+    uint32_t tmp[16];
+    uint32_t n = 0;
+    if (q < nq) {
+      const int im = qimg ? qimg[q] : 0;
+      n = first_touch_slots(q, basekey, vmask, gcount, gfirst, b, (uint32_t)(im * nbins1), thr, tmp);
+      skey[q] = basekey[q];
+      smask[q] = vmask[q] & 0xFFFFu;
+      simg[q] = im;
+    }
+    uint32_t x = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t off = carry_s, tot = 0;
+    for (int i = 0; i < kW; ++i) {
+      if (i < w) off += sh[i];
+      tot += sh[i];
+    }
+    const uint32_t pos = off + x - n;
+    for (uint32_t i = 0; i < n; ++i) {
+      vbin[pos + i] = tmp[i];
+      if (pos + i < kSmallV) vb_lb[pos + i] = tmp[i];
+    }
+    __syncthreads();
+    if (tid == 0) carry_s += tot;
+    __syncthreads();
+  }
+  const int64_t V = carry_s;
+  // 2. member offsets
+  const bool in_lds = V <= kSmallV;
+  for (int64_t v0 = 0; v0 < V; v0 += kSmallT) {
+    const int64_t v = v0 + tid;
+    uint32_t c = 0u;
+    if (v < V) {
+      const uint32_t lb = in_lds ? vb_lb[v] : vbin[v];
+      c = gcount[lb];
+      if (in_lds) {
+        vb_need[v] = c;
+        vb_first[v] = gfirst[lb];
+      }
+    }
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int i = 0; i < kW; ++i) {
+      if (i < w) off += sh[i];
+      tot += sh[i];
+    }
+    const int64_t base = carry64_s;
+    if (v < V) {
+      voff[v] = base + off + x - c;
+      if (in_lds) vb_off[v] = (uint32_t)(base + off + x - c);   // < 16 * kSmallQ
+    }
+    __syncthreads();
+    if (tid == 0) carry64_s = base + tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    scal[0] = (uint32_t)V;
+    scal[1] = (uint32_t)carry64_s;
+    voff[V] = carry64_s;
+  }
+  __syncthreads();   // voff (global) written above is read by other waves below
+  // 3. members in query order, one wave per bin
+  for (int64_t v = w; v < V; v += kW) {
+    const uint32_t lb = in_lds ? vb_lb[v] : vbin[v];
+    const int img = qimg ? (int)(lb / nbins1) : 0;
+    const uint32_t ll = qimg ? (uint32_t)(lb % nbins1) : lb;   // bin within its image
+    const int bs_ = ll % b.s, bt_ = (ll / b.s) % b.t, by_ = (ll / (b.s * b.t)) % b.y,
+              bx_ = ll / (b.s * b.t * b.y);
+    const uint32_t need = in_lds ? vb_need[v] : gcount[lb];
+    const int64_t off = in_lds ? (int64_t)vb_off[v] : voff[v];
+    uint32_t got = 0;
+    for (int64_t q0 = (in_lds ? vb_first[v] : gfirst[lb]) >> 4; got < need && q0 < nq; q0 += 64) {
+      const int64_t q = q0 + lane;
+      bool mem = false;
+      if (q < nq && simg[q] == img) {
+        const uint32_t m = smask[q], key = skey[q];
+        const int dx = bx_ - (int)(key & 0xFF), dy = by_ - (int)((key >> 8) & 0xFF),
+                  dt = bt_ - (int)((key >> 16) & 0xFF), ds = bs_ - (int)(key >> 24);
+        if (m && (unsigned)dx <= 1u && (unsigned)dy <= 1u && (unsigned)dt <= 1u && (unsigned)ds <= 1u)
+          mem = (m >> (dx * 8 + dy * 4 + dt * 2 + ds)) & 1u;
+      }
+      const uint64_t bal = __ballot(mem);
+      if (mem) members[off + got + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)q;
+      got += __popcll(bal);
     }
   }
 }
@@ -1391,6 +1547,14 @@ static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* t
   return SOD_OK;
 }
 
+static int launch_members_multi(sod_ctx* ctx, uint32_t thr, int64_t nq);
+static int launch_means(sod_ctx* ctx);
+// SOD_SELECT_MULTI=1: small windows take the multi-kernel path too (parity tests of both)
+static bool select_multi_forced() {
+  const char* e = std::getenv("SOD_SELECT_MULTI");
+  return e && e[0] == '1';
+}
+
 int launch_select(sod_ctx* ctx, int32_t thr) {
   const int64_t nq = sod_win_n(ctx);
   std::swap(ctx->scal, ctx->scal_b);
@@ -1411,7 +1575,21 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
     SOD_TRY(sod_reserve(ctx, ctx->vidx, (size_t)ctx->nbins));
     SOD_HIP(ctx, hipMemsetAsync(ctx->vidx.p, 0xFF, ctx->vidx.n * 4, ctx->stream));
   }
-  SOD_TRY(run_compaction(ctx, (uint32_t)thr, ctx->vbin.p, ctx->scal.p + 0, ctx->vidx.p));
+  if (nq <= kSmallQ && !select_multi_forced()) {   // one work-group, one launch
+    hipLaunchKernelGGL(select_small_kernel, dim3(1), dim3(kSmallT), 0, ctx->stream, nq,
+                       ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
+                       qimg_p(ctx), ctx->nbins1, (uint32_t)thr, ctx->vbin.p, ctx->scal.p,
+                       ctx->voff.p, ctx->members.p);
+    SOD_HIP(ctx, hipGetLastError());
+  } else {
+    SOD_TRY(launch_members_multi(ctx, (uint32_t)thr, nq));
+  }
+  return launch_means(ctx);
+}
+
+// select + members over several work-groups (any window size)
+static int launch_members_multi(sod_ctx* ctx, uint32_t thr, int64_t nq) {
+  SOD_TRY(run_compaction(ctx, thr, ctx->vbin.p, ctx->scal.p + 0, ctx->vidx.p));
   hipLaunchKernelGGL(member_offsets_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->vbin.p,
                      ctx->counts.p, ctx->scal.p, ctx->voff.p, ctx->cursor.p);
   SOD_HIP(ctx, hipGetLastError());
@@ -1434,6 +1612,10 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
                        ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->members.p);
     SOD_HIP(ctx, hipGetLastError());
   }
+  return SOD_OK;
+}
+
+static int launch_means(sod_ctx* ctx) {
   // PoseBin means depend only on the member lists: they run on the side stream, beside the
   // affine verification and the next step's matcher tail (their inputs are double-buffered);
   // entry points that read results join them (set_dev)

@@ -574,3 +574,48 @@ def test_pipeline_empty_and_ragged(ctx, case):
     post = ctx.postprocess()                     # clustering of the survivors: also empty-safe
     if not any(r["survived"] for r in aff):
         assert len(post["final_pose"]) == 0
+
+
+@pytest.mark.parametrize("bins", [15, (32, 32, 8, 12)])
+def test_select_one_workgroup_equals_multi_kernel(bins, monkeypatch):
+    """Windows of <= 2048 queries take select + member lists in one work-group
+    (select_small_kernel); SOD_SELECT_MULTI=1 forces the multi-kernel path.  Both equal the
+    oracle and each other bit for bit (valid bins, votes, offsets, members, means, affine),
+    for a plain query window and for a fused batch of two images (image-major bin keys)."""
+    db = synthetic.make_database(12, 500, seed=91)
+    imgs = []
+    for k, (nq, shape) in enumerate(((1900, (800, 1000, 3)), (800, (600, 900, 3)),
+                                     (900, (1000, 1200, 3)))):
+        qs = synthetic.make_queries(nq, seed=92 + k, db_seed=91, kp_per_image=500,
+                                    n_objects=3, shape=shape)
+        imgs.append((qs.des, qs.kp, qs.shape))
+    res = {}
+    with _lib.Context(0) as c:
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        for multi in ("0", "1"):
+            monkeypatch.setenv("SOD_SELECT_MULTI", multi)
+            des, kp_, shape = imgs[0]
+            c.upload_queries(des, kp_)
+            c.pipeline(shape, bins)
+            one = (c.valid_result(), c.affine_result())
+            batch = sod.run_query_batch(c, imgs[1:], bins=bins, fused=True)   # 1700 queries
+            res[multi] = (one, batch)
+    (one0, b0), (one1, b1) = res["0"], res["1"]
+    for x, y in ((one0[0], one1[0]),) + tuple((p["valid"], q["valid"]) for p, q in zip(b0, b1)):
+        assert len(x["keys"]) > 0
+        for k in ("keys", "votes", "offsets", "members"):
+            assert np.array_equal(x[k], y[k]), k
+        np.testing.assert_array_equal(x["means"], y["means"])
+    for x, y in ((one0[1], one1[1]),) + tuple((p["affine"], q["affine"]) for p, q in zip(b0, b1)):
+        assert np.array_equal(x["survived"], y["survived"])
+        np.testing.assert_array_equal(x["params"], y["params"])
+    # oracle leg for the one-work-group results
+    des, kp_, shape = imgs[0]
+    dbkp, qkp, images = oracle_inputs(db, kp_)
+    o = orc.run_pipeline(des, qkp, db.des, dbkp, images, bins, shape)
+    assert_stages_equal_oracle(one0[0], one0[1], o["table"], o["valid"], o["affine"])
+    for (des, kp_, shape), b in zip(imgs[1:], b0):
+        dbkp, qkp, images = oracle_inputs(db, kp_)
+        o = orc.run_pipeline(des, qkp, db.des, dbkp, images, bins, shape)
+        assert_stages_equal_oracle(b["valid"], b["affine"], o["table"], o["valid"], o["affine"])
