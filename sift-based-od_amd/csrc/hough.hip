@@ -857,6 +857,15 @@ __global__ __launch_bounds__(256) void members_kernel(
 // Same outputs as the multi-kernel path: vbin, scal[0] = V, voff, scal[1], members.
 constexpr int kSmallT = 1024;
 constexpr int kSmallQ = 2048;
+#ifdef SOD_SEL_STAMP
+// diagnostic build only: s_memrealtime (100 MHz) at the phase boundaries of the last 64 launches
+__device__ unsigned long long g_selst[64][5];
+__device__ unsigned int g_selst_n;
+#define SEL_STAMP(i) \
+  if (tid == 0) st[i] = __builtin_amdgcn_s_memrealtime();
+#else
+#define SEL_STAMP(i)
+#endif
 constexpr int kSmallV = 2048;   // valid bins whose (bin, count, first touch, offset) stay in LDS
 
 __global__ __launch_bounds__(kSmallT) void select_small_kernel(
@@ -872,6 +881,10 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
   __shared__ int64_t carry64_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr int kW = kSmallT / 64;
+#ifdef SOD_SEL_STAMP
+  unsigned long long st[5] = {0, 0, 0, 0, 0};
+#endif
+  SEL_STAMP(0)
   if (tid == 0) {
     carry_s = 0;
     carry64_s = 0;
@@ -912,6 +925,7 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
     __syncthreads();
   }
   const int64_t V = carry_s;
+  SEL_STAMP(1)
   // 2. member offsets
   const bool in_lds = V <= kSmallV;
   for (int64_t v0 = 0; v0 < V; v0 += kSmallT) {
@@ -953,6 +967,7 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
     voff[V] = carry64_s;
   }
   __syncthreads();   // voff (global) written above is read by other waves below
+  SEL_STAMP(2)
   // 3. members in query order, one wave per bin
   for (int64_t v = w; v < V; v += kW) {
     const uint32_t lb = in_lds ? vb_lb[v] : vbin[v];
@@ -963,21 +978,32 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
     const uint32_t need = in_lds ? vb_need[v] : gcount[lb];
     const int64_t off = in_lds ? (int64_t)vb_off[v] : voff[v];
     uint32_t got = 0;
-    for (int64_t q0 = (in_lds ? vb_first[v] : gfirst[lb]) >> 4; got < need && q0 < nq; q0 += 64) {
-      const int64_t q = q0 + lane;
-      bool mem = false;
-      if (q < nq && simg[q] == img) {
-        const uint32_t m = smask[q], key = skey[q];
-        const int dx = bx_ - (int)(key & 0xFF), dy = by_ - (int)((key >> 8) & 0xFF),
-                  dt = bt_ - (int)((key >> 16) & 0xFF), ds = bs_ - (int)(key >> 24);
-        if (m && (unsigned)dx <= 1u && (unsigned)dy <= 1u && (unsigned)dt <= 1u && (unsigned)ds <= 1u)
-          mem = (m >> (dx * 8 + dy * 4 + dt * 2 + ds)) & 1u;
-      }
+    const int qn = (int)nq;
+    for (int q0 = (int)((in_lds ? vb_first[v] : gfirst[lb]) >> 4); got < need && q0 < qn; q0 += 64) {
+      // branch-free test (a lane past the window reads the last query and is masked off):
+      // nested conditions cost an exec-mask branch and an LDS wait each
+      const int q = q0 + lane;
+      const int qq = min(q, qn - 1);
+      const uint32_t m = smask[qq], key = skey[qq];
+      const int qimg_q = simg[qq];
+      const uint32_t dx = (uint32_t)(bx_ - (int)(key & 0xFF)), dy = (uint32_t)(by_ - (int)((key >> 8) & 0xFF)),
+                     dt = (uint32_t)(bt_ - (int)((key >> 16) & 0xFF)), ds = (uint32_t)(bs_ - (int)(key >> 24));
+      const bool win = (dx | dy | dt | ds) <= 1u;
+      const bool mem = (q < qn) & (qimg_q == img) & win & (((m >> ((dx * 8 + dy * 4 + dt * 2 + ds) & 15u)) & 1u) != 0u);
       const uint64_t bal = __ballot(mem);
       if (mem) members[off + got + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)q;
       got += __popcll(bal);
     }
   }
+#ifdef SOD_SEL_STAMP
+  __syncthreads();
+  SEL_STAMP(3)
+  if (tid == 0) {
+    const unsigned k = atomicAdd(&g_selst_n, 1u) % 64u;
+    for (int i = 0; i < 4; ++i) g_selst[k][i] = st[i];
+    g_selst[k][4] = (unsigned long long)V;
+  }
+#endif
 }
 
 // PoseBin running means in vote order (PoseBin.py:19-43).  The recurrence
@@ -1679,3 +1705,9 @@ int launch_affine(sod_ctx* ctx, int64_t nb_host, bool count_on_device, const int
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
+
+#ifdef SOD_SEL_STAMP
+extern "C" int sod_debug_selstamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_selst), sizeof(g_selst)) == hipSuccess ? 0 : 1;
+}
+#endif
