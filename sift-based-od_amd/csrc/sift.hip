@@ -357,57 +357,70 @@ __device__ inline int refl(int p, int len, const int* tab) {
   if (len <= kTabMax) return tab[p + kMaxR];
   return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
 }
-// one blur pass (rows: along x; else along y) of a w x h LDS image, taps unrolled (R a
-// template parameter); the arithmetic of blur_rows_kernel / blur_cols_kernel
+// The passes run over runs of kChainSeg consecutive outputs (along x for the row pass, along
+// y for the column pass) from a register window of kChainSeg + 2R inputs: ~1/3 the LDS reads
+// of one output per thread at R 13.  The window holds the same (reflected) inputs the
+// per-tap form reads, and every output is still k0*x + sum_{i=1..R} k_i*(x[-i] + x[+i]) in
+// increasing i (blur_rows_kernel / blur_cols_kernel's arithmetic).
+constexpr int kChainSeg = 4;
 template <int R>
-__device__ inline float blur_px_r(const float* img, int w, int h, int x, int y, bool row,
-                                  const float* k, const int* tabx, const int* taby) {
-  float s;
-  if (row) {
-    const float* p = img + y * w;
-    s = k[0] * p[x];
-    if (x >= R && x + R < w) {
-#pragma unroll
-      for (int j = 1; j <= R; ++j) s += k[j] * (p[x - j] + p[x + j]);
-    } else {
-#pragma unroll
-      for (int j = 1; j <= R; ++j) s += k[j] * (p[refl(x - j, w, tabx)] + p[refl(x + j, w, tabx)]);
-    }
-  } else {
-    const float* p = img + x;
-    s = k[0] * p[y * w];
-    if (y >= R && y + R < h) {
-#pragma unroll
-      for (int j = 1; j <= R; ++j) s += k[j] * (p[(y - j) * w] + p[(y + j) * w]);
-    } else {
-#pragma unroll
-      for (int j = 1; j <= R; ++j)
-        s += k[j] * (p[refl(y - j, h, taby) * w] + p[refl(y + j, h, taby) * w]);
-    }
-  }
-  return s;
-}
-template <int R>
-__device__ void chain_rows(const float* cur, float* T, int w, int h, const float* k, const int* tabx,
+__device__ __forceinline__ void chain_rows(const float* cur, float* T, int w, int h, const float* k, const int* tabx,
                            const int* taby, int tid) {
-  for (int t = tid; t < w * h; t += 1024) {
-    const int y = t / w, x = t - y * w;
-    T[t] = blur_px_r<R>(cur, w, h, x, y, true, k, tabx, taby);
+  const int runs = (w + kChainSeg - 1) / kChainSeg;
+  for (int t = tid; t < runs * h; t += 1024) {
+    const int y = t / runs, x0 = (t - y * runs) * kChainSeg;
+    const float* p = cur + y * w;
+    float win[kChainSeg + 2 * R];
+    if (x0 >= R && x0 + kChainSeg + R <= w) {
+#pragma unroll
+      for (int j = 0; j < kChainSeg + 2 * R; ++j) win[j] = p[x0 - R + j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < kChainSeg + 2 * R; ++j)   // (past x + R: feeds no stored output)
+        win[j] = p[refl(min(x0 - R + j, w - 1 + R), w, tabx)];
+    }
+#pragma unroll
+    for (int o = 0; o < kChainSeg; ++o) {
+      float s = k[0] * win[o + R];
+#pragma unroll
+      for (int i = 1; i <= R; ++i) s += k[i] * (win[o + R - i] + win[o + R + i]);
+      if (x0 + o < w) T[y * w + x0 + o] = s;
+    }
   }
 }
 template <int R>
-__device__ void chain_cols(const float* T, const float* cur, float* nxt, float* dst, float* dg,
+__device__ __forceinline__ void chain_cols(const float* T, const float* cur, float* nxt, float* dst, float* dg,
                            float* dgl, float* keep, int w, int h, const float* k, const int* tabx,
                            const int* taby, int tid) {
-  for (int t = tid; t < w * h; t += 1024) {
-    const int y = t / w, x = t - y * w;
-    const float s = blur_px_r<R>(T, w, h, x, y, false, k, tabx, taby);
-    const float d = s - cur[t];
-    nxt[t] = s;
-    dst[t] = s;
-    dg[t] = d;
-    dgl[t] = d;
-    if (keep) keep[t] = s;
+  const int runs = (h + kChainSeg - 1) / kChainSeg;
+  for (int t = tid; t < runs * w; t += 1024) {
+    const int x = t / runs, y0 = (t - x * runs) * kChainSeg;
+    const float* p = T + x;
+    float win[kChainSeg + 2 * R];
+    if (y0 >= R && y0 + kChainSeg + R <= h) {
+#pragma unroll
+      for (int j = 0; j < kChainSeg + 2 * R; ++j) win[j] = p[(y0 - R + j) * w];
+    } else {
+#pragma unroll
+      for (int j = 0; j < kChainSeg + 2 * R; ++j)
+        win[j] = p[refl(min(y0 - R + j, h - 1 + R), h, taby) * w];
+    }
+#pragma unroll
+    for (int o = 0; o < kChainSeg; ++o) {
+      float s = k[0] * win[o + R];
+#pragma unroll
+      for (int i = 1; i <= R; ++i) s += k[i] * (win[o + R - i] + win[o + R + i]);
+      const int y = y0 + o;
+      if (y < h) {
+        const int tt = y * w + x;
+        const float d = s - cur[tt];
+        nxt[tt] = s;
+        dst[tt] = s;
+        dg[tt] = d;
+        dgl[tt] = d;
+        if (keep) keep[tt] = s;
+      }
+    }
   }
 }
 #define SOD_CHAIN_CASES(F, ...)                                                         \
