@@ -440,7 +440,7 @@ __global__ __launch_bounds__(64 * kMergeW) void merge_kernel(
   // the matcher's shared thresholds of this partial-result slot: "nothing known" again for
   // the next launch that takes the slot (it waits for this merge)
   if (reset)
-    for (int r = 0; r < kThrWords; ++r) reset[q * kThrWords + r] = (int)0x80808080;
+    for (int r = 0; r < kThrWords; ++r) reset[(int64_t)r * nq + q] = (int)0x80808080;
   od1[q] = v1;
   oidx[q] = i1;
   od2[q] = v2;

@@ -241,6 +241,10 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_SLOTS
 #define SOD_I8_SLOTS 1     // shared bound from the best rows of the even / odd DB chunks
 #endif
+// threshold words a wave exchanges per query: t2, plus the two best-row slots below 8 query
+// tiles per wave (gthr layout: kThrWords regions of nq_pad words)
+template <int QT>
+constexpr int gwords() { return SOD_I8_SLOTS && QT <= 4 ? kThrWords : 1; }
 #ifndef SOD_I8_SEEDSLOT
 #define SOD_I8_SEEDSLOT 1  // the seed's best row goes out with the seed's t2
 #endif
@@ -557,14 +561,20 @@ __device__ __forceinline__ void match_unit(
   // different chunks, so min(even best, odd best) has two distinct rows at or above it and
   // is a valid bound too -- close to the second best over ALL rows the chunks have seen so
   // far, where the max of the chunks' own second bests lags far behind with many chunks.
-  // Layout: gthr[q * kThrWords + {0: t2, 1: even best, 2: odd best}] (h units).
+  // Layout: gthr[r * nq_pad + q], r = 0: t2, 1: even best, 2: odd best (h units).  The
+  // kernel at 8 query tiles per wave (C3) leaves the slots out: no time gained there, three
+  // times the exchange loads (gwords<QT>).
+  constexpr bool kSlots = gwords<QT>() > 1;
   const int wq = __builtin_amdgcn_readfirstlane(wave);
   const int ntile = max(0, min(QT, nqt - (qb * NW16 + wq) * QT));   // real tiles of the wave
-  int* const gw = gthr + (int64_t)(qb * NW16 + wq) * QT * 16 * kThrWords;   // the wave's queries
-  const __amdgpu_buffer_rsrc_t rg =
-      __builtin_amdgcn_make_buffer_rsrc((void*)gw, (short)0, ntile * 64 * kThrWords, kRsrcWord3);
+  const int64_t qw0 = (int64_t)(qb * NW16 + wq) * QT * 16;   // the wave's first query
+  int* const gw = gthr + qw0;
+  // one descriptor over the three words of the slot (a padding tile's load reads the next
+  // queries' words or, past the end, 0; its bound is never used)
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)gthr, (short)0, (int)(kThrWords * nq_pad * 4), kRsrcWord3);
   uint8_t* const gl =
-      lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64 * kThrWords);
+      lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64 * gwords<QT>());
   [[maybe_unused]] const int oslot = 1 + (sp & 1);   // this chunk's best-row word
 #endif
 #if SOD_I8_PIPE
@@ -625,9 +635,7 @@ __device__ __forceinline__ void match_unit(
       // normally, its rows below the seed skipped, instead of every tile of its 32 subtiles
       // taking the exact update (the dense phase).
       int sm[QT];
-#if SOD_I8_SLOTS
-      int sb1[QT];
-#endif
+      [[maybe_unused]] int sb1[QT];
 #pragma unroll
       for (int t = 0; t < QT; ++t) sm[t] = INT_MIN;
 #pragma unroll 1
@@ -653,17 +661,14 @@ __device__ __forceinline__ void match_unit(
         // out to the chunks of the same queries now: their first threshold load (this
         // stage's share_load) then already sees the other chunks' seeds
         if (lane < 16 && t < ntile) {
-          __hip_atomic_fetch_max(gw + (16 * t + lane) * kThrWords, t2[t], __ATOMIC_RELAXED,
+          __hip_atomic_fetch_max(gw + 16 * t + lane, t2[t], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
-#if SOD_I8_SLOTS && SOD_I8_SEEDSLOT
-          __hip_atomic_fetch_max(gw + (16 * t + lane) * kThrWords + oslot, g1, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-#endif
+          if constexpr (kSlots && SOD_I8_SEEDSLOT)
+            __hip_atomic_fetch_max(gw + oslot * nq_pad + 16 * t + lane, g1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
 #endif
-#if SOD_I8_SLOTS
-        sb1[t] = g1;   // the chunk's best so far (h), for the seed load below
-#endif
+        sb1[t] = g1;   // the chunk's best so far (h), for the seed load below (kSlots)
       }
 #if SOD_I8_XCHUNK && SOD_I8_SEEDPUB && SOD_I8_SEEDLOAD
       // the chunks of a query block run their seed passes side by side: one round trip
@@ -677,18 +682,18 @@ __device__ __forceinline__ void match_unit(
 #pragma unroll
         for (int t = 0; t < QT; ++t)   // one load per query (lanes 0-15), then to its groups
 #pragma unroll
-          for (int r = 0; r < kThrWords; ++r)
+          for (int r = 0; r < gwords<QT>(); ++r)
             gq[t][r] = lane < 16 && t < ntile
-                           ? __hip_atomic_load(gw + (16 * t + lane) * kThrWords + r,
+                           ? __hip_atomic_load(gw + r * nq_pad + 16 * t + lane,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                            : INT_MIN;
 #pragma unroll
         for (int t = 0; t < QT; ++t) {
-#if SOD_I8_SLOTS
-          const bool odd = oslot == 2;   // selects, not an indexed register array
-          const int own = max(odd ? gq[t][2] : gq[t][1], sb1[t]), other = odd ? gq[t][1] : gq[t][2];
-          gq[t][0] = max(gq[t][0], min(own, other));
-#endif
+          if constexpr (kSlots) {
+            const bool odd = oslot == 2;   // selects, not an indexed register array
+            const int own = max(odd ? gq[t][2] : gq[t][1], sb1[t]), other = odd ? gq[t][1] : gq[t][2];
+            gq[t][0] = max(gq[t][0], min(own, other));
+          }
           t2[t] = max(t2[t], __shfl(gq[t][0], lane & 15));
         }
       }
@@ -773,49 +778,46 @@ __device__ __forceinline__ void match_unit(
       // refill pieces went out before the load) it publishes its own t2 where above them and
       // raises t2 to them
       const bool xstage = kXEvery == 1 || s < kXDense || s % kXEvery == 0;   // wave-uniform
-      // the wave's QT x 16 x kThrWords values: QT*4*kThrWords lanes x 16 B, in pieces of 64
-      constexpr int kGLanes = QT * 4 * kThrWords;
-      if (share_load(u) && xstage) {
+      // the wave's QT x 16 values of each word: QT*4 lanes x 16 B per word
+      if (share_load(u) && xstage && lane < QT * 4) {
 #pragma unroll
-        for (int g = 0; g < kGLanes; g += 64)
-          if (lane < kGLanes - g)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_void*)(gl + g * 16), 16,
-                                                     (uint32_t)(g + lane) * 16u, 0, 0,
-                                                     16 /* sc1: past this XCD's L2 */);
+        for (int r = 0; r < gwords<QT>(); ++r)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rg, (lds_void*)(gl + r * QT * 64), 16,
+              (uint32_t)((qw0 + r * nq_pad) * 4) + (uint32_t)lane * 16u, 0, 0,
+              16 /* sc1: past this XCD's L2 */);
       }
       if (share_apply(u) && xstage && (SOD_I8_SHARE2 == 0 || u != 12 || s > 0)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15) * kThrWords;
+        const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15);
         // publishing is a device-scope atomic per query (a memory-side transaction each):
         // every stage while the thresholds still move fast, then every kPublishEvery-th
         const bool publish = s < kPublishDense || s % kPublishEvery == 0;
         int gq[QT];
-#if SOD_I8_SLOTS
-        int go[QT], gx[QT];
-#endif
+        [[maybe_unused]] int go[QT], gx[QT];
 #pragma unroll
         for (int t = 0; t < QT; ++t) {   // all reads, then one wait
-          gq[t] = gv[16 * kThrWords * t];
-#if SOD_I8_SLOTS
-          go[t] = gv[16 * kThrWords * t + oslot];
-          gx[t] = gv[16 * kThrWords * t + 3 - oslot];
-#endif
+          gq[t] = gv[16 * t];
+          if constexpr (kSlots) {
+            go[t] = gv[oslot * QT * 16 + 16 * t];
+            gx[t] = gv[(3 - oslot) * QT * 16 + 16 * t];
+          }
         }
 #pragma unroll
         for (int t = 0; t < QT; ++t) {
-#if SOD_I8_SLOTS
-          // the query-wide best of this wave's rows (y units -> h)
-          const int hb = max_xor3216(y1[t]) >> 1;
-          if (publish && lane < 16 && t < ntile && hb > go[t])
-            __hip_atomic_fetch_max(gw + (16 * t + lane) * kThrWords + oslot, hb,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          // t2 goes out only where it beats what every chunk derives from the words itself
-          // (a t2 raised by the slot bound would otherwise be re-published by all chunks at
-          // every exchange: same-address atomics that the vmcnt(0) above then waits for)
-          gq[t] = max(gq[t], min(max(go[t], hb), gx[t]));
-#endif
+          if constexpr (kSlots) {
+            // the query-wide best of this wave's rows (y units -> h)
+            const int hb = max_xor3216(y1[t]) >> 1;
+            if (publish && lane < 16 && t < ntile && hb > go[t])
+              __hip_atomic_fetch_max(gw + oslot * nq_pad + 16 * t + lane, hb, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            // t2 goes out only where it beats what every chunk derives from the words itself
+            // (a t2 raised by the slot bound would otherwise be re-published by all chunks at
+            // every exchange: same-address atomics that the vmcnt(0) above then waits for)
+            gq[t] = max(gq[t], min(max(go[t], hb), gx[t]));
+          }
           if (publish && lane < 16 && t < ntile && t2[t] > gq[t])
-            __hip_atomic_fetch_max(gw + (16 * t + lane) * kThrWords, t2[t], __ATOMIC_RELAXED,
+            __hip_atomic_fetch_max(gw + 16 * t + lane, t2[t], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
           t2[t] = max(t2[t], gq[t]);
         }
@@ -874,7 +876,7 @@ __global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
     int* __restrict__ pidx, float* __restrict__ pd2, int nqb, int* __restrict__ gthr,
     int seedload) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageBytes + kNormRing * kStageNorm +
-                                                     SOD_I8_XCHUNK * NW16 * QT * 64 * kThrWords];
+                                                     SOD_I8_XCHUNK * NW16 * QT * 64 * gwords<QT>()];
 #ifdef SOD_I8_STAMP
   unsigned long long t0 = 0, r0 = 0;
   if (threadIdx.x == 0) {

@@ -86,7 +86,7 @@ struct sod_ctx {
   DevBuf<float> cd1, cd2;       // merged (this shard / after allgather: global)  [nq_pad]
   DevBuf<int32_t> cidx;
   DevBuf<int32_t> gthr;         // matcher: prefilter thresholds shared by the DB chunks
-  int64_t gthr_n = 0;           //   [partial-result slot][nq_pad][kThrWords]; reset by the merge
+  int64_t gthr_n = 0;           //   [partial-result slot][kThrWords][nq_pad]; reset by the merge
   DevBuf<float> gd1, gd2;       // allgather landing [nranks * nq_pad]
   DevBuf<int32_t> gidx;
   DevBuf<float> d1, d2;         // sqrt distances [nq]
