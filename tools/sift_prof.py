@@ -11,8 +11,11 @@ sod_pkg.load()
 from sift_based_od_amd import _lib, synthetic  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+lane_order = int(sys.argv[2]) if len(sys.argv) > 2 else -1   # -1: the context's probe decides
 img = synthetic.textured_image(800, 1000, seed=2000)
 c = _lib.Context(0)
+if lane_order >= 0:
+    c.sift_set_lane_order(lane_order)
 for _ in range(5):
     c.sift_detect(img)
 c.synchronize()
