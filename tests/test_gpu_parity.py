@@ -95,6 +95,14 @@ def test_matcher_query_tiles_shared_thresholds(ctx, monkeypatch, qt):
     db[75001:75005] = db[75000]
     q[900:950] = db[0]
     q[950:1000] = db[75000]
+    # duplicates spread over chunks of both parities (the best-row slots: the even-chunk and
+    # odd-chunk bests are then EQUAL, so the bound equals both winners' value)
+    for a, b in ((25000, 130000), (33000, 91000), (47000, 118000), (61000, 62000)):
+        db[b:b + 100] = db[a:a + 100]
+    q[1000:1100] = db[25000:25100]
+    q[1100:1200] = db[33000:33100]
+    q[1200:1300] = np.clip(db[47000:47100].astype(int) + rng.integers(-1, 2, (100, 128)), 0, 255)
+    q[1300:1400] = db[61000:61100]
     ctx.set_impl("i8")
     ctx.upload_db(db)
     ctx.upload_queries(q)
