@@ -498,6 +498,20 @@ def main():
             ctx.synchronize()
             full.append(ctx.stage_ms())
         stage_full = np.mean(np.array(full), axis=0)
+    # one query image alone, start to finish: host clock around one step between two device
+    # syncs, tail on the whole chip -- the latency a single main.py query sees (the timed
+    # steps above overlap each image's tail with the next image's matcher)
+    lat = []
+    ctx.set_stage_timing(False)
+    for _ in range(5):
+        turn[0] = 0
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        step()
+        ctx.synchronize()
+        lat.append((time.perf_counter() - t0) * 1000.0)
+    ctx.set_stage_timing(True)
+    latency_ms = float(np.median(lat))
 
     # post-processing (main.py:159-168) over the surviving bins: timed
     # separately (it ends in a host DFS, so it is not inside the stream-ordered step)
@@ -580,6 +594,7 @@ def main():
         "stage_ms": dict({"match_kernel": match_ms, "match_kernel_isolated": match_iso},
                          **{k: float(v) for k, v in zip(_lib.Context.STAGES[1:], stage[1:])},
                          post_process=post_ms),
+        "single_image_latency_ms": latency_ms,
         "stage_ms_whole_chip": ({k: float(v) for k, v in zip(_lib.Context.STAGES, stage_full)}
                                 if stage_full is not None else None),
         "roofline_hough": roofline_hough,
