@@ -850,6 +850,8 @@ __device__ inline bool kp_same(const Kp& a, const Kp& b) {
 }
 
 constexpr int kRankTile = 64;
+constexpr int kSortMax = 3072;   // keypoint lists up to this size: sort_dedup_kernel
+constexpr int kSortPow2 = 4096;  // its bitonic network (the next power of two)
 // (i tile, j tile) pairs, strided over the grid.  pass 0: dup[i] |= an equal (x, y, size,
 // angle) keypoint precedes i; pass 1: before[i] += kept keypoints preceding i (the sorted
 // position)
@@ -860,6 +862,7 @@ __global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ 
   __shared__ Kp tile[kRankTile];
   __shared__ unsigned tdup[kRankTile];
   const int n = (int)min(*nkp, (unsigned)kcap);
+  if (n <= kSortMax) return;   // sort_dedup_kernel took it
   const int tiles = (n + kRankTile - 1) / kRankTile;
   for (int tp = blockIdx.x; tp < tiles * tiles; tp += gridDim.x) {
     const int i = (tp % tiles) * kRankTile + threadIdx.x;
@@ -894,9 +897,94 @@ __global__ void scatter_kernel(const Kp* __restrict__ kps, const unsigned* __res
                                const unsigned* __restrict__ dup, const unsigned* __restrict__ before,
                                Kp* __restrict__ sorted, unsigned* __restrict__ nfinal) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int)min(*nkp, (unsigned)kcap) || dup[i]) return;
+  const int n = (int)min(*nkp, (unsigned)kcap);
+  if (n <= kSortMax || i >= n || dup[i]) return;
   sorted[before[i]] = kps[i];
   atomicAdd(nfinal, 1u);
+}
+
+// Lists of up to kSortMax keypoints: OpenCV's order and dedup in ONE work-group instead of
+// the two O(n^2) rank passes and the scatter.  A bitonic sort of the indices under
+// kp_less (its index tie-break makes it a strict total order, so any correct sort gives the
+// rank kernels' order), then a keypoint is kept unless the one before it is kp_same (equal
+// (x, y, size, angle) keypoints are adjacent in that order: nothing sorts between them), and
+// the kept ones are compacted in order -- the output rank_kernel + scatter_kernel produce.
+// (x, y) as one 64-bit key that orders like kp_less's first two fields (IEEE order of the
+// float bits: flip the negatives, set the sign of the positives); equal keys (rare) fall back
+// to the full comparison
+__device__ inline uint32_t f32_order(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline bool key_less(const Kp* sk, uint64_t ka, int a, uint64_t kb, int b, int n) {
+  if (a >= n || b >= n) return a < b;   // padding sorts last (a < n <= b: real first)
+  if (ka != kb) return ka < kb;
+  return kp_less(sk[a], a, sk[b], b);
+}
+__global__ __launch_bounds__(1024) void sort_dedup_kernel(const Kp* __restrict__ kps,
+                                                          const unsigned* __restrict__ nkp, int kcap,
+                                                          Kp* __restrict__ sorted,
+                                                          unsigned* __restrict__ nfinal) {
+  __shared__ Kp sk[kSortMax];
+  __shared__ uint64_t k64[kSortPow2];   // the (x, y) keys, sorted with their indices
+  __shared__ unsigned short ix[kSortPow2];
+  __shared__ int wsum[16];
+  __shared__ int carry_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = (int)min(*nkp, (unsigned)kcap);
+  if (n > kSortMax) return;   // rank_kernel / scatter_kernel take it
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (int t = tid; t < n; t += 1024) {
+    const Kp kp = kps[t];
+    sk[t] = kp;
+    // -0.0 and +0.0 compare equal under kp_less: fold them (one key for both)
+    const float x = kp.x == 0.f ? 0.f : kp.x, y = kp.y == 0.f ? 0.f : kp.y;
+    k64[t] = (uint64_t)f32_order(x) << 32 | f32_order(y);
+  }
+  for (int t = tid; t < np2; t += 1024) {
+    ix[t] = (unsigned short)t;
+    if (t >= n) k64[t] = ~0ull;
+  }
+  if (tid == 0) carry_s = 0;
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int q = tid; q < (np2 >> 1); q += 1024) {   // pair q: t with bit j clear, p = t | j
+        const int t = ((q & ~(j - 1)) << 1) | (q & (j - 1)), p = t | j;
+        const int a = ix[t], b = ix[p];
+        const uint64_t ka = k64[t], kb = k64[p];
+        const bool asc = (t & k) == 0;
+        if (asc ? key_less(sk, kb, b, ka, a, n) : key_less(sk, ka, a, kb, b, n)) {
+          ix[t] = (unsigned short)b;
+          ix[p] = (unsigned short)a;
+          k64[t] = kb;
+          k64[p] = ka;
+        }
+      }
+      // a wave's 64 pairs of stage (k, j <= 64) lie in its own 128 elements, and one wave's
+      // LDS operations complete in order: only stages that cross waves need the barrier
+      const int jn = j > 1 ? j >> 1 : k;
+      if (j > 64 || jn > 64) __syncthreads();
+    }
+  __syncthreads();
+  for (int p0 = 0; p0 < n; p0 += 1024) {
+    const int p = p0 + tid;
+    const bool kept = p < n && (p == 0 || !kp_same(sk[ix[p - 1]], sk[ix[p]]));
+    const uint64_t m = __ballot(kept);
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int off = carry_s, tot = 0;
+    for (int i = 0; i < 16; ++i) {
+      off += i < w ? wsum[i] : 0;
+      tot += wsum[i];
+    }
+    if (kept) sorted[off + __popcll(m & ((1ull << lane) - 1ull))] = sk[ix[p]];
+    __syncthreads();
+    if (tid == 0) carry_s += tot;
+    __syncthreads();
+  }
+  if (tid == 0) *nfinal = (unsigned)carry_s;
 }
 
 // ---- descriptors: calcSIFTDescriptor, one 256-thread block per keypoint ---------------
@@ -1419,6 +1507,8 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                      S.cnt.p + 3);
   hipLaunchKernelGGL(orient_kernel, dim3(kOrientGrid), dim3(kOT), 0, st, S.gauss.p, P, S.surv.p,
                      S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap, W.lane_order);
+  hipLaunchKernelGGL(sort_dedup_kernel, dim3(1), dim3(1024), 0, st, S.kps.p, S.cnt.p + 1, cap,
+                     S.sorted.p, S.cnt.p + 2);
   SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)cap * 4, st));
   SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)cap * 4, st));
   for (int pass = 0; pass < 2; ++pass)
