@@ -21,6 +21,7 @@
 //   descriptors (one thread per keypoint, 4x4x8 trilinear histogram).
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -858,11 +859,11 @@ constexpr int kSortPow2 = 4096;  // its bitonic network (the next power of two)
 __global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ kps,
                                                          const unsigned* __restrict__ nkp, int kcap,
                                                          int pass, unsigned* __restrict__ dup,
-                                                         unsigned* __restrict__ before) {
+                                                         unsigned* __restrict__ before, int smax) {
   __shared__ Kp tile[kRankTile];
   __shared__ unsigned tdup[kRankTile];
   const int n = (int)min(*nkp, (unsigned)kcap);
-  if (n <= kSortMax) return;   // sort_dedup_kernel took it
+  if (n <= smax) return;   // sort_dedup_kernel took it
   const int tiles = (n + kRankTile - 1) / kRankTile;
   for (int tp = blockIdx.x; tp < tiles * tiles; tp += gridDim.x) {
     const int i = (tp % tiles) * kRankTile + threadIdx.x;
@@ -895,10 +896,10 @@ __global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ 
 
 __global__ void scatter_kernel(const Kp* __restrict__ kps, const unsigned* __restrict__ nkp, int kcap,
                                const unsigned* __restrict__ dup, const unsigned* __restrict__ before,
-                               Kp* __restrict__ sorted, unsigned* __restrict__ nfinal) {
+                               Kp* __restrict__ sorted, unsigned* __restrict__ nfinal, int smax) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = (int)min(*nkp, (unsigned)kcap);
-  if (n <= kSortMax || i >= n || dup[i]) return;
+  if (n <= smax || i >= n || dup[i]) return;
   sorted[before[i]] = kps[i];
   atomicAdd(nfinal, 1u);
 }
@@ -924,7 +925,7 @@ __device__ inline bool key_less(const Kp* sk, uint64_t ka, int a, uint64_t kb, i
 __global__ __launch_bounds__(1024) void sort_dedup_kernel(const Kp* __restrict__ kps,
                                                           const unsigned* __restrict__ nkp, int kcap,
                                                           Kp* __restrict__ sorted,
-                                                          unsigned* __restrict__ nfinal) {
+                                                          unsigned* __restrict__ nfinal, int smax) {
   __shared__ Kp sk[kSortMax];
   __shared__ uint64_t k64[kSortPow2];   // the (x, y) keys, sorted with their indices
   __shared__ unsigned short ix[kSortPow2];
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(1024) void sort_dedup_kernel(const Kp* __restrict__
   __shared__ int carry_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = (int)min(*nkp, (unsigned)kcap);
-  if (n > kSortMax) return;   // rank_kernel / scatter_kernel take it
+  if (n > smax) return;   // rank_kernel / scatter_kernel take it
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
   for (int t = tid; t < n; t += 1024) {
@@ -1507,15 +1508,18 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                      S.cnt.p + 3);
   hipLaunchKernelGGL(orient_kernel, dim3(kOrientGrid), dim3(kOT), 0, st, S.gauss.p, P, S.surv.p,
                      S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap, W.lane_order);
+  // SOD_SIFT_SORT_MAX (tests): a lower one-work-group limit, so the rank path runs too
+  int smax = kSortMax;
+  if (const char* e = std::getenv("SOD_SIFT_SORT_MAX")) smax = std::max(-1, std::min(kSortMax, std::atoi(e)));
   hipLaunchKernelGGL(sort_dedup_kernel, dim3(1), dim3(1024), 0, st, S.kps.p, S.cnt.p + 1, cap,
-                     S.sorted.p, S.cnt.p + 2);
+                     S.sorted.p, S.cnt.p + 2, smax);
   SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)cap * 4, st));
   SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)cap * 4, st));
   for (int pass = 0; pass < 2; ++pass)
     hipLaunchKernelGGL(rank_kernel, dim3(kRankGrid), dim3(kRankTile), 0, st, S.kps.p, S.cnt.p + 1, cap,
-                       pass, S.dup.p, S.before.p);
+                       pass, S.dup.p, S.before.p, smax);
   hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, S.kps.p,
-                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2);
+                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2, smax);
   hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, P, S.sorted.p,
                      S.cnt.p + 2, S.desc.p, W.lane_order);
   SOD_HIP(ctx, hipGetLastError());

@@ -139,6 +139,17 @@ def test_sift_parity_images(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sort_max", ["0", "64"])
+def test_sift_rank_path(ctx, monkeypatch, sort_max):
+    """Keypoint order + dedup: lists above SOD_SIFT_SORT_MAX (default 3072) take the O(n^2)
+    rank passes instead of the one-work-group sort; forcing that path (and a mixed limit)
+    gives the same bit-exact results against the C oracle."""
+    monkeypatch.setenv("SOD_SIFT_SORT_MAX", sort_max)
+    for name, img in _images().items():
+        _assert_same(ctx.sift_detect(img), osift.detect_and_compute(img), name + "/rank" + sort_max)
+
+
+@pytest.mark.gpu
 def test_sift_lane_order_paths(ctx):
     """Both histogram-add paths bit-exact against the C oracle on the reference's images
     (their orientation / descriptor bins collide inside one wave all the time, so the sums
