@@ -262,8 +262,10 @@ __global__ __launch_bounds__(256) void blur_tile_kernel(const float* __restrict_
                                                         float* __restrict__ dst, int w, int h,
                                                         const float* __restrict__ kern,
                                                         float* __restrict__ dog) {
-  constexpr int IW = kTW + 2 * R, IH = kTH + 2 * R;
-  __shared__ float in[IH * IW];
+  // IP: the LDS row pitch, odd, so the row pass's windows (8 rows x 8 runs per wave) spread
+  // over the banks
+  constexpr int IW = kTW + 2 * R, IH = kTH + 2 * R, IP = IW | 1, NS = (IW * IH + 255) / 256;
+  __shared__ float in[IH * IP];
   __shared__ float mid[IH * kTW];
   const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
   const int tid = threadIdx.x;
@@ -271,20 +273,30 @@ __global__ __launch_bounds__(256) void blur_tile_kernel(const float* __restrict_
 #pragma unroll
   for (int i = 0; i <= R; ++i) k[i] = kern[i];
   const bool interior = x0 >= R && x0 + kTW + R <= w && y0 >= R && y0 + kTH + R <= h;
-  for (int t = tid; t < IW * IH; t += 256) {
+  // staging: all NS loads of a thread in flight together (a load-then-store loop waits on
+  // each load in turn), the tail index clamped
+  float sv[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int t = min(tid + 256 * j, IW * IH - 1);
     const int u = t % IW, v = t / IW;
     int gx = x0 - R + u, gy = y0 - R + v;
     if (!interior) {
       gx = reflect101(gx, w);
       gy = reflect101(gy, h);
     }
-    in[t] = src[(size_t)gy * w + gx];
+    sv[j] = src[(size_t)gy * w + gx];
+  }
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int t = tid + 256 * j;
+    if (t < IW * IH) in[(t / IW) * IP + t % IW] = sv[j];
   }
   __syncthreads();
   // row pass: IH rows x (kTW / kSeg) runs
   for (int t = tid; t < IH * (kTW / kSeg); t += 256) {
     const int run = t % (kTW / kSeg), v = t / (kTW / kSeg);
-    const float* row = in + v * IW + run * kSeg;   // window starts R left of the first output
+    const float* row = in + v * IP + run * kSeg;   // window starts R left of the first output
     float win[kSeg + 2 * R];
 #pragma unroll
     for (int j = 0; j < kSeg + 2 * R; ++j) win[j] = row[j];
@@ -314,7 +326,7 @@ __global__ __launch_bounds__(256) void blur_tile_kernel(const float* __restrict_
       if (x < w && y < h) {
         const size_t oo = (size_t)y * w + x;
         dst[oo] = s;
-        if (dog) dog[oo] = s - in[(run * kSeg + o + R) * IW + R + u];
+        if (dog) dog[oo] = s - in[(run * kSeg + o + R) * IP + R + u];
       }
     }
   }
@@ -515,7 +527,7 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
       nxt = t2;
     }
     if (SOD_SIFT_EXP & 4) continue;
-    // extrema of this octave (extrema_kernel's test) on the LDS DoG layers
+    // extrema of this octave (extrema_all_kernel's test) on the LDS DoG layers
     const int iw = w - 2 * kBorder, ih = h - 2 * kBorder;
     if (iw > 0 && ih > 0) {
       for (int t = tid; t < iw * ih * L; t += 1024) {
@@ -554,21 +566,39 @@ __global__ void down2_kernel(const float* __restrict__ src, int sw, float* __res
 }
 
 // ---- extrema ------------------------------------------------------------------------
-__global__ void extrema_kernel(const float* __restrict__ dogs, Pyr P, int o, float thr,
-                               int4* __restrict__ cand, unsigned* __restrict__ ncand, int cap) {
+// 3x3x3 extrema of the octaves above the small-octave chain in ONE launch: block b of the
+// flat grid is block (b - first[o]) of octave o's (256-pixel x blocks, rows, layers) grid
+// (candidates are appended in any order: the keypoint sort orders them)
+constexpr int kExtRows = 8;   // rows per work-group: their centre loads are in flight together
+struct ExtGrid {
+  int first[kMaxOct + 1];   // first flat block of each octave; first[n] = total
+  int n;
+};
+__global__ void extrema_all_kernel(const float* __restrict__ dogs, Pyr P, ExtGrid G, float thr,
+                                   int4* __restrict__ cand, unsigned* __restrict__ ncand, int cap) {
+  int o = 0;
+  while (o + 1 < G.n && (int)blockIdx.x >= G.first[o + 1]) ++o;
   const Oct& q = P.o[o];
-  const int x = blockIdx.x * blockDim.x + threadIdx.x + kBorder, y = blockIdx.y + kBorder;
-  const int layer = blockIdx.z + 1;
+  const int bx = (q.w - 2 * kBorder + 255) / 256, rows = q.h - 2 * kBorder;
+  const int ry = (rows + kExtRows - 1) / kExtRows;
+  const int lb = (int)blockIdx.x - G.first[o];
+  const int layer = lb / (bx * ry) + 1, rem = lb % (bx * ry);
+  const int x = (rem % bx) * 256 + threadIdx.x + kBorder, y0 = (rem / bx) * kExtRows + kBorder;
   if (x >= q.w - kBorder) return;
   const size_t plane = (size_t)q.w * q.h;
   const float* cur = dogs + q.d + plane * layer;
-  const size_t c = (size_t)y * q.w + x;
-  const float val = cur[c];
-  if (!(fabsf(val) > thr)) return;
-  const bool ext = is_extremum(cur, plane, c, q.w, val);
-  if (!ext) return;
-  const unsigned i = atomicAdd(ncand, 1u);
-  if (i < (unsigned)cap) cand[i] = make_int4(o, layer, y, x);
+  float val[kExtRows];
+#pragma unroll
+  for (int r = 0; r < kExtRows; ++r)   // clamped rows: every load is unconditional
+    val[r] = cur[(size_t)min(y0 + r, q.h - kBorder - 1) * q.w + x];
+#pragma unroll
+  for (int r = 0; r < kExtRows; ++r) {
+    const int y = y0 + r;
+    if (y >= q.h - kBorder || !(fabsf(val[r]) > thr)) continue;
+    if (!is_extremum(cur, plane, (size_t)y * q.w + x, q.w, val[r])) continue;
+    const unsigned i = atomicAdd(ncand, 1u);
+    if (i < (unsigned)cap) cand[i] = make_int4(o, layer, y, x);
+  }
 }
 
 // ---- refine + orientation -------------------------------------------------------------
@@ -1228,6 +1258,10 @@ int gauss_kernel(double sigma, float* k) {
 // own stream (a batch keeps several images in flight)
 struct SiftSlot {
   hipStream_t stream = nullptr;
+  // a lone image runs the big octaves' extrema on `side`, beside the small-octave chain
+  // (one work-group) on `stream`; a batch keeps to one stream per image
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   Pyr P{};
   DevBuf<uint8_t> gray, bgr;
   DevBuf<float> gauss, dogs, tmp, up;
@@ -1277,6 +1311,10 @@ static void free_slot(SiftSlot* S) {
   sod_release(S->cnt);
   sod_release(S->desc);
   if (S->hcnt) (void)hipHostFree(S->hcnt);
+  if (S->side) (void)hipStreamSynchronize(S->side);
+  if (S->fork) (void)hipEventDestroy(S->fork);
+  if (S->join) (void)hipEventDestroy(S->join);
+  if (S->side) (void)hipStreamDestroy(S->side);
   if (S->stream) (void)hipStreamDestroy(S->stream);
   delete S;
 }
@@ -1452,7 +1490,7 @@ void plan_pyramid(int L, int w, int h, Pyr& P, int64_t& go, int64_t& dof, int& o
 
 // enqueue detect + describe of the image in S.gray on S.stream (no host sync); the counts
 // land in S.hcnt.  `pyramid` false re-runs only the stages after it (list overflow).
-int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, bool pyramid) {
+int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, bool pyramid, bool lone) {
   const int L = W.L;
   Pyr& P = S.P;
   int64_t go, dof;
@@ -1494,15 +1532,39 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                      S.dogs.p + q.d + plane * (i - 1)));
     }
   }
-  for (int o = 0; o < o_small; ++o) {
-    const Oct& q = P.o[o];
-    if (q.w <= 2 * kBorder || q.h <= 2 * kBorder) continue;
-    dim3 g((unsigned)((q.w - 2 * kBorder + 255) / 256), (unsigned)(q.h - 2 * kBorder), (unsigned)L);
-    hipLaunchKernelGGL(extrema_kernel, g, dim3(256), 0, st, S.dogs.p, P, o, thr, S.cand.p, S.cnt.p, cap);
+  {   // the octaves above the small-octave chain: one launch
+    ExtGrid G{};
+    int tot = 0;
+    for (int o = 0; o < o_small; ++o) {
+      const Oct& q = P.o[o];
+      G.first[o] = tot;
+      if (q.w > 2 * kBorder && q.h > 2 * kBorder)
+        tot += ((q.w - 2 * kBorder + 255) / 256) * ((q.h - 2 * kBorder + kExtRows - 1) / kExtRows) * L;
+    }
+    G.first[o_small] = tot;
+    G.n = o_small;
+    // both append to the candidate list (atomically; the keypoint sort fixes the order)
+    const bool split = lone && tot > 0 && o_small < nOct;
+    hipStream_t xs = st;
+    if (split) {
+      if (!S.side) {
+        SOD_HIP(ctx, hipStreamCreateWithFlags(&S.side, hipStreamNonBlocking));
+        SOD_HIP(ctx, hipEventCreateWithFlags(&S.fork, hipEventDisableTiming));
+        SOD_HIP(ctx, hipEventCreateWithFlags(&S.join, hipEventDisableTiming));
+      }
+      SOD_HIP(ctx, hipEventRecord(S.fork, st));
+      SOD_HIP(ctx, hipStreamWaitEvent(S.side, S.fork, 0));
+      xs = S.side;
+    }
+    if (tot > 0)
+      hipLaunchKernelGGL(extrema_all_kernel, dim3((unsigned)tot), dim3(256), 0, xs, S.dogs.p, P, G,
+                         thr, S.cand.p, S.cnt.p, cap);
+    if (split) SOD_HIP(ctx, hipEventRecord(S.join, S.side));
+    if (o_small < nOct)   // re-running it re-blurs the small octaves identically
+      hipLaunchKernelGGL(small_octaves_kernel, dim3(1), dim3(1024), 0, st, S.gauss.p, S.dogs.p, P,
+                         o_small, W.kern.p, W.rad.p, thr, S.cand.p, S.cnt.p, cap);
+    if (split) SOD_HIP(ctx, hipStreamWaitEvent(st, S.join, 0));
   }
-  if (o_small < nOct)   // re-running it re-blurs the small octaves identically
-    hipLaunchKernelGGL(small_octaves_kernel, dim3(1), dim3(1024), 0, st, S.gauss.p, S.dogs.p, P,
-                       o_small, W.kern.p, W.rad.p, thr, S.cand.p, S.cnt.p, cap);
   hipLaunchKernelGGL(refine_kernel, dim3((unsigned)((cap + 127) / 128)), dim3(128), 0, st, S.dogs.p, P,
                      S.cand.p, S.cnt.p, cap, (float)W.contrast, (float)W.edge, (float)W.sigma, S.surv.p,
                      S.cnt.p + 3);
@@ -1583,7 +1645,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
       SOD_TRY(get_slot(ctx, W, j, &S));
       const int i = i0 + j;
       SOD_TRY(slot_upload(ctx, *S, imgs[i], ws[i], hs[i], chans ? chans[i] : 1));
-      SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], true));
+      SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], true, m == 1));
     }
     for (int j = 0; j < m; ++j) {
       SiftSlot* S = W.slots[(size_t)j];
@@ -1595,7 +1657,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
         if (attempt >= 3) return sod_fail(ctx, SOD_ENOMEM, "SIFT: candidate list did not fit after growing");
         // grow and redo after the pyramid (the result does not depend on discovery order)
         S->cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)std::max(c0, c1));
-        SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], false));
+        SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], false, m == 1));
       }
       const int64_t cnt = S->hcnt[2];
       const int64_t at = W.off.back();

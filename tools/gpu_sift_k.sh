@@ -14,6 +14,6 @@ for r in csv.DictReader(open(sys.argv[1])):
 n = int(rows["descriptor_kernel"]["Calls"])
 tot = sum(float(r["TotalDurationNs"]) for r in rows.values()) / n / 1000
 print(sys.argv[2], "per image %.1f us" % tot, " ".join("%s %.1f" % (k, float(rows[k]["AverageNs"]) / 1000)
-      for k in ("descriptor_kernel", "small_octaves_kernel", "orient_kernel", "rank_kernel") if k in rows))
+      for k in ("descriptor_kernel", "small_octaves_kernel", "orient_kernel", "rank_kernel", "extrema_all_kernel", "sort_dedup_kernel") if k in rows))
 PY
 done
