@@ -436,6 +436,33 @@ __device__ __forceinline__ void chain_cols(const float* T, const float* cur, flo
     }
   }
 }
+// octaves of at most 1024 pixels: one output per thread, taps read straight from LDS (one
+// run per thread either way, and a run's cost is its instruction count); r is a run-time
+// value, the arithmetic the same as above
+__device__ __forceinline__ void chain_rows1(const float* cur, float* T, int w, int h, int r,
+                                            const float* k, const int* tabx, int tid) {
+  if (tid >= w * h) return;
+  const int y = tid / w, x = tid - y * w;
+  const float* p = cur + y * w;
+  float s = k[0] * p[x];
+  for (int i = 1; i <= r; ++i) s += k[i] * (p[refl(x - i, w, tabx)] + p[refl(x + i, w, tabx)]);
+  T[tid] = s;
+}
+__device__ __forceinline__ void chain_cols1(const float* T, const float* cur, float* nxt, float* dst,
+                                            float* dg, float* dgl, float* keep, int w, int h, int r,
+                                            const float* k, const int* taby, int tid) {
+  if (tid >= w * h) return;
+  const int y = tid / w, x = tid - y * w;
+  const float* p = T + x;
+  float s = k[0] * p[y * w];
+  for (int i = 1; i <= r; ++i) s += k[i] * (p[refl(y - i, h, taby) * w] + p[refl(y + i, h, taby) * w]);
+  const float d = s - cur[tid];
+  nxt[tid] = s;
+  dst[tid] = s;
+  dg[tid] = d;
+  dgl[tid] = d;
+  if (keep) keep[tid] = s;
+}
 #define SOD_CHAIN_CASES(F, ...)                                                         \
   switch (r) {                                                                          \
     case 1: F<1>(__VA_ARGS__); break;   case 2: F<2>(__VA_ARGS__); break;               \
@@ -513,13 +540,19 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
     float* nxt = C;
     for (int i = 1; i < L + 3; ++i) {
       const int r = radius[i];
-      SOD_CHAIN_CASES(chain_rows, cur, T, w, h, kk[i], tabx, taby, tid)
+      if (np <= 1024)
+        chain_rows1(cur, T, w, h, r, kk[i], tabx, tid);
+      else
+        SOD_CHAIN_CASES(chain_rows, cur, T, w, h, kk[i], tabx, taby, tid)
       lds_barrier();
       SIFT_STAMP(stamp++)
       float* dst = g0 + (size_t)np * i;
       float* dg = dogs + q.d + (size_t)np * (i - 1);
-      SOD_CHAIN_CASES(chain_cols, T, cur, nxt, dst, dg, Dg[i - 1], i == L ? Bl : nullptr, w, h,
-                      kk[i], tabx, taby, tid)
+      if (np <= 1024)
+        chain_cols1(T, cur, nxt, dst, dg, Dg[i - 1], i == L ? Bl : nullptr, w, h, r, kk[i], taby, tid);
+      else
+        SOD_CHAIN_CASES(chain_cols, T, cur, nxt, dst, dg, Dg[i - 1], i == L ? Bl : nullptr, w, h,
+                        kk[i], tabx, taby, tid)
       lds_barrier();
       SIFT_STAMP(stamp++)
       float* t2 = cur;
