@@ -253,9 +253,12 @@ __global__ void blur_cols_kernel(const float* __restrict__ src, float* __restric
 // fused separable blur of one kTW x kTH output tile, radius R a template parameter: the
 // source tile with an R-pixel halo (rows and columns reflected, BORDER_REFLECT_101) is
 // staged in LDS; the row pass (each thread a run of kSeg outputs from a register window)
-// writes an LDS intermediate, the column pass (runs of kSeg down a column) the output and
-// the DoG = output - source.  Per output the arithmetic is exactly blur_rows_kernel's
-// then blur_cols_kernel's: k0*x + sum_{i=1..R} k_i*(x[-i] + x[+i]) in increasing i.
+// writes its results over the source row it read, as the intermediate (one LDS tile per
+// work-group: more work-groups per CU) -- a row's runs are 8 lanes of one wave, whose LDS
+// reads all precede its writes; the column pass (runs of kSeg down a column) writes the
+// output and the DoG = output - source (the source values read before the row pass).  Per output the
+// arithmetic is exactly blur_rows_kernel's then blur_cols_kernel's:
+// k0*x + sum_{i=1..R} k_i*(x[-i] + x[+i]) in increasing i.
 constexpr int kTW = 64, kTH = 32, kSeg = 8, kMaxR = 16;
 template <int R>
 __global__ __launch_bounds__(256) void blur_tile_kernel(const float* __restrict__ src,
@@ -265,8 +268,9 @@ __global__ __launch_bounds__(256) void blur_tile_kernel(const float* __restrict_
   // IP: the LDS row pitch, odd, so the row pass's windows (8 rows x 8 runs per wave) spread
   // over the banks
   constexpr int IW = kTW + 2 * R, IH = kTH + 2 * R, IP = IW | 1, NS = (IW * IH + 255) / 256;
-  __shared__ float in[IH * IP];
-  __shared__ float mid[IH * kTW];
+  static_assert(kTW * (kTH / kSeg) == 256, "one column run per thread");
+  static_assert(kTW / kSeg == 8 && 64 % (kTW / kSeg) == 0, "a row's runs in one wave");
+  __shared__ float in[IH * IP];   // the source tile, then the row pass's output (pitch IP)
   const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH;
   const int tid = threadIdx.x;
   float k[R + 1];
@@ -293,40 +297,50 @@ __global__ __launch_bounds__(256) void blur_tile_kernel(const float* __restrict_
     if (t < IW * IH) in[(t / IW) * IP + t % IW] = sv[j];
   }
   __syncthreads();
-  // row pass: IH rows x (kTW / kSeg) runs
-  for (int t = tid; t < IH * (kTW / kSeg); t += 256) {
+  // this thread's column run (u, cr): its source values, for the DoG
+  const int u = tid % kTW, cr = tid / kTW;
+  float dv[kSeg];
+#pragma unroll
+  for (int o = 0; o < kSeg; ++o) dv[o] = in[(cr * kSeg + o + R) * IP + R + u];
+  __syncthreads();   // before any row is overwritten
+  // row pass: IH rows x (kTW / kSeg) runs, each row's output over its own source row
+  for (int t = tid; t < IH * (kTW / kSeg); t += 256) {   // (wave-uniform trip count per row)
     const int run = t % (kTW / kSeg), v = t / (kTW / kSeg);
-    const float* row = in + v * IP + run * kSeg;   // window starts R left of the first output
+    float* row = in + v * IP + run * kSeg;   // window starts R left of the first output
     float win[kSeg + 2 * R];
 #pragma unroll
     for (int j = 0; j < kSeg + 2 * R; ++j) win[j] = row[j];
+    float res[kSeg];
 #pragma unroll
     for (int o = 0; o < kSeg; ++o) {
       float s = k[0] * win[o + R];
 #pragma unroll
       for (int i = 1; i <= R; ++i) s += k[i] * (win[o + R - i] + win[o + R + i]);
-      mid[v * kTW + run * kSeg + o] = s;
+      res[o] = s;
     }
+    // the row's other lanes read these words too: no write moves above this wave's reads
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int o = 0; o < kSeg; ++o) row[o] = res[o];
   }
   __syncthreads();
-  // column pass: kTW columns x (kTH / kSeg) runs
-  for (int t = tid; t < kTW * (kTH / kSeg); t += 256) {
-    const int u = t % kTW, run = t / kTW;
-    const float* col = mid + run * kSeg * kTW + u;
+  // column pass: kTW columns x (kTH / kSeg) runs, one per thread
+  {
+    const float* col = in + cr * kSeg * IP + u;
     float win[kSeg + 2 * R];
 #pragma unroll
-    for (int j = 0; j < kSeg + 2 * R; ++j) win[j] = col[j * kTW];
+    for (int j = 0; j < kSeg + 2 * R; ++j) win[j] = col[j * IP];
     const int x = x0 + u;
 #pragma unroll
     for (int o = 0; o < kSeg; ++o) {
-      const int y = y0 + run * kSeg + o;
+      const int y = y0 + cr * kSeg + o;
       float s = k[0] * win[o + R];
 #pragma unroll
       for (int i = 1; i <= R; ++i) s += k[i] * (win[o + R - i] + win[o + R + i]);
       if (x < w && y < h) {
         const size_t oo = (size_t)y * w + x;
         dst[oo] = s;
-        if (dog) dog[oo] = s - in[(run * kSeg + o + R) * IP + R + u];
+        if (dog) dog[oo] = s - dv[o];
       }
     }
   }
