@@ -1072,6 +1072,13 @@ __global__ __launch_bounds__(1024) void sort_dedup_kernel(const Kp* __restrict__
 // bins of a sample are distinct), so every bin sums in OpenCV's order.
 constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);
 constexpr int kDT = 256;
+// a histogram index in one of the d x d inner cells: the only bins the descriptor reads (the
+// border ring, ~1/3 of the trilinear contributions, and the dummy padding bins are skipped;
+// every inner bin still receives its adds in sample order)
+__device__ __forceinline__ bool inner_bin(int b) {
+  const int cell = b / (kN + 2), r = cell / (kD + 2), c = cell - r * (kD + 2);
+  return r >= 1 && r <= kD && c >= 1 && c <= kD;
+}
 __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
                                                          const Kp* __restrict__ sorted,
                                                          const unsigned* __restrict__ nfinal,
@@ -1184,8 +1191,10 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
         const int offe = e == 0 ? 0 : e == 1 ? 1 : e == 2 ? kN + 2 : e == 3 ? kN + 3
                        : e == 4 ? (kD + 2) * (kN + 2) : e == 5 ? (kD + 2) * (kN + 2) + 1
                        : e == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
-        for (int t0 = 0; t0 < nv; t0 += 8)
-          if (t0 + s8 < nv) atomicAdd(&hist[sidx[t0 + s8] + offe], svalT[e][t0 + s8]);
+        for (int t0 = 0; t0 < nv; t0 += 8) {
+          const int b = sidx[t0 + s8] + offe;
+          if (t0 + s8 < nv && inner_bin(b)) atomicAdd(&hist[b], svalT[e][t0 + s8]);
+        }
       }
       } else if (tid < 8 && !(SOD_SIFT_EXP & 1)) {
         // 16 samples' indices and this lane's values read as 128-bit vectors, then the
@@ -1200,10 +1209,10 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            atomicAdd(&hist[i4[u].x + off], v4[u].x);
-            atomicAdd(&hist[i4[u].y + off], v4[u].y);
-            atomicAdd(&hist[i4[u].z + off], v4[u].z);
-            atomicAdd(&hist[i4[u].w + off], v4[u].w);
+            if (inner_bin(i4[u].x + off)) atomicAdd(&hist[i4[u].x + off], v4[u].x);
+            if (inner_bin(i4[u].y + off)) atomicAdd(&hist[i4[u].y + off], v4[u].y);
+            if (inner_bin(i4[u].z + off)) atomicAdd(&hist[i4[u].z + off], v4[u].z);
+            if (inner_bin(i4[u].w + off)) atomicAdd(&hist[i4[u].w + off], v4[u].w);
           }
         }
       }
