@@ -294,6 +294,18 @@ def test_sift_batch_equals_single(ctx):
 
 
 @pytest.mark.gpu
+def test_sift_batch_lone_tail_image(ctx):
+    """Five images: four in flight, then the fifth alone, which runs the big octaves'
+    extrema on the slot's side stream beside the small-octave chain (sift.hip
+    slot_enqueue); every image equals the oracle."""
+    batch = [synthetic.textured_image(h, w, seed=70 + i)
+             for i, (h, w) in enumerate([(120, 160), (96, 128), (150, 110), (80, 200), (180, 240)])]
+    out = ctx.sift_detect_batch(batch)
+    for i, (img, dev) in enumerate(zip(batch, out)):
+        _assert_same(dev, osift.detect_and_compute(img), "batch %d" % i)
+
+
+@pytest.mark.gpu
 def test_sift_query_batch_equals_per_image(ctx):
     """SURVEY 8(f) rows 3 + 4: three query images -> SIFT batch -> one matcher pass ->
     fused stages equals each image run alone through Main.get_query_image."""
