@@ -1066,12 +1066,13 @@ __global__ __launch_bounds__(1024) void sort_dedup_kernel(const Kp* __restrict__
 }
 
 // ---- descriptors: calcSIFTDescriptor, one 256-thread block per keypoint ---------------
-// The window's samples are computed 256 at a time (one per thread, OpenCV's row-major
-// order), compacted in that order, and their eight trilinear contributions added to the
-// LDS histogram sample by sample (lanes 0-7 of wave 0, one contribution each: the eight
-// bins of a sample are distinct), so every bin sums in OpenCV's order.
+// The window's samples are computed 192 at a time by waves 1-3 (one per thread, OpenCV's
+// row-major order), compacted in that order, and their eight trilinear contributions added
+// to the LDS histogram by wave 0 one chunk behind, sample by sample (the eight bins of a
+// sample are distinct), so every bin sums in OpenCV's order.
 constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);
 constexpr int kDT = 256;
+constexpr int kDP = kDT - 64;   // window samples per chunk: waves 1-3 produce, wave 0 adds
 // a histogram index in one of the d x d inner cells: the only bins the descriptor reads (the
 // border ring, ~1/3 of the trilinear contributions, and the dummy padding bins are skipped;
 // every inner bin still receives its adds in sample order)
@@ -1083,12 +1084,12 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
                                                          const Kp* __restrict__ sorted,
                                                          const unsigned* __restrict__ nfinal,
                                                          float* __restrict__ desc, int lane_order) {
-  __shared__ float hist[kHistLen + 72];   // + a dummy region for the padding samples
-  __shared__ __attribute__((aligned(16))) int sidx[kDT + 16];
-  __shared__ __attribute__((aligned(16))) float svalT[8][kDT + 16];
+  __shared__ float hist[kHistLen];
+  __shared__ int sidx[2][kDP / 64][64];           // [buffer][producer wave][compacted slot]
+  __shared__ float svalT[2][kDP / 64][8][64];     // the 8 contributions of each slot
+  __shared__ int nseg[2][kDP / 64];
   __shared__ float raw[kD * kD * kN];
   __shared__ float scal[2];
-  __shared__ int wcnt[kDT / 64];
   const int tid = threadIdx.x;
   const int nf = (int)*nfinal;
 #if SOD_SIFT_WAVE_ORDER_ARCH
@@ -1129,94 +1130,106 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
     for (int t = tid; t < kHistLen; t += kDT) hist[t] = 0.f;
     const int side = 2 * radius + 1;
     const int64_t total = (int64_t)side * side;
-    for (int64_t p0 = 0; p0 < total; p0 += kDT) {
-      const int64_t p = p0 + tid;
-      const int i = (int)(p / side) - radius, j = (int)(p % side) - radius;
-      const float c_rot = j * cos_t - i * sin_t;
-      const float r_rot = j * sin_t + i * cos_t;
-      float rbin = r_rot + kD / 2 - 0.5f;
-      float cbin = c_rot + kD / 2 - 0.5f;
-      const int r = py + i, c = px + j;
-      const bool ok = p < total && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 &&
-                      r < rows - 1 && c > 0 && c < cols - 1;
-      int idx = 0;
-      float v8[8];
-      if (ok) {
-        const float dx = at(img, cols, r, c + 1) - at(img, cols, r, c - 1);
-        const float dy = at(img, cols, r - 1, c) - at(img, cols, r + 1, c);
-        const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
-        const float o_k = fast_atan2(dy, dx);
-        const float mag_k = fmag(dx, dy);
-        const float w_k = fexp(wexp);
-        float obin = (o_k - ori) * bins_per_rad;
-        const float mag = mag_k * w_k;
-        const int r0 = flo(rbin), c0 = flo(cbin);
-        int o0 = flo(obin);
-        rbin -= r0;
-        cbin -= c0;
-        obin -= o0;
-        if (o0 < 0) o0 += kN;
-        if (o0 >= kN) o0 -= kN;
-        const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-        const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-        const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-        v8[7] = v_rc11 * obin;            // v_rco111
-        v8[6] = v_rc11 - v8[7];           // v_rco110
-        v8[5] = v_rc10 * obin;            // v_rco101
-        v8[4] = v_rc10 - v8[5];           // v_rco100
-        v8[3] = v_rc01 * obin;            // v_rco011
-        v8[2] = v_rc01 - v8[3];           // v_rco010
-        v8[1] = v_rc00 * obin;            // v_rco001
-        v8[0] = v_rc00 - v8[1];           // v_rco000
-        idx = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
-      }
-      int nv;
-      const int slot = block_compact_slot(ok, wcnt, nv);
-      if (ok) {
-        sidx[slot] = idx;
+    // Waves 1-3 compute chunk c (192 window samples, one per thread, OpenCV's row-major
+    // order) while wave 0 adds chunk c-1 into the histogram: two buffers, one barrier per
+    // chunk.  Each producer wave compacts its 64 samples into its own segment (ballot, no
+    // barrier); segments 1, 2, 3 in turn are the chunk's samples in order.
+    const int64_t nch = (total + kDP - 1) / kDP;
+    const int wv = tid >> 6, lane = tid & 63;
+    for (int64_t ch = 0; ch <= nch; ++ch) {
+      const int buf = (int)(ch & 1);
+      if (wv > 0 && ch < nch) {
+        const int64_t p = ch * kDP + (tid - 64);
+        const int i = (int)(p / side) - radius, j = (int)(p % side) - radius;
+        const float c_rot = j * cos_t - i * sin_t;
+        const float r_rot = j * sin_t + i * cos_t;
+        float rbin = r_rot + kD / 2 - 0.5f;
+        float cbin = c_rot + kD / 2 - 0.5f;
+        const int r = py + i, c = px + j;
+        const bool ok = p < total && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 &&
+                        r < rows - 1 && c > 0 && c < cols - 1;
+        int idx = 0;
+        float v8[8];
+        if (ok) {
+          const float dx = at(img, cols, r, c + 1) - at(img, cols, r, c - 1);
+          const float dy = at(img, cols, r - 1, c) - at(img, cols, r + 1, c);
+          const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
+          const float o_k = fast_atan2(dy, dx);
+          const float mag_k = fmag(dx, dy);
+          const float w_k = fexp(wexp);
+          float obin = (o_k - ori) * bins_per_rad;
+          const float mag = mag_k * w_k;
+          const int r0 = flo(rbin), c0 = flo(cbin);
+          int o0 = flo(obin);
+          rbin -= r0;
+          cbin -= c0;
+          obin -= o0;
+          if (o0 < 0) o0 += kN;
+          if (o0 >= kN) o0 -= kN;
+          const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+          const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+          const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+          v8[7] = v_rc11 * obin;            // v_rco111
+          v8[6] = v_rc11 - v8[7];           // v_rco110
+          v8[5] = v_rc10 * obin;            // v_rco101
+          v8[4] = v_rc10 - v8[5];           // v_rco100
+          v8[3] = v_rc01 * obin;            // v_rco011
+          v8[2] = v_rc01 - v8[3];           // v_rco010
+          v8[1] = v_rc00 * obin;            // v_rco001
+          v8[0] = v_rc00 - v8[1];           // v_rco000
+          idx = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
+        }
+        const uint64_t m = __ballot(ok);
+        const int sg = wv - 1;
+        if (ok) {
+          const int slot = __popcll(m & ((1ull << lane) - 1ull));
+          sidx[buf][sg][slot] = idx;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) svalT[e][slot] = v8[e];
+          for (int e = 0; e < 8; ++e) svalT[buf][sg][e][slot] = v8[e];
+        }
+        if (lane == 0) nseg[buf][sg] = __popcll(m);
       }
-      if (tid < 16) {   // pad to a multiple of 16 with zero adds to the dummy bins
-        sidx[nv + tid] = kHistLen;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) svalT[e][nv + tid] = 0.f;
-      }
-      __syncthreads();
-      if (wave_order) {
-      // wave 0 adds 8 samples per LDS atomic instruction: lane 8 s + e carries contribution
-      // e of sample s (same-bin lanes apply in lane order = sample order, see orient_kernel)
-      if (tid < 64 && !(SOD_SIFT_EXP & 1)) {
-        const int s8 = tid >> 3, e = tid & 7;
-        const int offe = e == 0 ? 0 : e == 1 ? 1 : e == 2 ? kN + 2 : e == 3 ? kN + 3
-                       : e == 4 ? (kD + 2) * (kN + 2) : e == 5 ? (kD + 2) * (kN + 2) + 1
-                       : e == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
-        for (int t0 = 0; t0 < nv; t0 += 8) {
-          const int b = sidx[t0 + s8] + offe;
-          if (t0 + s8 < nv && inner_bin(b)) atomicAdd(&hist[b], svalT[e][t0 + s8]);
+      if (wv == 0 && ch > 0) {
+        const int pb = buf ^ 1;
+        if (wave_order) {
+          // 8 samples per LDS atomic instruction: lane 8 s + e carries contribution e of
+          // sample s (same-bin lanes apply in lane order = sample order, see orient_kernel);
+          // the next group's operands are read before this group's atomic goes out (a wave's
+          // LDS operations complete in order: reads issued after the atomic would wait on it)
+          const int s8 = lane >> 3, e = lane & 7;
+          const int offe = e == 0 ? 0 : e == 1 ? 1 : e == 2 ? kN + 2 : e == 3 ? kN + 3
+                         : e == 4 ? (kD + 2) * (kN + 2) : e == 5 ? (kD + 2) * (kN + 2) + 1
+                         : e == 6 ? (kD + 3) * (kN + 2) : (kD + 3) * (kN + 2) + 1;
+          for (int sg = 0; sg < kDP / 64; ++sg) {
+            const int n = nseg[pb][sg];
+            int b = sidx[pb][sg][min(s8, 63)] + offe;
+            float v = svalT[pb][sg][e][min(s8, 63)];
+            for (int t0 = 0; t0 < n; t0 += 8) {
+              const int tn = min(t0 + 8 + s8, 63);
+              const int bn = sidx[pb][sg][tn] + offe;
+              const float vn = svalT[pb][sg][e][tn];
+              if (t0 + s8 < n && inner_bin(b)) {
+                if (SOD_SIFT_EXP & 1)   // timing build: a plain store (wrong sums)
+                  hist[b] = v;
+                else
+                  atomicAdd(&hist[b], v);
+              }
+              b = bn;
+              v = vn;
+            }
+          }
+        } else if (lane < 8) {
+          // ordered single-lane adds: lane e adds contribution e, one sample per instruction
+          for (int sg = 0; sg < kDP / 64; ++sg) {
+            const int n = nseg[pb][sg];
+            for (int t = 0; t < n; ++t) {
+              const int b = sidx[pb][sg][t] + off;
+              if (inner_bin(b)) atomicAdd(&hist[b], svalT[pb][sg][lane][t]);
+            }
+          }
         }
       }
-      } else if (tid < 8 && !(SOD_SIFT_EXP & 1)) {
-        // 16 samples' indices and this lane's values read as 128-bit vectors, then the
-        // 16 adds (in order, fire-and-forget)
-        for (int t0 = 0; t0 < nv; t0 += 16) {
-          int4 i4[4];
-          float4 v4[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            i4[u] = *reinterpret_cast<const int4*>(&sidx[t0 + 4 * u]);
-            v4[u] = *reinterpret_cast<const float4*>(&svalT[tid][t0 + 4 * u]);
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (inner_bin(i4[u].x + off)) atomicAdd(&hist[i4[u].x + off], v4[u].x);
-            if (inner_bin(i4[u].y + off)) atomicAdd(&hist[i4[u].y + off], v4[u].y);
-            if (inner_bin(i4[u].z + off)) atomicAdd(&hist[i4[u].z + off], v4[u].z);
-            if (inner_bin(i4[u].w + off)) atomicAdd(&hist[i4[u].w + off], v4[u].w);
-          }
-        }
-      }
-      __syncthreads();
+      __syncthreads();   // chunk ch written, chunk ch-1 added: the buffers swap roles
     }
     // finalize: fold the circular orientation bins, then OpenCV's sequential norms
     if (tid < kD * kD) {
