@@ -1073,6 +1073,7 @@ __global__ __launch_bounds__(1024) void sort_dedup_kernel(const Kp* __restrict__
 constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);
 constexpr int kDT = 256;
 constexpr int kDP = kDT - 64;   // window samples per chunk: waves 1-3 produce, wave 0 adds
+constexpr int kDescSide = kDT;  // windows up to this many rows enumerate per-row j ranges
 // a histogram index in one of the d x d inner cells: the only bins the descriptor reads (the
 // border ring, ~1/3 of the trilinear contributions, and the dummy padding bins are skipped;
 // every inner bin still receives its adds in sample order)
@@ -1088,6 +1089,8 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
   __shared__ int sidx[2][kDP / 64][64];           // [buffer][producer wave][compacted slot]
   __shared__ float svalT[2][kDP / 64][8][64];     // the 8 contributions of each slot
   __shared__ int nseg[2][kDP / 64];
+  __shared__ int rlo[kDescSide], roff[kDescSide + 1];   // per window row: first j, first sample
+  __shared__ int wsum[kDT / 64];
   __shared__ float raw[kD * kD * kN];
   __shared__ float scal[2];
   const int tid = threadIdx.x;
@@ -1129,7 +1132,58 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
     const int rows = q.h, cols = q.w;
     for (int t = tid; t < kHistLen; t += kDT) hist[t] = 0.f;
     const int side = 2 * radius + 1;
-    const int64_t total = (int64_t)side * side;
+    // The samples enumerated: per window row i, a j range that holds every position the
+    // test below can accept (rbin, cbin in (-1, d): |r_rot|, |c_rot| < d/2 + 0.5, widened by
+    // 1e-3 and one column each side; r, c inside the image), in row-major order -- about
+    // half the window's positions.  The per-sample test still decides, so the samples and
+    // their order are OpenCV's.  Windows over kDescSide rows enumerate every position.
+    const bool ranged = side <= kDescSide;
+    int64_t total = (int64_t)side * side;
+    if (ranged) {
+      int cnt = 0, jl = 0;
+      if (tid < side) {
+        const int i = tid - radius, r = py + i;
+        double lo = max(-radius, 1 - px), hi = min(radius, cols - 2 - px);
+        if (r <= 0 || r >= rows - 1) hi = lo - 1;
+        constexpr double E = kD * 0.5 + 0.5 + 1e-3;
+        const double ab[2][2] = {{(double)sin_t, (double)i * cos_t}, {(double)cos_t, -(double)i * sin_t}};
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {   // a j + b in (-E, E)
+          const double a = ab[k2][0], b = ab[k2][1];
+          if (fabs(a) < 1e-12) {
+            if (fabs(b) >= E) hi = lo - 1;
+          } else {
+            const double j1 = (-E - b) / a, j2 = (E - b) / a;
+            lo = fmax(lo, floor(fmin(j1, j2)) - 1);
+            hi = fmin(hi, ceil(fmax(j1, j2)) + 1);
+          }
+        }
+        if (hi >= lo) {
+          jl = (int)lo;
+          cnt = (int)hi - jl + 1;
+        }
+      }
+      // exclusive scan of the row counts over the block
+      int x = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d);
+        if ((tid & 63) >= d) x += y;
+      }
+      if ((tid & 63) == 63) wsum[tid >> 6] = x;
+      __syncthreads();
+      int before = 0, tot = 0;
+#pragma unroll
+      for (int k2 = 0; k2 < kDT / 64; ++k2) {
+        before += k2 < (tid >> 6) ? wsum[k2] : 0;
+        tot += wsum[k2];
+      }
+      roff[tid] = before + x - cnt;
+      rlo[tid] = jl;
+      if (tid == 0) roff[kDescSide] = tot;
+      total = tot;
+      __syncthreads();
+    }
     // Waves 1-3 compute chunk c (192 window samples, one per thread, OpenCV's row-major
     // order) while wave 0 adds chunk c-1 into the histogram: two buffers, one barrier per
     // chunk.  Each producer wave compacts its 64 samples into its own segment (ballot, no
@@ -1140,7 +1194,18 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
       const int buf = (int)(ch & 1);
       if (wv > 0 && ch < nch) {
         const int64_t p = ch * kDP + (tid - 64);
-        const int i = (int)(p / side) - radius, j = (int)(p % side) - radius;
+        int i, j;
+        if (ranged) {   // the row holding sample p: last t with roff[t] <= p
+          int t = 0;
+#pragma unroll
+          for (int st = kDescSide / 2; st >= 1; st >>= 1)
+            if (roff[t + st] <= p) t += st;
+          i = t - radius;
+          j = rlo[t] + (int)(p - roff[t]);
+        } else {
+          i = (int)(p / side) - radius;
+          j = (int)(p % side) - radius;
+        }
         const float c_rot = j * cos_t - i * sin_t;
         const float r_rot = j * sin_t + i * cos_t;
         float rbin = r_rot + kD / 2 - 0.5f;
