@@ -1084,7 +1084,8 @@ __device__ __forceinline__ bool inner_bin(int b) {
 __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict__ gauss, Pyr P,
                                                          const Kp* __restrict__ sorted,
                                                          const unsigned* __restrict__ nfinal,
-                                                         float* __restrict__ desc, int lane_order) {
+                                                         float* __restrict__ desc, int lane_order,
+                                                         int range_max) {
   __shared__ float hist[kHistLen];
   __shared__ int sidx[2][kDP / 64][64];           // [buffer][producer wave][compacted slot]
   __shared__ float svalT[2][kDP / 64][8][64];     // the 8 contributions of each slot
@@ -1136,8 +1137,9 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
     // test below can accept (rbin, cbin in (-1, d): |r_rot|, |c_rot| < d/2 + 0.5, widened by
     // 1e-3 and one column each side; r, c inside the image), in row-major order -- about
     // half the window's positions.  The per-sample test still decides, so the samples and
-    // their order are OpenCV's.  Windows over kDescSide rows enumerate every position.
-    const bool ranged = side <= kDescSide;
+    // their order are OpenCV's.  Windows over range_max (<= kDescSide) rows enumerate every
+    // position.
+    const bool ranged = side <= range_max;
     int64_t total = (int64_t)side * side;
     if (ranged) {
       int cnt = 0, jl = 0;
@@ -1716,8 +1718,12 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                        pass, S.dup.p, S.before.p, smax);
   hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, S.kps.p,
                      S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2, smax);
+  // SOD_SIFT_DESC_RANGE_MAX (tests): a lower window-row limit of the ranged enumeration
+  int rmax = kDescSide;
+  if (const char* e = std::getenv("SOD_SIFT_DESC_RANGE_MAX"))
+    rmax = std::max(0, std::min(kDescSide, std::atoi(e)));
   hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, P, S.sorted.p,
-                     S.cnt.p + 2, S.desc.p, W.lane_order);
+                     S.cnt.p + 2, S.desc.p, W.lane_order, rmax);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipMemcpyAsync(S.hcnt, S.cnt.p, 16, hipMemcpyDeviceToHost, st));
   return SOD_OK;

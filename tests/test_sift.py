@@ -150,6 +150,17 @@ def test_sift_rank_path(ctx, monkeypatch, sort_max):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("range_max", ["0", "41"])
+def test_sift_descriptor_full_window_path(ctx, monkeypatch, range_max):
+    """Descriptor windows above SOD_SIFT_DESC_RANGE_MAX rows (default 256) enumerate every
+    window position instead of the per-row j ranges; forcing that path (and a limit that
+    splits the keypoints between the two) gives the same bit-exact results."""
+    monkeypatch.setenv("SOD_SIFT_DESC_RANGE_MAX", range_max)
+    for name, img in _images().items():
+        _assert_same(ctx.sift_detect(img), osift.detect_and_compute(img), name + "/range" + range_max)
+
+
+@pytest.mark.gpu
 def test_sift_lane_order_paths(ctx):
     """Both histogram-add paths bit-exact against the C oracle on the reference's images
     (their orientation / descriptor bins collide inside one wave all the time, so the sums
