@@ -929,6 +929,9 @@ __device__ inline bool kp_same(const Kp& a, const Kp& b) {
 
 constexpr int kRankTile = 64;
 constexpr int kSortMax = 3072;   // keypoint lists up to this size: sort_dedup_kernel
+// images up to this size leave the rank path to a second enqueue, after the host saw a list
+// longer than kSortMax (textured 1000 x 800 images hold ~1 450 keypoints)
+constexpr int64_t kEagerRankPixels = 1200000;
 constexpr int kSortPow2 = 4096;  // its bitonic network (the next power of two)
 // (i tile, j tile) pairs, strided over the grid.  pass 0: dup[i] |= an equal (x, y, size,
 // angle) keypoint precedes i; pass 1: before[i] += kept keypoints preceding i (the sorted
@@ -1409,6 +1412,7 @@ struct SiftSlot {
   DevBuf<float> desc;          // [cap * 128]
   unsigned* hcnt = nullptr;    // pinned copy of cnt
   int cap = 1 << 16;
+  bool rank_deferred = false;   // the rank path was left out of the last enqueue
 };
 
 struct SiftWork {
@@ -1578,12 +1582,12 @@ int set_kernels(sod_ctx* ctx, SiftWork& W) {
 }
 
 int blur(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, const float* src, float* dst, int w, int h,
-         int layer, const float* prev, float* dog) {
+         int layer, const float* prev, float* dog, hipStream_t bs = nullptr) {
   const float* k = W.kern.p + (size_t)layer * kMaxTaps;
   const int r = W.radius[layer];
-  if (r >= 1 && r <= kMaxR) {
+  if (r >= 1 && r <= kMaxR) {   // (no scratch: the one path `bs` may name another stream for)
     dim3 gt((unsigned)((w + kTW - 1) / kTW), (unsigned)((h + kTH - 1) / kTH));
-    hipLaunchKernelGGL(kBlurFns[r], gt, dim3(256), 0, S.stream, src, dst, w, h, k, dog);
+    hipLaunchKernelGGL(kBlurFns[r], gt, dim3(256), 0, bs ? bs : S.stream, src, dst, w, h, k, dog);
     return SOD_OK;
   }
   dim3 g((unsigned)((w + 255) / 256), (unsigned)h);
@@ -1624,6 +1628,42 @@ void plan_pyramid(int L, int w, int h, Pyr& P, int64_t& go, int64_t& dof, int& o
     }
 }
 
+// SOD_SIFT_SORT_MAX (tests): a lower one-work-group limit, so the rank path runs too
+int sort_max() {
+  int smax = kSortMax;
+  if (const char* e = std::getenv("SOD_SIFT_SORT_MAX")) smax = std::max(-1, std::min(kSortMax, std::atoi(e)));
+  return smax;
+}
+
+// keypoint order + dedup of lists longer than smax: two O(n^2) rank passes and a scatter
+// (each exits at once when sort_dedup_kernel took the list)
+int enqueue_rank(sod_ctx* ctx, SiftSlot& S, int smax) {
+  hipStream_t st = S.stream;
+  const int cap = S.cap;
+  SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)cap * 4, st));
+  SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)cap * 4, st));
+  for (int pass = 0; pass < 2; ++pass)
+    hipLaunchKernelGGL(rank_kernel, dim3(kRankGrid), dim3(kRankTile), 0, st, S.kps.p, S.cnt.p + 1, cap,
+                       pass, S.dup.p, S.before.p, smax);
+  hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, S.kps.p,
+                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2, smax);
+  return SOD_OK;
+}
+
+// descriptors of the final list, then the counts to the host
+int enqueue_describe(sod_ctx* ctx, SiftSlot& S, int lane_order) {
+  hipStream_t st = S.stream;
+  // SOD_SIFT_DESC_RANGE_MAX (tests): a lower window-row limit of the ranged enumeration
+  int rmax = kDescSide;
+  if (const char* e = std::getenv("SOD_SIFT_DESC_RANGE_MAX"))
+    rmax = std::max(0, std::min(kDescSide, std::atoi(e)));
+  hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, S.P, S.sorted.p,
+                     S.cnt.p + 2, S.desc.p, lane_order, rmax);
+  SOD_HIP(ctx, hipGetLastError());
+  SOD_HIP(ctx, hipMemcpyAsync(S.hcnt, S.cnt.p, 16, hipMemcpyDeviceToHost, st));
+  return SOD_OK;
+}
+
 // enqueue detect + describe of the image in S.gray on S.stream (no host sync); the counts
 // land in S.hcnt.  `pyramid` false re-runs only the stages after it (list overflow).
 int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, bool pyramid, bool lone) {
@@ -1649,6 +1689,30 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
   const float thr = (float)(int)std::floor(0.5 * W.contrast / L * 255 * 1);
   hipStream_t st = S.stream;
   SOD_HIP(ctx, hipMemsetAsync(S.cnt.p, 0, 16, st));
+  ExtGrid G{};   // the octaves above the small-octave chain: one extrema launch
+  int tot = 0;
+  for (int o = 0; o < o_small; ++o) {
+    const Oct& q = P.o[o];
+    G.first[o] = tot;
+    if (q.w > 2 * kBorder && q.h > 2 * kBorder)
+      tot += ((q.w - 2 * kBorder + 255) / 256) * ((q.h - 2 * kBorder + kExtRows - 1) / kExtRows) * L;
+  }
+  G.first[o_small] = tot;
+  G.n = o_small;
+  // a lone image runs the big octaves' extrema on S.side beside the small-octave chain (both
+  // append to the candidate list atomically; the keypoint sort fixes the order) and, when it
+  // builds the pyramid, also the top two layers of every big octave: the next octave needs
+  // only layer L, so its chain starts while layers L+1, L+2 blur beside it
+  const bool split = lone && tot > 0 && o_small < nOct;
+  bool lsplit = split && pyramid && W.radius[L + 1] >= 1 && W.radius[L + 1] <= kMaxR &&
+                W.radius[L + 2] >= 1 && W.radius[L + 2] <= kMaxR;
+  int nsplit = kMaxOct;   // SOD_SIFT_LAYER_SPLIT=n (A/B): only the first n octaves split
+  if (const char* e = std::getenv("SOD_SIFT_LAYER_SPLIT")) nsplit = std::max(0, std::atoi(e));
+  if (split && !S.side) {
+    SOD_HIP(ctx, hipStreamCreateWithFlags(&S.side, hipStreamNonBlocking));
+    SOD_HIP(ctx, hipEventCreateWithFlags(&S.fork, hipEventDisableTiming));
+    SOD_HIP(ctx, hipEventCreateWithFlags(&S.join, hipEventDisableTiming));
+  }
   if (pyramid) {
     hipLaunchKernelGGL(upscale_kernel, dim3((unsigned)((bw + 255) / 256), (unsigned)bh), dim3(256), 0,
                        st, S.gray.p, w, h, S.up.p);
@@ -1663,31 +1727,21 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
         hipLaunchKernelGGL(down2_kernel, dim3((unsigned)((q.w + 255) / 256), (unsigned)q.h), dim3(256),
                            0, st, S.gauss.p + pq.g + (size_t)pq.w * pq.h * L, pq.w, g0, q.w);
       }
-      for (int i = 1; i < L + 3; ++i)
+      for (int i = 1; i < L + 3; ++i) {
+        hipStream_t bs = st;
+        if (lsplit && o < nsplit && i == L + 1) {   // layer L is done on st: fork
+          SOD_HIP(ctx, hipEventRecord(S.fork, st));
+          SOD_HIP(ctx, hipStreamWaitEvent(S.side, S.fork, 0));
+        }
+        if (lsplit && o < nsplit && i > L) bs = S.side;
         SOD_TRY(blur(ctx, W, S, g0 + plane * (i - 1), g0 + plane * i, q.w, q.h, i, g0 + plane * (i - 1),
-                     S.dogs.p + q.d + plane * (i - 1)));
+                     S.dogs.p + q.d + plane * (i - 1), bs));
+      }
     }
   }
-  {   // the octaves above the small-octave chain: one launch
-    ExtGrid G{};
-    int tot = 0;
-    for (int o = 0; o < o_small; ++o) {
-      const Oct& q = P.o[o];
-      G.first[o] = tot;
-      if (q.w > 2 * kBorder && q.h > 2 * kBorder)
-        tot += ((q.w - 2 * kBorder + 255) / 256) * ((q.h - 2 * kBorder + kExtRows - 1) / kExtRows) * L;
-    }
-    G.first[o_small] = tot;
-    G.n = o_small;
-    // both append to the candidate list (atomically; the keypoint sort fixes the order)
-    const bool split = lone && tot > 0 && o_small < nOct;
+  {
     hipStream_t xs = st;
-    if (split) {
-      if (!S.side) {
-        SOD_HIP(ctx, hipStreamCreateWithFlags(&S.side, hipStreamNonBlocking));
-        SOD_HIP(ctx, hipEventCreateWithFlags(&S.fork, hipEventDisableTiming));
-        SOD_HIP(ctx, hipEventCreateWithFlags(&S.join, hipEventDisableTiming));
-      }
+    if (split) {   // the side stream holds the top layers (lsplit) and waits for the rest
       SOD_HIP(ctx, hipEventRecord(S.fork, st));
       SOD_HIP(ctx, hipStreamWaitEvent(S.side, S.fork, 0));
       xs = S.side;
@@ -1706,27 +1760,17 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                      S.cnt.p + 3);
   hipLaunchKernelGGL(orient_kernel, dim3(kOrientGrid), dim3(kOT), 0, st, S.gauss.p, P, S.surv.p,
                      S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap, W.lane_order);
-  // SOD_SIFT_SORT_MAX (tests): a lower one-work-group limit, so the rank path runs too
-  int smax = kSortMax;
-  if (const char* e = std::getenv("SOD_SIFT_SORT_MAX")) smax = std::max(-1, std::min(kSortMax, std::atoi(e)));
+  const int smax = sort_max();
   hipLaunchKernelGGL(sort_dedup_kernel, dim3(1), dim3(1024), 0, st, S.kps.p, S.cnt.p + 1, cap,
                      S.sorted.p, S.cnt.p + 2, smax);
-  SOD_HIP(ctx, hipMemsetAsync(S.dup.p, 0, (size_t)cap * 4, st));
-  SOD_HIP(ctx, hipMemsetAsync(S.before.p, 0, (size_t)cap * 4, st));
-  for (int pass = 0; pass < 2; ++pass)
-    hipLaunchKernelGGL(rank_kernel, dim3(kRankGrid), dim3(kRankTile), 0, st, S.kps.p, S.cnt.p + 1, cap,
-                       pass, S.dup.p, S.before.p, smax);
-  hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, S.kps.p,
-                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2, smax);
-  // SOD_SIFT_DESC_RANGE_MAX (tests): a lower window-row limit of the ranged enumeration
-  int rmax = kDescSide;
-  if (const char* e = std::getenv("SOD_SIFT_DESC_RANGE_MAX"))
-    rmax = std::max(0, std::min(kDescSide, std::atoi(e)));
-  hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, P, S.sorted.p,
-                     S.cnt.p + 2, S.desc.p, W.lane_order, rmax);
-  SOD_HIP(ctx, hipGetLastError());
-  SOD_HIP(ctx, hipMemcpyAsync(S.hcnt, S.cnt.p, 16, hipMemcpyDeviceToHost, st));
-  return SOD_OK;
+  // lists longer than smax take the rank path; an image small enough that its list most
+  // likely fits leaves those launches (two memsets, three kernels that would exit at once:
+  // ~25 us of a ~660 us image) to a second enqueue after the host sees the count
+  S.rank_deferred = (int64_t)w * h <= kEagerRankPixels;
+  if (const char* e = std::getenv("SOD_SIFT_EAGER_RANK"))   // A/B and tests: 1 = always eager
+    S.rank_deferred = S.rank_deferred && std::atoi(e) == 0;
+  if (!S.rank_deferred) SOD_TRY(enqueue_rank(ctx, S, smax));
+  return enqueue_describe(ctx, S, W.lane_order);
 }
 
 // upload one image (8-bit gray, or BGR converted on the device) into S.gray
@@ -1798,6 +1842,11 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
         // grow and redo after the pyramid (the result does not depend on discovery order)
         S->cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)std::max(c0, c1));
         SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], false, m == 1));
+      }
+      if (S->rank_deferred && (int64_t)S->hcnt[1] > sort_max()) {   // the list did not fit one work-group
+        SOD_TRY(enqueue_rank(ctx, *S, sort_max()));
+        SOD_TRY(enqueue_describe(ctx, *S, W.lane_order));
+        SOD_HIP(ctx, hipStreamSynchronize(S->stream));
       }
       const int64_t cnt = S->hcnt[2];
       const int64_t at = W.off.back();
