@@ -1709,7 +1709,18 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
   int nsplit = kMaxOct;   // SOD_SIFT_LAYER_SPLIT=n (A/B): only the first n octaves split
   if (const char* e = std::getenv("SOD_SIFT_LAYER_SPLIT")) nsplit = std::max(0, std::atoi(e));
   if (split && !S.side) {
-    SOD_HIP(ctx, hipStreamCreateWithFlags(&S.side, hipStreamNonBlocking));
+    // the side stream leaves one CU out of its mask (SOD_SIFT_SIDE_MASK=0: all CUs): the
+    // small-octave chain (one 1 024-thread work-group, ~146 KB of LDS) then always finds a
+    // free CU instead of waiting for the extrema launch's work-groups to drain
+    int keep_free = 1;
+    if (const char* e = std::getenv("SOD_SIFT_SIDE_MASK")) keep_free = std::atoi(e) != 0;
+    if (keep_free && ctx->num_cus > 1) {
+      std::vector<uint32_t> mask((size_t)(ctx->num_cus + 31) / 32, 0u);
+      for (int i = 0; i < ctx->num_cus - 1; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+      SOD_HIP(ctx, hipExtStreamCreateWithCUMask(&S.side, (uint32_t)mask.size(), mask.data()));
+    } else {
+      SOD_HIP(ctx, hipStreamCreateWithFlags(&S.side, hipStreamNonBlocking));
+    }
     SOD_HIP(ctx, hipEventCreateWithFlags(&S.fork, hipEventDisableTiming));
     SOD_HIP(ctx, hipEventCreateWithFlags(&S.join, hipEventDisableTiming));
   }
@@ -1742,8 +1753,12 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
   {
     hipStream_t xs = st;
     if (split) {   // the side stream holds the top layers (lsplit) and waits for the rest
-      SOD_HIP(ctx, hipEventRecord(S.fork, st));
-      SOD_HIP(ctx, hipStreamWaitEvent(S.side, S.fork, 0));
+      // (when the last big octave split, the side stream already waits for every layer the
+      // image's stream blurs: no second event right before the small-octave chain)
+      if (!(lsplit && o_small - 1 < nsplit) || std::getenv("SOD_SIFT_FORK2")) {
+        SOD_HIP(ctx, hipEventRecord(S.fork, st));
+        SOD_HIP(ctx, hipStreamWaitEvent(S.side, S.fork, 0));
+      }
       xs = S.side;
     }
     if (tot > 0)
