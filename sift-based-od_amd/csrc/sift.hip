@@ -1413,6 +1413,12 @@ struct SiftSlot {
   unsigned* hcnt = nullptr;    // pinned copy of cnt
   int cap = 1 << 16;
   bool rank_deferred = false;   // the rank path was left out of the last enqueue
+  // a lone image writes its final keypoints / descriptors straight into the context's
+  // result arrays (no copy after the host sync); null: into `sorted` / `desc`
+  Kp* out_kp = nullptr;
+  float* out_desc = nullptr;
+  Kp* final_kp() { return out_kp ? out_kp : sorted.p; }
+  float* final_desc() { return out_desc ? out_desc : desc.p; }
 };
 
 struct SiftWork {
@@ -1646,7 +1652,7 @@ int enqueue_rank(sod_ctx* ctx, SiftSlot& S, int smax) {
     hipLaunchKernelGGL(rank_kernel, dim3(kRankGrid), dim3(kRankTile), 0, st, S.kps.p, S.cnt.p + 1, cap,
                        pass, S.dup.p, S.before.p, smax);
   hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, S.kps.p,
-                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.sorted.p, S.cnt.p + 2, smax);
+                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.final_kp(), S.cnt.p + 2, smax);
   return SOD_OK;
 }
 
@@ -1657,8 +1663,8 @@ int enqueue_describe(sod_ctx* ctx, SiftSlot& S, int lane_order) {
   int rmax = kDescSide;
   if (const char* e = std::getenv("SOD_SIFT_DESC_RANGE_MAX"))
     rmax = std::max(0, std::min(kDescSide, std::atoi(e)));
-  hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, S.P, S.sorted.p,
-                     S.cnt.p + 2, S.desc.p, lane_order, rmax);
+  hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, S.P, S.final_kp(),
+                     S.cnt.p + 2, S.final_desc(), lane_order, rmax);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipMemcpyAsync(S.hcnt, S.cnt.p, 16, hipMemcpyDeviceToHost, st));
   return SOD_OK;
@@ -1777,7 +1783,7 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                      S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap, W.lane_order);
   const int smax = sort_max();
   hipLaunchKernelGGL(sort_dedup_kernel, dim3(1), dim3(1024), 0, st, S.kps.p, S.cnt.p + 1, cap,
-                     S.sorted.p, S.cnt.p + 2, smax);
+                     S.final_kp(), S.cnt.p + 2, smax);
   // lists longer than smax take the rank path; an image small enough that its list most
   // likely fits leaves those launches (two memsets, three kernels that would exit at once:
   // ~25 us of a ~660 us image) to a second enqueue after the host sees the count
@@ -1823,6 +1829,19 @@ int grow_results(sod_ctx* ctx, SiftWork& W, int64_t need) {
   return SOD_OK;
 }
 
+// point a lone image's final lists at the result arrays (grown to hold its capacity at the
+// next offset), or back at the slot's own buffers
+int set_direct(sod_ctx* ctx, SiftWork& W, SiftSlot& S, bool on) {
+  S.out_kp = nullptr;
+  S.out_desc = nullptr;
+  if (!on) return SOD_OK;
+  const int64_t at = W.off.back();
+  SOD_TRY(grow_results(ctx, W, at + S.cap));
+  S.out_kp = W.all_kp.p + at;
+  S.out_desc = W.all_desc.p + at * 128;
+  return SOD_OK;
+}
+
 // detect + describe n images, kSlots in flight on their own streams; the results are
 // appended to W.all_kp / W.all_desc in image order (W.off = prefix counts)
 int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws, const int32_t* hs,
@@ -1837,6 +1856,8 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
   W.off.assign(1, 0);
   W.shapes.clear();
   const int K = std::min(n, kSlots);
+  bool direct = true;   // SOD_SIFT_DIRECT=0 (A/B): a lone image's results copied after the sync too
+  if (const char* e = std::getenv("SOD_SIFT_DIRECT")) direct = std::atoi(e) != 0;
   for (int i0 = 0; i0 < n; i0 += K) {
     const int m = std::min(K, n - i0);
     for (int j = 0; j < m; ++j) {
@@ -1844,6 +1865,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
       SOD_TRY(get_slot(ctx, W, j, &S));
       const int i = i0 + j;
       SOD_TRY(slot_upload(ctx, *S, imgs[i], ws[i], hs[i], chans ? chans[i] : 1));
+      SOD_TRY(set_direct(ctx, W, *S, m == 1 && direct));
       SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], true, m == 1));
     }
     for (int j = 0; j < m; ++j) {
@@ -1856,6 +1878,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
         if (attempt >= 3) return sod_fail(ctx, SOD_ENOMEM, "SIFT: candidate list did not fit after growing");
         // grow and redo after the pyramid (the result does not depend on discovery order)
         S->cap = (int)std::min<int64_t>(1 << 26, 2 * (int64_t)std::max(c0, c1));
+        SOD_TRY(set_direct(ctx, W, *S, S->out_kp != nullptr));   // room for the grown list
         SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], false, m == 1));
       }
       if (S->rank_deferred && (int64_t)S->hcnt[1] > sort_max()) {   // the list did not fit one work-group
@@ -1866,7 +1889,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
       const int64_t cnt = S->hcnt[2];
       const int64_t at = W.off.back();
       SOD_TRY(grow_results(ctx, W, at + cnt));
-      if (cnt > 0) {
+      if (cnt > 0 && !S->out_kp) {
         SOD_HIP(ctx, hipMemcpyAsync(W.all_kp.p + at, S->sorted.p, (size_t)cnt * sizeof(Kp),
                                     hipMemcpyDeviceToDevice, S->stream));
         SOD_HIP(ctx, hipMemcpyAsync(W.all_desc.p + at * 128, S->desc.p, (size_t)cnt * 512,
