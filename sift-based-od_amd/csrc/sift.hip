@@ -976,11 +976,13 @@ __global__ __launch_bounds__(kRankTile) void rank_kernel(const Kp* __restrict__ 
 
 __global__ void scatter_kernel(const Kp* __restrict__ kps, const unsigned* __restrict__ nkp, int kcap,
                                const unsigned* __restrict__ dup, const unsigned* __restrict__ before,
-                               Kp* __restrict__ sorted, unsigned* __restrict__ nfinal, int smax) {
+                               Kp* __restrict__ sorted, unsigned* __restrict__ nfinal, int smax,
+                               int* __restrict__ src) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = (int)min(*nkp, (unsigned)kcap);
   if (n <= smax || i >= n || dup[i]) return;
   sorted[before[i]] = kps[i];
+  if (src) src[before[i]] = i;
   atomicAdd(nfinal, 1u);
 }
 
@@ -1005,7 +1007,8 @@ __device__ inline bool key_less(const Kp* sk, uint64_t ka, int a, uint64_t kb, i
 __global__ __launch_bounds__(1024) void sort_dedup_kernel(const Kp* __restrict__ kps,
                                                           const unsigned* __restrict__ nkp, int kcap,
                                                           Kp* __restrict__ sorted,
-                                                          unsigned* __restrict__ nfinal, int smax) {
+                                                          unsigned* __restrict__ nfinal, int smax,
+                                                          int* __restrict__ src) {
   __shared__ Kp sk[kSortMax];
   __shared__ uint64_t k64[kSortPow2];   // the (x, y) keys, sorted with their indices
   __shared__ unsigned short ix[kSortPow2];
@@ -1060,12 +1063,25 @@ __global__ __launch_bounds__(1024) void sort_dedup_kernel(const Kp* __restrict__
       off += i < w ? wsum[i] : 0;
       tot += wsum[i];
     }
-    if (kept) sorted[off + __popcll(m & ((1ull << lane) - 1ull))] = sk[ix[p]];
+    if (kept) {
+      const int o = off + __popcll(m & ((1ull << lane) - 1ull));
+      sorted[o] = sk[ix[p]];
+      if (src) src[o] = ix[p];   // raw index (early descriptors)
+    }
     __syncthreads();
     if (tid == 0) carry_s += tot;
     __syncthreads();
   }
   if (tid == 0) *nfinal = (unsigned)carry_s;
+}
+
+// final descriptors from the ones computed early on the raw keypoint list (the sort's
+// source index per kept keypoint): one float4 per thread
+__global__ void gather_desc_kernel(const float4* __restrict__ rdesc, const int* __restrict__ src,
+                                   const unsigned* __restrict__ nfinal, float4* __restrict__ desc) {
+  const int64_t n = (int64_t)*nfinal * 32;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+    desc[t] = rdesc[(int64_t)src[t >> 5] * 32 + (t & 31)];
 }
 
 // ---- descriptors: calcSIFTDescriptor, one 256-thread block per keypoint ---------------
@@ -1088,7 +1104,7 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
                                                          const Kp* __restrict__ sorted,
                                                          const unsigned* __restrict__ nfinal,
                                                          float* __restrict__ desc, int lane_order,
-                                                         int range_max) {
+                                                         int range_max, int ncap) {
   __shared__ float hist[kHistLen];
   __shared__ int sidx[2][kDP / 64][64];           // [buffer][producer wave][compacted slot]
   __shared__ float svalT[2][kDP / 64][8][64];     // the 8 contributions of each slot
@@ -1098,7 +1114,7 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
   __shared__ float raw[kD * kD * kN];
   __shared__ float scal[2];
   const int tid = threadIdx.x;
-  const int nf = (int)*nfinal;
+  const int nf = (int)min(*nfinal, (unsigned)ncap);   // (a raw list may exceed its capacity)
 #if SOD_SIFT_WAVE_ORDER_ARCH
   const bool wave_order = lane_order != 0;
 #else
@@ -1417,6 +1433,11 @@ struct SiftSlot {
   // result arrays (no copy after the host sync); null: into `sorted` / `desc`
   Kp* out_kp = nullptr;
   float* out_desc = nullptr;
+  // a lone image computes the descriptors of the raw keypoint list on `side` while the sort
+  // runs, into `rdesc`; the sort's source indices (`src`) then gather the final ones
+  bool early_desc = false;
+  DevBuf<float> rdesc;
+  DevBuf<int> src;
   Kp* final_kp() { return out_kp ? out_kp : sorted.p; }
   float* final_desc() { return out_desc ? out_desc : desc.p; }
 };
@@ -1456,6 +1477,8 @@ static void free_slot(SiftSlot* S) {
   sod_release(S->before);
   sod_release(S->cnt);
   sod_release(S->desc);
+  sod_release(S->rdesc);
+  sod_release(S->src);
   if (S->hcnt) (void)hipHostFree(S->hcnt);
   if (S->side) (void)hipStreamSynchronize(S->side);
   if (S->fork) (void)hipEventDestroy(S->fork);
@@ -1493,7 +1516,21 @@ int get_slot(sod_ctx* ctx, SiftWork& W, int i, SiftSlot** out) {
   while ((int)W.slots.size() <= i) {
     SiftSlot* S = new SiftSlot();
     W.slots.push_back(S);
-    SOD_HIP(ctx, hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking));
+    // a CU-masked stream gets a hardware queue of its own (unmasked streams share a pool of
+    // GPU_MAX_HW_QUEUES with every other stream of the process -- the contexts' matcher and
+    // tail streams among them -- and the image's stream and its side stream on ONE queue
+    // serialise and stall on their cross-stream events: 0.65 -> 1.2-1.5 ms per image
+    // measured); the mask leaves out CU 0, the side stream's leaves out the last CU
+    // (SOD_SIFT_STREAM_MASK=0: an unmasked stream)
+    int masked = 1;
+    if (const char* e = std::getenv("SOD_SIFT_STREAM_MASK")) masked = std::atoi(e) != 0;
+    if (masked && ctx->num_cus > 2) {
+      std::vector<uint32_t> mask((size_t)(ctx->num_cus + 31) / 32, 0u);
+      for (int i = 1; i < ctx->num_cus; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+      SOD_HIP(ctx, hipExtStreamCreateWithCUMask(&S->stream, (uint32_t)mask.size(), mask.data()));
+    } else {
+      SOD_HIP(ctx, hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking));
+    }
     SOD_HIP(ctx, hipHostMalloc((void**)&S->hcnt, 16, hipHostMallocDefault));
   }
   *out = W.slots[(size_t)i];
@@ -1652,7 +1689,8 @@ int enqueue_rank(sod_ctx* ctx, SiftSlot& S, int smax) {
     hipLaunchKernelGGL(rank_kernel, dim3(kRankGrid), dim3(kRankTile), 0, st, S.kps.p, S.cnt.p + 1, cap,
                        pass, S.dup.p, S.before.p, smax);
   hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, S.kps.p,
-                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.final_kp(), S.cnt.p + 2, smax);
+                     S.cnt.p + 1, cap, S.dup.p, S.before.p, S.final_kp(), S.cnt.p + 2, smax,
+                     S.early_desc ? S.src.p : nullptr);
   return SOD_OK;
 }
 
@@ -1663,8 +1701,13 @@ int enqueue_describe(sod_ctx* ctx, SiftSlot& S, int lane_order) {
   int rmax = kDescSide;
   if (const char* e = std::getenv("SOD_SIFT_DESC_RANGE_MAX"))
     rmax = std::max(0, std::min(kDescSide, std::atoi(e)));
-  hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, S.P, S.final_kp(),
-                     S.cnt.p + 2, S.final_desc(), lane_order, rmax);
+  if (S.early_desc)
+    hipLaunchKernelGGL(gather_desc_kernel, dim3(1024), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(S.rdesc.p), S.src.p, S.cnt.p + 2,
+                       reinterpret_cast<float4*>(S.final_desc()));
+  else
+    hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, st, S.gauss.p, S.P, S.final_kp(),
+                       S.cnt.p + 2, S.final_desc(), lane_order, rmax, S.cap);
   SOD_HIP(ctx, hipGetLastError());
   SOD_HIP(ctx, hipMemcpyAsync(S.hcnt, S.cnt.p, 16, hipMemcpyDeviceToHost, st));
   return SOD_OK;
@@ -1781,9 +1824,26 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                      S.cnt.p + 3);
   hipLaunchKernelGGL(orient_kernel, dim3(kOrientGrid), dim3(kOT), 0, st, S.gauss.p, P, S.surv.p,
                      S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap, W.lane_order);
+  // lone image: descriptors of the raw list on the side stream, beside the keypoint sort
+  // (a descriptor depends on its keypoint only; the few duplicates the sort drops cost their
+  // work-groups); SOD_SIFT_EARLY_DESC=0: after the sort, of the final list
+  S.early_desc = split;
+  if (const char* e = std::getenv("SOD_SIFT_EARLY_DESC")) S.early_desc = split && std::atoi(e) != 0;
+  if (S.early_desc) {
+    SOD_TRY(sod_reserve(ctx, S.rdesc, (size_t)cap * 128));
+    SOD_TRY(sod_reserve(ctx, S.src, (size_t)cap));
+    int rmax = kDescSide;
+    if (const char* e = std::getenv("SOD_SIFT_DESC_RANGE_MAX"))
+      rmax = std::max(0, std::min(kDescSide, std::atoi(e)));
+    SOD_HIP(ctx, hipEventRecord(S.fork, st));
+    SOD_HIP(ctx, hipStreamWaitEvent(S.side, S.fork, 0));
+    hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, S.side, S.gauss.p, P, S.kps.p,
+                       S.cnt.p + 1, S.rdesc.p, W.lane_order, rmax, cap);
+    SOD_HIP(ctx, hipEventRecord(S.join, S.side));
+  }
   const int smax = sort_max();
   hipLaunchKernelGGL(sort_dedup_kernel, dim3(1), dim3(1024), 0, st, S.kps.p, S.cnt.p + 1, cap,
-                     S.final_kp(), S.cnt.p + 2, smax);
+                     S.final_kp(), S.cnt.p + 2, smax, S.early_desc ? S.src.p : nullptr);
   // lists longer than smax take the rank path; an image small enough that its list most
   // likely fits leaves those launches (two memsets, three kernels that would exit at once:
   // ~25 us of a ~660 us image) to a second enqueue after the host sees the count
@@ -1791,6 +1851,7 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
   if (const char* e = std::getenv("SOD_SIFT_EAGER_RANK"))   // A/B and tests: 1 = always eager
     S.rank_deferred = S.rank_deferred && std::atoi(e) == 0;
   if (!S.rank_deferred) SOD_TRY(enqueue_rank(ctx, S, smax));
+  if (S.early_desc) SOD_HIP(ctx, hipStreamWaitEvent(st, S.join, 0));
   return enqueue_describe(ctx, S, W.lane_order);
 }
 
