@@ -1520,10 +1520,13 @@ int get_slot(sod_ctx* ctx, SiftWork& W, int i, SiftSlot** out) {
     // GPU_MAX_HW_QUEUES with every other stream of the process -- the contexts' matcher and
     // tail streams among them -- and the image's stream and its side stream on ONE queue
     // serialise and stall on their cross-stream events: 0.65 -> 1.2-1.5 ms per image
-    // measured); the mask leaves out CU 0, the side stream's leaves out the last CU
-    // (SOD_SIFT_STREAM_MASK=0: an unmasked stream)
-    int masked = 1;
-    if (const char* e = std::getenv("SOD_SIFT_STREAM_MASK")) masked = std::atoi(e) != 0;
+    // measured); the mask leaves out CU 0, the side stream's leaves out the last CU.  Only
+    // slot 0, the one a lone image (and so the side stream) uses: a batch of 16 on four
+    // masked streams ran 7.43 ms against 6.29 unmasked (SOD_SIFT_STREAM_MASK=0: none masked,
+    // 2: all four)
+    int masked = S->stream == nullptr && W.slots.size() == 1 ? 1 : 0;
+    if (const char* e = std::getenv("SOD_SIFT_STREAM_MASK"))
+      masked = std::atoi(e) == 2 ? 1 : std::atoi(e) == 0 ? 0 : masked;
     if (masked && ctx->num_cus > 2) {
       std::vector<uint32_t> mask((size_t)(ctx->num_cus + 31) / 32, 0u);
       for (int i = 1; i < ctx->num_cus; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
