@@ -165,8 +165,14 @@ int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t
  * distance sqrtf(d^2) with ties to the lower trainIdx: idx1 = the lowest row at the float
  * d1 (the matcher's own idx1 whenever every distance is < 2048, sod_match_exact_order),
  * idx2 = the lowest other row at the float d2 (-1 with a single DB row) -- found by MFMA
- * passes over the DB after a bf16 match (sod_match_set_impl(ctx, 0)), single context. */
+ * passes over the DB after an int8 (impl 1, default) or bf16 (impl 0) match, single
+ * context.  SOD_ESTATE after sod_matches_set (no distances) or with impl 2. */
 int sod_match_knn_indices(sod_ctx* ctx, int32_t* idx1, int32_t* idx2);
+/* Make the device's trainIdx (what the Hough stage reads) OpenCV's: main.py:85 reads
+ * m.trainIdx of knnMatch, whose order is the float distance.  A no-op when
+ * sod_match_exact_order holds (always for SIFT input); otherwise idx1 is replaced by
+ * sod_match_knn_indices' idx1 on the device.  Call after sod_ratio_enqueue. */
+int sod_match_float_order(sod_ctx* ctx);
 /* 1 if every distance is provably < 2048 (sqrtf then injective on the squared
  * distances, so squared-distance ordering == OpenCV's float ordering), else 0. */
 int sod_match_exact_order(sod_ctx* ctx, int* exact);

@@ -35,7 +35,7 @@ from .affine import (AffineParameters, Calc_x, Ext_Params, Gen_A, Gen_b,  # noqa
 from .pipeline import Main  # noqa: F401
 from .postprocessing import (dfs, find_max_orientation, get_final_pose,  # noqa: F401
                              group_orientation, group_position)
-from .sharded import HostComm, RcclComm, TorchHostComm, run_sharded, shard_range  # noqa: F401
+from .sharded import FileHostComm, FileStore, HostComm, RcclComm, run_sharded, shard_range  # noqa: F401
 from .batch import run_query_batch, sift_query_batch  # noqa: F401
 from .sift import SIFT, SIFT_create, bgr_to_gray  # noqa: F401
 
@@ -45,5 +45,5 @@ __all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid
            "estimate_object_pose", "estimate_object_pose_batch", "perform_hough_transform",
            "AffineParameters", "Calc_x", "Ext_Params", "Gen_A", "Gen_b", "remove_outliers",
            "verify_bins", "Main", "dfs", "group_position", "group_orientation",
-           "find_max_orientation", "get_final_pose", "run_query_batch", "sift_query_batch", "HostComm", "RcclComm", "TorchHostComm", "run_sharded",
+           "find_max_orientation", "get_final_pose", "run_query_batch", "sift_query_batch", "HostComm", "RcclComm", "FileHostComm", "FileStore", "run_sharded",
            "shard_range", "SIFT", "SIFT_create", "bgr_to_gray"]

@@ -72,6 +72,7 @@ SIGNATURES = {
     "sod_matches_set": (C.c_int, [c_ctx, C.c_int32, c_i32p, c_u8p]),
     "sod_match_exact_order": (C.c_int, [c_ctx, C.POINTER(C.c_int)]),
     "sod_match_knn_indices": (C.c_int, [c_ctx, c_i32p, c_i32p]),
+    "sod_match_float_order": (C.c_int, [c_ctx]),
     "sod_hough_enqueue": (C.c_int, [c_ctx, C.c_int32, C.c_int32, c_i32p, C.c_int64, C.c_int64]),
     "sod_hough_allreduce_enqueue": (C.c_int, [c_ctx]),
     "sod_select_enqueue": (C.c_int, [c_ctx, C.c_int32]),
@@ -295,11 +296,16 @@ class Context:
 
     def knn_indices(self):
         """knnMatch's (m.trainIdx, n.trainIdx) per query, OpenCV's float-distance order
-        (sod_match_knn_indices; bf16 matcher only)."""
+        (sod_match_knn_indices; int8 16x16x64 or bf16 matcher)."""
         i1 = np.empty(self.nq, np.int32)
         i2 = np.empty(self.nq, np.int32)
         self._chk(self._L.sod_match_knn_indices(self._h, ptr(i1, C.c_int32), ptr(i2, C.c_int32)))
         return i1, i2
+
+    def float_order(self):
+        """The device's trainIdx becomes OpenCV's float-order one (sod_match_float_order; a
+        no-op when exact_order() holds)."""
+        self._chk(self._L.sod_match_float_order(self._h))
 
     def exact_order(self):
         v = C.c_int()

@@ -22,8 +22,7 @@ def run_query_batch(ctx, images, bins=15, ratio=0.75, vote_threshold=5, affine_t
     bin keys); otherwise the stages run image by image on query windows."""
     des = np.concatenate([np.asarray(d) for d, _, _ in images], axis=0)
     kps = [k for _, k, _ in images]
-    kp = Keypoints(np.concatenate([k.x for k in kps]), np.concatenate([k.y for k in kps]),
-                   np.concatenate([k.angle for k in kps]), np.concatenate([k.octave for k in kps]))
+    kp = Keypoints.concat(kps)
     ctx.upload_queries(des, kp)
     ctx.match()
     ctx.ratio(ratio)

@@ -685,6 +685,7 @@ int sod_match_enqueue(sod_ctx* ctx) {
   ctx->nseg = 0;                    // a new step for sod_last_stage_ms
   SOD_TRY(ctx->impl != 0 ? launch_match_i8(ctx) : launch_match(ctx));
   ctx->matched = true;
+  ctx->matches_given = false;
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
 }
@@ -863,20 +864,25 @@ static void sqrt_preimage(float d, float* lo, float* hi) {
   }
 }
 
-int sod_match_knn_indices(sod_ctx* ctx, int32_t* idx1, int32_t* idx2) {
-  SOD_TRY(set_dev(ctx));
-  if (!idx1 && !idx2) return sod_fail(ctx, SOD_EINVAL, "null outputs");
+// knnMatch's float-order indices (see sod_match_knn_indices): f1 always, f2 when want2
+static int knn_float_indices(sod_ctx* ctx, bool want2, std::vector<int32_t>& f1,
+                             std::vector<int32_t>& f2) {
   if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue + sod_ratio_enqueue first");
-  if (ctx->impl != 0)
-    return sod_fail(ctx, SOD_ESTATE, "knnMatch's indices need the bf16 matcher "
-                                     "(sod_match_set_impl(ctx, 0) before the uploads)");
+  if (ctx->matches_given)
+    return sod_fail(ctx, SOD_ESTATE, "the matches were set by sod_matches_set (no distances): "
+                                     "run sod_match_enqueue first");
+  if (ctx->impl == 2)
+    return sod_fail(ctx, SOD_ESTATE, "knnMatch's indices need the int8 16x16x64 or the bf16 "
+                                     "matcher (sod_match_set_impl(ctx, 1 or 0) before the uploads)");
   if (ctx->nranks > 1 || ctx->comm || ctx->row_offset != 0)
     return sod_fail(ctx, SOD_ESTATE, "knnMatch's indices are single-context only");
   int exact = 0;
   SOD_TRY(sod_match_exact_order(ctx, &exact));
   const size_t n = (size_t)ctx->nq, np = (size_t)sod_nq_pad(ctx);
   std::vector<float> d1(n), d2(n), lo(np, 1.0f), hi(np, 0.0f);
-  std::vector<int32_t> i1(n), ex(np, -1), f1(np), f2(np);
+  std::vector<int32_t> i1(n), ex(np, -1);
+  f1.assign(np, 0);
+  f2.assign(np, 0x7f7f7f7f);
   SOD_TRY(download(ctx, i1.data(), ctx->idx1.p, n));
   SOD_TRY(download(ctx, d1.data(), ctx->d1.p, n));
   SOD_TRY(download(ctx, d2.data(), ctx->d2.p, n));
@@ -890,7 +896,9 @@ int sod_match_knn_indices(sod_ctx* ctx, int32_t* idx1, int32_t* idx2) {
     if (rc == SOD_OK) rc = upload(ctx, dhi, hi.data(), np);
     if (rc == SOD_OK) rc = upload(ctx, dex, ex.data(), np);
     if (rc == SOD_OK) rc = sod_reserve(ctx, dfound, np);
-    if (rc == SOD_OK) rc = launch_find_rows(ctx, dlo.p, dhi.p, dex.p, dfound.p);
+    if (rc == SOD_OK)
+      rc = ctx->impl == 1 ? launch_find_rows_i8(ctx, dlo.p, dhi.p, dex.p, dfound.p)
+                          : launch_find_rows(ctx, dlo.p, dhi.p, dex.p, dfound.p);
     if (rc == SOD_OK) rc = download(ctx, out.data(), dfound.p, np);
     if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
       rc = sod_fail(ctx, SOD_EHIP, "knn index pass failed");
@@ -906,7 +914,7 @@ int sod_match_knn_indices(sod_ctx* ctx, int32_t* idx1, int32_t* idx2) {
       if (f1[q] == 0x7f7f7f7f) f1[q] = i1[q];   // unreachable: the best row is at d1
   }
   // the second: the lowest row other than that one at the float d2
-  if (rc == SOD_OK && idx2) {
+  if (rc == SOD_OK && want2) {
     for (size_t q = 0; q < n; ++q) ex[q] = f1[q];
     pass(d2, f2);
   }
@@ -915,10 +923,32 @@ int sod_match_knn_indices(sod_ctx* ctx, int32_t* idx1, int32_t* idx2) {
   sod_release(dhi);
   sod_release(dex);
   sod_release(dfound);
-  SOD_TRY(rc);
+  return rc;
+}
+
+int sod_match_knn_indices(sod_ctx* ctx, int32_t* idx1, int32_t* idx2) {
+  SOD_TRY(set_dev(ctx));
+  if (!idx1 && !idx2) return sod_fail(ctx, SOD_EINVAL, "null outputs");
+  std::vector<int32_t> f1, f2;
+  SOD_TRY(knn_float_indices(ctx, idx2 != nullptr, f1, f2));
+  const size_t n = (size_t)ctx->nq;
   if (idx1) std::memcpy(idx1, f1.data(), n * 4);
   if (idx2)
     for (size_t q = 0; q < n; ++q) idx2[q] = f2[q] == 0x7f7f7f7f ? -1 : f2[q];   // single DB row
+  return SOD_OK;
+}
+
+int sod_match_float_order(sod_ctx* ctx) {
+  SOD_TRY(set_dev(ctx));
+  int exact = 0;
+  if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue + sod_ratio_enqueue first");
+  SOD_TRY(sod_match_exact_order(ctx, &exact));
+  if (exact) return SOD_OK;   // the matcher's idx1 already is OpenCV's
+  std::vector<int32_t> f1, f2;
+  SOD_TRY(knn_float_indices(ctx, false, f1, f2));
+  SOD_TRY(upload(ctx, ctx->idx1, f1.data(), (size_t)ctx->nq));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
 }
 
@@ -939,6 +969,7 @@ int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t
   ctx->ratio_fused_valid = false;
   ctx->nseg = 0;
   ctx->matched = ctx->ratio_done = true;
+  ctx->matches_given = true;
   ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
 }

@@ -1131,7 +1131,101 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
 
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Row-finding pass for the BFMatcher.knnMatch drop-in on the int8 layout (the counterpart
+// of match.hip's match_kernel<true>): per query the LOWEST row other than excl[q] whose
+// exact squared distance lies in [flo[q], fhi[q]] (the integers whose sqrtf is one float
+// distance).  distance^2 = ||q'||^2 - y with y = 2 (q'.d' + c) + p exactly, so the test is
+// y in [||q'||^2 - fhi, ||q'||^2 - flo] -- integer compares.  A wave keeps kFindQT query tiles
+// in VGPRs and walks its subtiles of the work-group's DB chunk in increasing order (A
+// fragments and the c / parity words straight from global: an auxiliary pass, not the hot
+// loop); the lowest hit per lane is min-merged over the lane groups and atomicMin-merged over
+// waves and chunks into found[q] (0x7f7f7f7f = none, preset by the launcher).
+constexpr int kFindQT = 4;
+constexpr int kFindWaves = 4;
+__global__ __launch_bounds__(kFindWaves * 64) void find_rows_i8_kernel(
+    const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
+    const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int split,
+    int64_t sub_per_split, int row_offset, const float* __restrict__ flo,
+    const float* __restrict__ fhi, const int* __restrict__ excl, int* __restrict__ found) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sp = blockIdx.x % split, qb = blockIdx.x / split;
+  const int qt0 = qb * kFindQT;
+  const int64_t npad = nsub * kSubRows;
+  i32x4 bq[kFindQT][2];
+  int ylo[kFindQT], yhi[kFindQT], ex[kFindQT], id[kFindQT];
+#pragma unroll
+  for (int t = 0; t < kFindQT; ++t) {
+    const int qt = qt0 + t;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      bq[t][k] = qt < nqt ? *reinterpret_cast<const i32x4*>(qpack + ((int64_t)qt * 2 + k) * 1024 + lane * 16)
+                          : i32x4{0, 0, 0, 0};
+    const int64_t q = (int64_t)qt * 16 + (lane & 15);
+    ylo[t] = 1;   // empty
+    yhi[t] = 0;
+    ex[t] = -1;
+    id[t] = 0x7fffffff;
+    if (qt < nqt && flo[q] <= fhi[q]) {   // integers < 2^24: exact
+      ylo[t] = qn[q] - (int)fhi[q];
+      yhi[t] = qn[q] - (int)flo[q];
+      ex[t] = excl[q];
+    }
+  }
+  const int64_t s_lo = (int64_t)sp * sub_per_split;
+  const int64_t s_hi = min(nsub, s_lo + sub_per_split);
+  for (int64_t u = s_lo + wave; u < s_hi; u += kFindWaves) {
+    const uint8_t* a = dbpack + u * kSub + lane * 16;
+    const i32x4 a0 = *reinterpret_cast<const i32x4*>(a);
+    const i32x4 a1 = *reinterpret_cast<const i32x4*>(a + 1024);
+    const int64_t r0 = u * kSubRows + (lane >> 4) * 4;   // the lane's 4 rows
+    const i32x4 c = *reinterpret_cast<const i32x4*>(dn + r0);
+    const i32x4 p = *reinterpret_cast<const i32x4*>(dn + npad + r0);
+    const int rowb = row_offset + (int)r0;
+#pragma unroll
+    for (int t = 0; t < kFindQT; ++t) {
+      i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq[t][0], c, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq[t][1], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 3; r >= 0; --r) {   // the lowest matching row of the four wins
+        const int y = 2 * acc[r] + p[r];
+        const bool in = y >= ylo[t] && y <= yhi[t] && rowb + r != ex[t];
+        id[t] = (in && rowb + r < id[t]) ? rowb + r : id[t];
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < kFindQT; ++t) {
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) id[t] = min(id[t], __shfl_xor(id[t], m));
+    const int qt = qt0 + t;
+    if (lane < 16 && qt < nqt && id[t] != 0x7fffffff)
+      atomicMin(&found[(int64_t)qt * 16 + lane], id[t]);
+  }
+}
+
 }  // namespace
+
+// per query the lowest row other than excl[q] whose exact squared distance lies in
+// [flo[q], fhi[q]] over the int8-packed DB (16x16x64 layout; arrays [nq_pad] on the device);
+// found[q] = 0x7f7f7f7f where there is none
+int launch_find_rows_i8(sod_ctx* ctx, const float* flo, const float* fhi, const int32_t* excl,
+                        int32_t* found) {
+  if (ctx->impl != 1) return sod_fail(ctx, SOD_ESTATE, "find_rows_i8: int8 16x16x64 layout only");
+  const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
+  const int64_t qblocks = cdiv(ctx->nqt, kFindQT);
+  // about 8 work-groups per CU in total, chunks of whole subtiles
+  int64_t split = std::max<int64_t>(1, 8LL * ctx->num_cus / qblocks);
+  split = std::min<int64_t>(split, cdiv(ctx->nsub, kFindWaves));
+  const int64_t sub_per_split = cdiv(ctx->nsub, split);
+  split = cdiv(ctx->nsub, sub_per_split);
+  SOD_HIP(ctx, hipMemsetAsync(found, 0x7f, (size_t)nq_pad * 4, ctx->stream));
+  hipLaunchKernelGGL(find_rows_i8_kernel, dim3((unsigned)(qblocks * split)), dim3(kFindWaves * 64),
+                     0, ctx->stream, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
+                     ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt,
+                     (int)split, sub_per_split, (int)ctx->row_offset, flo, fhi, excl, found);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
 
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db) {
   const bool wide = ctx->impl == 2;

@@ -94,6 +94,7 @@ struct sod_ctx {
   DevBuf<uint8_t> good;         // [nq]
   DevBuf<uint32_t> flags;       // [0]=invalid descriptor count, [1]=max dn bits, [2]=max qn bits
   bool matched = false, ratio_done = false;
+  bool matches_given = false;   // the matches came from sod_matches_set (no distances)
   // sod_pipeline_enqueue: the ratio its final merge applies in the same kernel (-1 = none),
   // and the ratio that merge applied (valid only while ratio_fused_valid: the last merge
   // fused it), which sod_ratio_enqueue then skips
@@ -288,6 +289,8 @@ int sod_stage_mark(sod_ctx* ctx, int stage, bool end);
 int launch_match(sod_ctx* ctx);
 int launch_find_rows(sod_ctx* ctx, const float* flo, const float* fhi, const int32_t* excl,
                      int32_t* found);
+int launch_find_rows_i8(sod_ctx* ctx, const float* flo, const float* fhi, const int32_t* excl,
+                        int32_t* found);
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db);
 int launch_match_i8(sod_ctx* ctx);
 // matcher-input writers call these around their writes; the match launchers around the

@@ -65,9 +65,14 @@ class BFMatcher:
     float distance with ties to the lower trainIdx, so ``n.trainIdx`` is the lowest row other
     than ``m``'s at the second float distance -- and, for inputs whose distances reach 2048
     (not SIFT: its norms are ~512), where two squared distances can share a float,
-    ``m.trainIdx`` is the lowest row at the first.  Those indices come from MFMA passes over
-    the DB (``sod_match_knn_indices``, bf16 matcher), so this object runs on a bf16 context
-    of its own unless one is given."""
+    ``m.trainIdx`` is the lowest row at the first.  Those indices come from MFMA row-finding
+    passes over the resident DB (``sod_match_knn_indices``) after the int8 matcher.
+
+    The train set stays on the device between calls: ``knnMatch(q, train)`` re-uploads
+    only when ``train`` is not the array object of the previous call or is writeable (its
+    content could have changed in place; a content hash of a 1M-row DB costs more than the
+    upload), and OpenCV's own resident-collection API -- ``add([des])`` + ``train()``, then
+    ``knnMatch(q, k=2)`` -- uploads once."""
 
     def __init__(self, normType=NORM_L2, crossCheck=False, ctx=None):
         if normType != NORM_L2:
@@ -75,32 +80,86 @@ class BFMatcher:
         if crossCheck:
             raise NotImplementedError("crossCheck is not used by the reference")
         self._ctx = ctx
+        self._resident = None      # the array object whose rows are on the device
+        self._collection = []      # add() / train(): OpenCV's train descriptor collection
+        self._trained = None
+        self.uploads = 0           # descriptor uploads so far (a residency check)
 
     def _context(self):
         if self._ctx is None:
             self._ctx = _lib.Context(0)
-            self._ctx.set_impl("bf16")
         return self._ctx
 
-    def knnMatch(self, queryDescriptors, trainDescriptors, k=2):
+    # ---- OpenCV DescriptorMatcher collection API ----------------------------------------
+    def add(self, descriptors):
+        """Append train descriptor sets (a list of [n_i, 128] arrays), as OpenCV's ``add``;
+        their rows are numbered consecutively (``imgIdx`` is the set)."""
+        self._collection.extend(np.asarray(d) for d in descriptors)
+        self._trained = None
+
+    def getTrainDescriptors(self):
+        return list(self._collection)
+
+    def clear(self):
+        self._collection = []
+        self._trained = None
+        self._resident = None
+
+    def empty(self):
+        return len(self._collection) == 0
+
+    def train(self):
+        """Concatenate the collection and upload it once (later knnMatch calls without a
+        train argument reuse it)."""
+        if not self._collection:
+            self._trained = np.zeros((0, 128), np.uint8)
+        else:
+            self._trained = np.concatenate(self._collection, axis=0)
+            self._trained.flags.writeable = False   # ours: never changes once uploaded
+        self._starts = np.cumsum([0] + [len(d) for d in self._collection])
+
+    def _upload(self, d, ctx):
+        if self._resident is d and not d.flags.writeable:
+            return
+        ctx.upload_db(d)
+        self._resident = d
+        self.uploads += 1
+
+    def knnMatch(self, queryDescriptors, trainDescriptors=None, k=2):
         if k not in (1, 2):
             raise NotImplementedError("k must be 1 or 2 (main.py uses k=2)")
+        img_of = None
+        if trainDescriptors is None:   # the collection (OpenCV: knnMatch(query, k))
+            if self._trained is None:
+                self.train()
+            d = self._trained
+            if len(self._collection) > 1:
+                starts = self._starts
+                img_of = lambda t: int(np.searchsorted(starts, t, side="right") - 1)  # noqa: E731
+        elif isinstance(trainDescriptors, (int, np.integer)):   # knnMatch(query, k) form
+            return self.knnMatch(queryDescriptors, None, int(trainDescriptors))
+        else:
+            d = trainDescriptors if isinstance(trainDescriptors, np.ndarray) else \
+                np.asarray(trainDescriptors)
         q = np.asarray(queryDescriptors)
-        d = np.asarray(trainDescriptors)
         ntrain = d.shape[0]
         if ntrain == 0:   # OpenCV: no neighbours for any query
             return [[] for _ in range(q.shape[0])]
         if q.shape[0] == 0:
             return []
         ctx = self._context()
-        ctx.set_impl("bf16")
-        ctx.upload_db(d)
+        self._upload(d, ctx)
         ctx.upload_queries(q)
         ctx.match()
         ctx.ratio(0.75)
         idx1, d1, d2, _ = ctx.match_result()
         idx1, idx2 = ctx.knn_indices()
+
+        def dm(i, t, dist):
+            if img_of is None:
+                return DMatch(i, int(t), 0, float(dist))
+            im = img_of(t)
+            return DMatch(i, int(t) - int(self._starts[im]), im, float(dist))
         if k == 1 or ntrain == 1:
-            return [[DMatch(i, int(idx1[i]), 0, float(d1[i]))] for i in range(len(idx1))]
-        return [[DMatch(i, int(idx1[i]), 0, float(d1[i])),
-                 DMatch(i, int(idx2[i]), 0, float(d2[i]))] for i in range(len(idx1))]
+            return [[dm(i, idx1[i], d1[i])] for i in range(len(idx1))]
+        return [[dm(i, idx1[i], d1[i]), dm(i, idx2[i], d2[i])] for i in range(len(idx1))]

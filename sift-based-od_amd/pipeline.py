@@ -57,6 +57,7 @@ class Main:
         self._sel_token = 0            # device selections made (PoseBin.bind_device)
         self._valid_sel = None         # (token, valid_result) of get_valid_bins' selection
         self._tuple_ctx = None         # context of the tuple-given Hough path (reused)
+        self._exact = None             # squared-distance order == OpenCV's (per upload)
         self.affine_path = None        # how the last apply_affine_parameters ran
 
     # ---------------------------------------------------------------- inputs
@@ -71,6 +72,7 @@ class Main:
         self.db = db
         self.des = db.des
         db.upload(self.ctx)
+        self._exact = None
         self.kp = _LazyKeypoints(self, "db")
 
     def get_query_features(self, des_query, kp_query, image_shape, database=None):
@@ -80,7 +82,7 @@ class Main:
         if database is not None:
             self.set_database(database)
         if not isinstance(kp_query, Keypoints):
-            kp_query = Keypoints.from_cv(kp_query)
+            kp_query = Keypoints.from_cv(kp_query)   # keeps the caller's objects (main.py:43)
         self._qkp = kp_query
         self.des_query = np.asarray(des_query)
         self.rgb_query = _Shape(image_shape)
@@ -101,7 +103,7 @@ class Main:
         if len(r["x"]) == 0:
             raise ValueError("the query image has no SIFT keypoints")
         self.ctx.sift_to_queries()
-        self._qkp = Keypoints(r["x"], r["y"], r["angle"], r["octave"])
+        self._qkp = Keypoints(r["x"], r["y"], r["angle"], r["octave"], r["size"], r["response"])
         self.des_query = r["descriptors"]
         self.sift_query = r
         self.rgb_query = _Shape(img.shape if img.ndim == 3 else img.shape + (3,))
@@ -109,7 +111,14 @@ class Main:
         self.kp_query = _LazyKeypoints(self, "query")
         self._reset_after_match()
 
+    def _exact_order(self):
+        """sod_match_exact_order of the current uploads (one device read per upload)."""
+        if self._exact is None:
+            self._exact = self.ctx.exact_order()
+        return self._exact
+
     def _reset_after_match(self):
+        self._exact = None
         self._matching = None
         self._match = None
         self._table = None
@@ -118,9 +127,14 @@ class Main:
 
     # ---------------------------------------------------------------- stages
     def run_matcher(self, ratio=0.75):
-        """``main.py:68-87``: knnMatch(k=2) + ratio test, on the device."""
+        """``main.py:68-87``: knnMatch(k=2) + ratio test, on the device.  ``m.trainIdx`` is
+        OpenCV's: ordered by the float distance, ties to the lower row.  The matcher orders by
+        the exact squared distance, which is the same order whenever every distance is below
+        2048 (always for SIFT descriptors, norm ~512); otherwise ``float_order`` re-derives
+        the index from the float distance on the device (sod_match_float_order)."""
         self.ctx.match()
         self.ctx.ratio(ratio)
+        self.ctx.float_order()
         idx1, d1, d2, good = self.ctx.match_result()
         self._match = (idx1, good)
         self._matching = None
@@ -272,9 +286,21 @@ class Main:
             post_process=True):
         """The whole path on one stream, results left on the device; returns a dict of
         arrays (matches, valid bins, members, means, affine survivors/params, and the
-        post-processing clusters / final poses)."""
-        self.ctx.pipeline(self.rgb_query.shape, bins, ratio, vote_threshold, affine_threshold,
-                          POS_FACTOR * 4.0, POS_FACTOR * 4.0, run_affine)
+        post-processing clusters / final poses).  When OpenCV's float order is not provably
+        the squared-distance order (distances reaching 2048: not SIFT input), the stages are
+        enqueued one by one with the float-order trainIdx in between (``run_matcher``)."""
+        if self._exact_order():
+            self.ctx.pipeline(self.rgb_query.shape, bins, ratio, vote_threshold,
+                              affine_threshold, POS_FACTOR * 4.0, POS_FACTOR * 4.0, run_affine)
+        else:
+            self.ctx.match()
+            self.ctx.ratio(ratio)
+            self.ctx.float_order()
+            self.ctx.hough(self.rgb_query.shape, bins)
+            self.ctx.select(vote_threshold)
+            if run_affine:
+                self.ctx.affine(self.image_query_size, POS_FACTOR * 4.0, POS_FACTOR * 4.0,
+                                affine_threshold)
         idx1, d1, d2, good = self.ctx.match_result()
         out = {"idx1": idx1, "d1": d1, "d2": d2, "good": good, "valid": self.ctx.valid_result()}
         if run_affine:
@@ -338,6 +364,6 @@ class _LazyKeypoints:
         i = int(i)
         k = self._cache.get(i)
         if k is None:
-            k = keypoints_from_arrays(self._src(), i)
+            k = keypoints_from_arrays(self._src(), i)   # the caller's own object when given
             self._cache[i] = k
         return k

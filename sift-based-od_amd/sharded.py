@@ -20,8 +20,8 @@ Two communicators carry the two exchanges:
   the production path.
 * :class:`HostComm` -- the same exchanges staged through host memory over any object
   providing ``allgather``/``allreduce`` of numpy arrays (``FileHostComm`` over the
-  stdlib :class:`FileStore` of one node; ``TorchHostComm`` wraps a torch.distributed gloo
-  group for the CPU tests); used where RCCL is unavailable.
+  stdlib :class:`FileStore` of one node; the CPU tests wrap a torch.distributed gloo group,
+  ``tests/torch_comm.py``); used where RCCL is unavailable.
 
 The bootstrap (RCCL unique id, barriers, max over ranks) needs nothing but the standard
 library: :class:`FileStore`.
@@ -86,20 +86,42 @@ class FileStore:
     unique-id broadcast, barriers, all-gathers of small byte strings.  Keys are files
     written to a temporary name and renamed into place (atomic), readers poll.
 
-    ``path`` defaults to ``$TMPDIR/sod_store_<MASTER_PORT>_<parent pid>``: the ranks a
-    launcher (torchrun's agent) started share their parent, so a run never meets an older
-    run's files.  ``close()`` removes the directory once every rank is done with it."""
+    ``path``: ``$SOD_STORE_DIR`` when set, else ``$TMPDIR/sod_store_<run id>`` with the run
+    id of the launcher (``TORCHELASTIC_RUN_ID``, which torchrun gives every rank of one
+    job), else ``<MASTER_PORT>_<parent pid>`` (the ranks a launcher started share their
+    parent; ranks started by mpirun / srun / by hand have none in common and must set
+    ``SOD_STORE_DIR``).  Every rank registers at construction and waits up to
+    ``join_timeout`` seconds for the others, so ranks that landed in different directories
+    fail at once with the path they used, not after ``timeout``.  ``close()`` removes the
+    directory once every rank is done with it."""
 
-    def __init__(self, world, rank, path=None, timeout=600.0):
+    def __init__(self, world, rank, path=None, timeout=600.0, join_timeout=60.0):
         import os
         import tempfile
         self.world, self.rank, self.timeout = world, rank, timeout
         if path is None:
-            path = os.path.join(tempfile.gettempdir(), "sod_store_%s_%d" % (
-                os.environ.get("MASTER_PORT", "0"), os.getppid()))
+            path = os.environ.get("SOD_STORE_DIR")
+        if path is None:
+            run = os.environ.get("TORCHELASTIC_RUN_ID")
+            if not run or run == "none":
+                run = "%s_%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+            path = os.path.join(tempfile.gettempdir(), "sod_store_%s" % run)
         self.path = path
         os.makedirs(path, exist_ok=True)
         self._seq = 0
+        if world > 1:
+            self.set("join_%d" % rank, b"")
+            t, self.timeout = self.timeout, join_timeout
+            try:
+                for r in range(world):
+                    self.get("join_%d" % r)
+            except TimeoutError:
+                raise TimeoutError(
+                    "FileStore: rank %d of %d found no rank %d in %s within %.0f s -- ranks not "
+                    "started by one launcher must share a directory: set SOD_STORE_DIR"
+                    % (rank, world, r, path, join_timeout)) from None
+            finally:
+                self.timeout = t
 
     def _file(self, key):
         import os
@@ -182,29 +204,6 @@ class FileHostComm(HostComm):
             return out
 
         super().__init__(store.world, store.rank, allgather, allreduce)
-
-
-class TorchHostComm(HostComm):
-    """HostComm over a torch.distributed process group (gloo): a test adapter."""
-
-    def __init__(self, group=None):
-        import torch
-        import torch.distributed as dist
-        self._t, self._d, self._g = torch, dist, group
-
-        def allgather(a):
-            t = torch.from_numpy(np.ascontiguousarray(a))
-            out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
-            dist.all_gather(out, t, group=group)
-            return [o.numpy() for o in out]
-
-        def allreduce(a, op):
-            t = torch.from_numpy(np.ascontiguousarray(a))
-            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MIN,
-                            group=group)
-            return t.numpy()
-
-        super().__init__(dist.get_world_size(group), dist.get_rank(group), allgather, allreduce)
 
 
 def run_sharded(ctx, comm, shard, query_shape, bins, ratio=0.75, vote_threshold=5,

@@ -84,6 +84,7 @@ def make_kp(temp_kp):
 
 
 def keypoints_from_arrays(kp, i):
-    """KeyPoint object for row ``i`` of a :class:`~.database.Keypoints` SoA."""
-    return new_keypoint(float(kp.x[i]), float(kp.y[i]), 0.0, float(kp.angle[i]), 0.0,
-                        int(kp.octave[i]))
+    """KeyPoint object for row ``i`` of a :class:`~.database.Keypoints` SoA: the caller's own
+    object when the table was built from objects, else a new one carrying every field
+    (pt, size, angle, response, octave, class_id) as ``make_kp`` builds it."""
+    return kp.keypoint(int(i))

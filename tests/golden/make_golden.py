@@ -516,8 +516,119 @@ def main():
          good=orc.ratio_test(e1, e2))
 
 
+KP_FIELDS = ("x", "y", "size", "angle", "response", "octave", "class_id")
+
+
+def kp_field_rows(kps):
+    """[n, 7] f64 rows (pt x, pt y, size, angle, response, octave, class_id) of KeyPoints."""
+    return np.array([[k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave, k.class_id]
+                     for k in kps], np.float64).reshape(-1, 7)
+
+
+def main_keypoints():
+    """The reference's own KeyPoint objects through main.py's stages (the
+    drop-in must hand back the reference's objects): for the c1_b15 and planted_b15 inputs
+    plus seeded size / response / class_id fields, the DB goes through the reference's
+    record format (``make_temp_kp`` tuples per image, main.py:53-66's flattening, ``make_kp``)
+    and ``Main.run_matcher`` runs with a stand-in ``cv2.BFMatcher`` whose knnMatch is the
+    oracle's exact k=2 (OpenCV is absent); ``matching_keypoints`` and the valid / surviving
+    bins' ``keypoint_pairs`` are stored field by field (written to kpfields_<case>.npz)."""
+    import sod_pkg
+    sod_pkg.load()
+    from oracle import oracle as orc
+    ref_main, _ = import_reference()
+    import SiftHelperFunctions as ref_sh  # noqa: E402
+
+    class _DMatch:
+        def __init__(self, q, t, d):
+            self.queryIdx, self.trainIdx, self.imgIdx, self.distance = q, t, 0, d
+
+    class _BFMatcher:
+        def knnMatch(self, q, d, k=2):
+            i1, e1, e2, i2 = orc.knn2_match(np.asarray(q), np.asarray(d), with_idx2=True)
+            return [(_DMatch(j, int(i1[j]), float(e1[j])), _DMatch(j, int(i2[j]), float(e2[j])))
+                    for j in range(len(i1))]
+    sys.modules["cv2"].BFMatcher = _BFMatcher
+
+    for name, seed in (("c1_b15", 601), ("planted_b15", 602)):
+        g = dict(np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False))
+        rng = np.random.default_rng(seed)
+        nd, nq = len(g["db_x"]), len(g["q_x"])
+        extra = {}
+        for pre, n in (("db_", nd), ("q_", nq)):
+            extra[pre + "size"] = rng.uniform(1.5, 40.0, n).astype(np.float32)
+            extra[pre + "response"] = rng.uniform(0.005, 0.12, n).astype(np.float32)
+            extra[pre + "class_id"] = rng.integers(-1, 6, n).astype(np.int32)
+
+        def objs(pre, n):
+            return [KeyPoint(x=float(g[pre + "x"][i]), y=float(g[pre + "y"][i]),
+                             _size=float(extra[pre + "size"][i]), _angle=float(g[pre + "angle"][i]),
+                             _response=float(extra[pre + "response"][i]),
+                             _octave=int(g[pre + "octave"][i]),
+                             _class_id=int(extra[pre + "class_id"][i])) for i in range(n)]
+        dbk, qk = objs("db_", nd), objs("q_", nq)
+        # the pickle's per-image records (GenerateDatabaseInfo.py:35) ...
+        records = []
+        for im in range(len(g["centroid"])):
+            rows = np.nonzero(g["db_img"] == im)[0]
+            records.append([ref_sh.make_temp_kp([dbk[r] for r in rows]), g["db_des"][rows],
+                            (int(g["size"][im][0]), int(g["size"][im][1])),
+                            (float(g["centroid"][im][0]), float(g["centroid"][im][1]))])
+        # ... flattened in record order (main.py:53-66), KeyPoints rebuilt by make_kp
+        M = ref_main.Main()
+        temp_kp, sizes, cents, des = [], [], [], []
+        for rec in records:
+            temp_kp.extend(rec[0])
+            sizes.extend([rec[2]] * len(rec[0]))
+            cents.extend([rec[3]] * len(rec[0]))
+            des.append(rec[1])
+        M.kp = ref_sh.make_kp(temp_kp)
+        M.des = np.concatenate(des, axis=0)
+        M.img_size_list, M.img_centroid_list = sizes, cents
+        M.kp_query, M.des_query = qk, g["q_des"]
+        shape = tuple(int(v) for v in g["shape"])
+        M.rgb_query = types.SimpleNamespace(shape=shape)
+        M.image_query_size = (shape[1], shape[0])
+        M.run_matcher()
+        mk = M.matching_keypoints
+        qpos = {id(k): i for i, k in enumerate(qk)}
+        out = dict(extra)
+        out["mk_q"] = np.array([qpos[id(t[1])] for t in mk], np.int32)
+        out["mk_model"] = kp_field_rows([t[0] for t in mk])
+        out["mk_query"] = kp_field_rows([t[1] for t in mk])
+        out["mk_img_size"] = np.array([t[2] for t in mk], np.int32).reshape(-1, 2)
+        out["mk_centroid"] = np.array([t[3] for t in mk], np.float64).reshape(-1, 2)
+        assert np.array_equal(out["mk_q"], np.nonzero(g["good"])[0])
+        M.apply_hough_transform(int(g["bins"]))
+        M.get_valid_bins(5)
+        off, pm, pq = [0], [], []
+        for b in M.valid_bins:
+            pm.extend(p[0] for p in b.keypoint_pairs)
+            pq.extend(p[1] for p in b.keypoint_pairs)
+            off.append(len(pm))
+        out["valid_off"] = np.array(off, np.int64)
+        out["valid_pairs_model"] = kp_field_rows(pm)
+        out["valid_pairs_query"] = kp_field_rows(pq)
+        assert np.array_equal(out["valid_off"], g["valid_off"])
+        M.apply_affine_parameters(4)
+        off, pm, pq = [0], [], []
+        for b in M.valid_bins:
+            pm.extend(p[0] for p in b.keypoint_pairs)
+            pq.extend(p[1] for p in b.keypoint_pairs)
+            off.append(len(pm))
+        out["surv_off"] = np.array(off, np.int64)
+        out["surv_pairs_model"] = kp_field_rows(pm)
+        out["surv_pairs_query"] = kp_field_rows(pq)
+        assert np.array_equal(out["surv_off"], g["surv_off"])
+        print(name, "matching_keypoints", len(mk), "valid pairs", len(out["valid_pairs_model"]),
+              "surviving pairs", len(out["surv_pairs_model"]))
+        save("kpfields_" + name, **out)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["near_edge"]:
         main_near_edge()
+    elif sys.argv[1:] == ["keypoints"]:
+        main_keypoints()
     else:
         main()

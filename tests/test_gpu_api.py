@@ -120,6 +120,58 @@ def test_main_stages_match_golden():
     np.testing.assert_allclose(got.reshape(-1, 6), g["final_pose"], rtol=1e-12, atol=1e-9)
 
 
+def _kf_rows(kps):
+    return np.array([[k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave, k.class_id]
+                     for k in kps], np.float64).reshape(-1, 7)
+
+
+@pytest.mark.parametrize("name", ["c1_b15", "planted_b15"])
+def test_main_keypoint_fields(name):
+    """Main hands back the reference's KeyPoint objects (SiftHelperFunctions.py:42-49,
+    main.py:43,65,85-86): the DB set from the reference's pickle records and the query's
+    KeyPoint objects given, matching_keypoints and every valid / surviving bin's
+    keypoint_pairs equal the reference's own Main output (kpfields_* goldens) field by field
+    -- pt, size, angle, response, octave, class_id -- and the query keypoints are the
+    caller's very objects, as in the reference."""
+    g, kf = golden(name), golden("kpfields_" + name)
+    mk_obj = lambda pre, src, i: sod.KeyPoint(  # noqa: E731
+        float(g[pre + "x"][i]), float(g[pre + "y"][i]), float(src[pre + "size"][i]),
+        float(g[pre + "angle"][i]), float(src[pre + "response"][i]), int(g[pre + "octave"][i]),
+        int(src[pre + "class_id"][i]))
+    records = []
+    for im in range(len(g["centroid"])):
+        rows = np.nonzero(g["db_img"] == im)[0]
+        records.append([sod.make_temp_kp([mk_obj("db_", kf, r) for r in rows]), g["db_des"][rows],
+                        (int(g["size"][im][0]), int(g["size"][im][1])),
+                        (float(g["centroid"][im][0]), float(g["centroid"][im][1])), "img"])
+    qk = [mk_obj("q_", kf, i) for i in range(len(g["q_x"]))]
+    m = sod.Main()
+    m.set_database(records)
+    m.get_query_features(g["q_des"], qk, tuple(int(v) for v in g["shape"]))
+    m.run_matcher()
+    mk = m.matching_keypoints
+    assert np.array_equal(_kf_rows([t[0] for t in mk]), kf["mk_model"])
+    assert np.array_equal(_kf_rows([t[1] for t in mk]), kf["mk_query"])
+    assert all(t[1] is qk[q] for t, q in zip(mk, kf["mk_q"]))           # the caller's objects
+    assert np.array_equal(np.array([t[2] for t in mk]).reshape(-1, 2), kf["mk_img_size"])
+    assert np.array_equal(np.array([t[3] for t in mk]).reshape(-1, 2), kf["mk_centroid"])
+    assert all(m.kp[int(g["idx1"][q])] is t[0] for t, q in zip(mk, kf["mk_q"]))  # one object per row
+    m.apply_hough_transform(int(g["bins"]))
+    m.get_valid_bins(5)
+    for tag, bins in (("valid", m.valid_bins),):
+        off = np.concatenate([[0], np.cumsum([len(b.keypoint_pairs) for b in bins])])
+        assert np.array_equal(off, kf[tag + "_off"])
+        pairs = [p for b in bins for p in b.keypoint_pairs]
+        assert np.array_equal(_kf_rows([p[0] for p in pairs]), kf[tag + "_pairs_model"])
+        assert np.array_equal(_kf_rows([p[1] for p in pairs]), kf[tag + "_pairs_query"])
+    m.apply_affine_parameters(4)
+    off = np.concatenate([[0], np.cumsum([len(b.keypoint_pairs) for b in m.valid_bins])])
+    assert np.array_equal(off, kf["surv_off"])
+    pairs = list(m.keypoint_pairs)
+    assert np.array_equal(_kf_rows([p[0] for p in pairs]), kf["surv_pairs_model"])
+    assert np.array_equal(_kf_rows([p[1] for p in pairs]), kf["surv_pairs_query"])
+
+
 def _main_on(g):
     db = sod.SiftDatabase(g["db_des"], kp(g, "db_"), g["db_img"], g["centroid"], g["size"])
     m = sod.Main()

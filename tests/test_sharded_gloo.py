@@ -1,4 +1,4 @@
-"""Multi-rank path on the CPU: the product's ``run_sharded`` + ``TorchHostComm`` over a
+"""Multi-rank path on the CPU: the product's ``run_sharded`` + ``TorchHostComm`` (tests/torch_comm.py) over a
 real torch.distributed gloo group (world_size 2), with the oracle test double standing
 in for the device.  The sharded result must equal the single-rank result bit for bit
 (global top-2 merge before the ratio test; partial histograms reduced
@@ -41,7 +41,8 @@ def _worker(rank, world, port, outdir, bins):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
                             world_size=world)
     from fake_ctx import OracleCtx
-    from sift_based_od_amd.sharded import TorchHostComm, run_sharded, shard_range
+    from sift_based_od_amd.sharded import run_sharded, shard_range
+    from torch_comm import TorchHostComm
     db, qs = _case()
     lo, hi = shard_range(len(db), rank, world)
     ctx = OracleCtx(db, lo, hi, qs.des, qs.kp)
@@ -167,3 +168,26 @@ def test_shard_range_covers_rows():
             r = [shard_range(n, i, w) for i in range(w)]
             assert r[0][0] == 0 and r[-1][1] == n
             assert all(r[i][1] == r[i + 1][0] for i in range(w - 1))
+
+
+def test_file_store_fails_fast_without_shared_dir(tmp_path, monkeypatch):
+    """Ranks that do not share a store directory (no common launcher, no SOD_STORE_DIR) fail
+    at construction with the path they used, not after the exchange timeout."""
+    import time
+    sys.path.insert(0, os.path.dirname(HERE))
+    import sod_pkg
+    sod_pkg.load()
+    from sift_based_od_amd.sharded import FileStore
+    t0 = time.perf_counter()
+    with pytest.raises(TimeoutError, match="SOD_STORE_DIR"):
+        FileStore(2, 1, path=str(tmp_path / "alone"), timeout=600, join_timeout=0.5)
+    assert time.perf_counter() - t0 < 30
+    # the directory choice: explicit env first, then the launcher's run id
+    monkeypatch.setenv("SOD_STORE_DIR", str(tmp_path / "env"))
+    assert FileStore(1, 0).path == str(tmp_path / "env")
+    monkeypatch.delenv("SOD_STORE_DIR")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job42_%d" % os.getpid())
+    st = FileStore(1, 0)
+    assert st.path.endswith("sod_store_job42_%d" % os.getpid())
+    st.close()
+    assert not os.path.exists(st.path)
