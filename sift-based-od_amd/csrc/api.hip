@@ -193,15 +193,20 @@ static int db_writable(sod_ctx* ctx) {
 int sod_stage_mark(sod_ctx* ctx, int stage, bool end) {
   if (!ctx->stage_timing) return SOD_OK;
   if (!end) {
-    if (ctx->nseg >= sod_ctx::kSegs) return SOD_OK;   // a step of more segments: the rest uncounted
+    if (ctx->nseg >= sod_ctx::kSegs) {   // a step of more segments: the rest uncounted
+      ctx->seg_open = false;             // (and its end mark must not move segment kSegs-1's end)
+      return SOD_OK;
+    }
+    ctx->seg_open = true;
     hipEvent_t* e = ctx->seg_ev[ctx->nseg];
     for (int k = 0; k < 2; ++k)
       if (!e[k]) SOD_HIP(ctx, hipEventCreate(&e[k]));
     ctx->seg_stage[ctx->nseg] = stage;
     SOD_HIP(ctx, hipEventRecord(e[0], ctx->stream));
     ctx->nseg++;
-  } else if (ctx->nseg > 0 && ctx->seg_stage[ctx->nseg - 1] == stage) {
+  } else if (ctx->seg_open && ctx->nseg > 0 && ctx->seg_stage[ctx->nseg - 1] == stage) {
     SOD_HIP(ctx, hipEventRecord(ctx->seg_ev[ctx->nseg - 1][1], ctx->stream));
+    ctx->seg_open = false;
   }
   return SOD_OK;
 }
@@ -683,6 +688,7 @@ int sod_match_enqueue(sod_ctx* ctx) {
   if (!ctx->nsub || !ctx->nqt) return sod_fail(ctx, SOD_ESTATE, "upload DB descriptors and queries first");
   ctx->ratio_fused_valid = false;   // set again by a final merge that applies the pipeline's ratio
   ctx->nseg = 0;                    // a new step for sod_last_stage_ms
+  ctx->seg_open = false;
   SOD_TRY(ctx->impl != 0 ? launch_match_i8(ctx) : launch_match(ctx));
   ctx->matched = true;
   ctx->matches_given = false;
@@ -968,6 +974,7 @@ int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->ratio_fused_valid = false;
   ctx->nseg = 0;
+  ctx->seg_open = false;
   ctx->matched = ctx->ratio_done = true;
   ctx->matches_given = true;
   ctx->houghed = ctx->selected = ctx->affined = false;

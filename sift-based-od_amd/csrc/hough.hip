@@ -1467,8 +1467,12 @@ void sod_guard_host_pose(const double r[8], const int32_t bins[4], double* x, do
 int sod_guard_resolve(sod_ctx* ctx) {
   if (ctx->guard_done || !ctx->houghed) return SOD_OK;
   SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // every copy here is ordered on the context stream and waited for on it: a null-stream copy
+  // would also wait for the matcher stream (CU-masked streams are blocking streams), i.e. for
+  // the next step's matcher when the caller reads step N while step N+1 is in flight
   uint32_t n = 0;
-  SOD_HIP(ctx, hipMemcpy(&n, ctx->gstat.p + 1, 4, hipMemcpyDeviceToHost));
+  SOD_HIP(ctx, hipMemcpyAsync(&n, ctx->gstat.p + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->guard_flagged = n;
   ctx->guard_patched = 0;
   ctx->guard_flagged_total += n;
@@ -1479,8 +1483,11 @@ int sod_guard_resolve(sod_ctx* ctx) {
   const int64_t nq = sod_win_n(ctx);
   std::vector<double> rec((size_t)n * kGuardRec);
   std::vector<uint32_t> key((size_t)nq);
-  SOD_HIP(ctx, hipMemcpy(rec.data(), ctx->grec.p, rec.size() * 8, hipMemcpyDeviceToHost));
-  SOD_HIP(ctx, hipMemcpy(key.data(), ctx->basekey.p, key.size() * 4, hipMemcpyDeviceToHost));
+  SOD_HIP(ctx, hipMemcpyAsync(rec.data(), ctx->grec.p, rec.size() * 8, hipMemcpyDeviceToHost,
+                              ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(key.data(), ctx->basekey.p, key.size() * 4, hipMemcpyDeviceToHost,
+                              ctx->stream));
+  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   std::vector<int32_t> pq(n);
   std::vector<uint32_t> pkey(n);
   std::vector<double> pxy(2 * (size_t)n);
@@ -1502,9 +1509,11 @@ int sod_guard_resolve(sod_ctx* ctx) {
   int rc = sod_reserve(ctx, dq, n);
   if (rc == SOD_OK) rc = sod_reserve(ctx, dk, n);
   if (rc == SOD_OK) rc = sod_reserve(ctx, dxy, 2 * (size_t)n);
-  if (rc == SOD_OK && (hipMemcpy(dq.p, pq.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
-                       hipMemcpy(dk.p, pkey.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
-                       hipMemcpy(dxy.p, pxy.data(), (size_t)n * 16, hipMemcpyHostToDevice) != hipSuccess))
+  // (the host vectors outlive the stream synchronisation below)
+  if (rc == SOD_OK &&
+      (hipMemcpyAsync(dq.p, pq.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+       hipMemcpyAsync(dk.p, pkey.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+       hipMemcpyAsync(dxy.p, pxy.data(), (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
     rc = sod_fail(ctx, SOD_EHIP, "guard patch upload failed");
   if (rc == SOD_OK) {
     hipLaunchKernelGGL(guard_patch_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, ctx->stream,

@@ -1564,8 +1564,11 @@ int lds_order_probe(sod_ctx* ctx, int* ok) {
   int rc = sod_reserve(ctx, dv, v.size());
   if (rc == SOD_OK) rc = sod_reserve(ctx, da, a.size());
   if (rc == SOD_OK) rc = sod_reserve(ctx, dout, o.size());
-  if (rc == SOD_OK && (hipMemcpy(dv.p, v.data(), v.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-                       hipMemcpy(da.p, a.data(), a.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+  // copies on the context stream (the synchronisation below covers them): a null-stream copy
+  // would wait for every blocking stream of the process, the CU-masked ones included
+  if (rc == SOD_OK &&
+      (hipMemcpyAsync(dv.p, v.data(), v.size() * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+       hipMemcpyAsync(da.p, a.data(), a.size() * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
     rc = sod_fail(ctx, SOD_EHIP, "lds order probe upload failed");
   if (rc == SOD_OK) {
     hipLaunchKernelGGL(lds_order_probe_kernel, dim3(1), dim3(64), 0, ctx->stream, dv.p, da.p,
@@ -1882,9 +1885,11 @@ int grow_results(sod_ctx* ctx, SiftWork& W, int64_t need) {
   SOD_TRY(sod_reserve(ctx, nk, (size_t)n));
   SOD_TRY(sod_reserve(ctx, nd, (size_t)n * 128));
   for (SiftSlot* S : W.slots) SOD_HIP(ctx, hipStreamSynchronize(S->stream));
-  if (have > 0) {
-    SOD_HIP(ctx, hipMemcpy(nk.p, W.all_kp.p, (size_t)have * sizeof(Kp), hipMemcpyDeviceToDevice));
-    SOD_HIP(ctx, hipMemcpy(nd.p, W.all_desc.p, (size_t)have * 512, hipMemcpyDeviceToDevice));
+  if (have > 0) {   // on slot 0's stream, not the null stream (see lds_order_probe)
+    hipStream_t s0 = W.slots[0]->stream;
+    SOD_HIP(ctx, hipMemcpyAsync(nk.p, W.all_kp.p, (size_t)have * sizeof(Kp), hipMemcpyDeviceToDevice, s0));
+    SOD_HIP(ctx, hipMemcpyAsync(nd.p, W.all_desc.p, (size_t)have * 512, hipMemcpyDeviceToDevice, s0));
+    SOD_HIP(ctx, hipStreamSynchronize(s0));
   }
   sod_release(W.all_kp);
   sod_release(W.all_desc);
@@ -2054,9 +2059,14 @@ int sod_sift_get(sod_ctx* ctx, int64_t cap, float* x, float* y, float* size, flo
   const int64_t n = std::min<int64_t>(W->off.back(), std::max<int64_t>(cap, 0));
   if (n > 0) {
     std::vector<Kp> h((size_t)n);
-    SOD_HIP(ctx, hipMemcpy(h.data(), W->all_kp.p, (size_t)n * sizeof(Kp), hipMemcpyDeviceToHost));
+    // the detection's streams are done (its count sync); the copies go on slot 0's stream
+    // rather than the null stream, which would wait for every blocking stream of the process
+    for (SiftSlot* S : W->slots) SOD_HIP(ctx, hipStreamSynchronize(S->stream));
+    hipStream_t s0 = W->slots[0]->stream;
+    SOD_HIP(ctx, hipMemcpyAsync(h.data(), W->all_kp.p, (size_t)n * sizeof(Kp), hipMemcpyDeviceToHost, s0));
     if (descriptors)
-      SOD_HIP(ctx, hipMemcpy(descriptors, W->all_desc.p, (size_t)n * 512, hipMemcpyDeviceToHost));
+      SOD_HIP(ctx, hipMemcpyAsync(descriptors, W->all_desc.p, (size_t)n * 512, hipMemcpyDeviceToHost, s0));
+    SOD_HIP(ctx, hipStreamSynchronize(s0));
     for (int64_t i = 0; i < n; ++i) {
       const Kp& k = h[(size_t)i];
       if (x) x[i] = k.x;

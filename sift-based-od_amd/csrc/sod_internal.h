@@ -217,6 +217,7 @@ struct sod_ctx {
   hipEvent_t seg_ev[kSegs][2] = {};
   int seg_stage[kSegs] = {};
   int nseg = 0;
+  bool seg_open = false;   // the last begin mark was recorded (not dropped at kSegs)
   hipEvent_t ev[8] = {};
   // begin/end events of the last kMatchRing matcher launches (sod_match_times), so the
   // kernel is timed inside a pipelined run, not only in isolated launches

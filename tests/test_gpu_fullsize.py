@@ -155,3 +155,49 @@ def test_c3_db_sharded_8_ways_equals_single(ctx, c3):
         assert np.array_equal(v1["means"], v2["means"])
         assert np.array_equal(a1["survived"], a2["survived"])
         assert np.array_equal(a1["params"], a2["params"])
+
+
+def test_result_read_does_not_wait_for_another_matcher(ctx, c3):
+    """A context reading its results while another context's C3 matcher runs on CU-masked
+    (hence blocking) streams: every copy of the read is ordered on the reader's own stream,
+    so it returns in well under that matcher's ~3.7 ms (a null-stream copy -- the boundary
+    guard's read-back before round 4 -- waited for it)."""
+    import time
+
+    from sift_based_od_amd import _lib
+    db, qs = c3
+    ctx.set_impl("i8")
+    try:
+        ctx.set_cu_reserve(1)
+    except _lib.SodError:
+        pytest.skip("CU split needs a whole MI355X")
+    try:
+        ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        ctx.upload_db(db.des)
+        ctx.upload_queries(qs.des, qs.kp)
+        ctx.match()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        ctx.match()
+        ctx.synchronize()
+        t_match = time.perf_counter() - t0
+        with _lib.Context(0) as a:
+            a.share_db(ctx)
+            a.upload_queries(qs.des[:500], qs.kp.slice(0, 500))
+            a.pipeline(qs.shape, BINS)
+            a.synchronize()
+            ref = a.valid_result()
+            a.upload_queries(qs.des[:500], qs.kp.slice(0, 500))
+            a.pipeline(qs.shape, BINS)
+            a.synchronize()
+            ctx.match()                       # the other context's matcher is in flight
+            t0 = time.perf_counter()
+            v = a.valid_result()
+            a.affine_result()
+            t_read = time.perf_counter() - t0
+            ctx.synchronize()
+        assert np.array_equal(v["keys"], ref["keys"])
+        assert t_read < 0.5 * t_match, (t_read, t_match)
+    finally:
+        ctx.synchronize()
+        ctx.set_cu_reserve(0)
