@@ -609,11 +609,10 @@ def main():
                      "traffic_gb_per_s": traffic / (match_ms * 1e6) if traffic else None,
                      "traffic_frac_of_hbm_peak": traffic / (match_ms * 1e6) / 8000.0 if traffic else None,
                      "mfma_busy_frac_pmc": pmc.get("mfma_busy_frac") if pmc else None,
-                     "clock_ghz_pmc": pmc.get("clock_ghz") if pmc else None,
-                     # the dense peak is quoted at 2.4 GHz; at the clock the chip holds
-                     # under this kernel (PMC passes) the attainable peak is lower
-                     "frac_at_pmc_clock": achieved / (peak * pmc["clock_ghz"] / 2.4)
-                     if pmc and pmc.get("clock_ghz") else None,
+                     # the profiled dispatches' own clock (GRBM_GUI_ACTIVE / 8 over their
+                     # own duration): how far below the 2.4 GHz of the quoted peak the chip
+                     # ran under the counters; no fraction is derived from it
+                     "clock_ghz_pmc_profiled": pmc.get("clock_ghz_profiled") if pmc else None,
                      "algorithmic_bytes": alg_bytes,
                      "kernel": kernel,
                      "algorithmic": "256 op/pair x %d x %d pairs per launch" % (nq, n_shard)},

@@ -69,6 +69,11 @@ int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n);
  * a marker packet on the tail's critical path, so a timed loop turns them off.  With them
  * off, sod_last_stage_ms reports 0 for the stages after the matcher. */
 int sod_set_stage_timing(sod_ctx* ctx, int on);
+/* Begin / end events of every matcher launch (1, the default; sod_match_times and
+ * sod_last_match_ms read them) or none (0) when the launch runs on the context stream: a
+ * dispatch that records an event delays the stream's next kernel by ~5 us, a share of a
+ * one-image step.  Launches on the matcher stream (overlap / CU split) keep their events. */
+int sod_set_match_timing(sod_ctx* ctx, int on);
 
 /* ---- database (replaces main.py:36-66 flattening + GenerateDatabaseInfo.py format) --
  * Keypoints and the per-image table cover the WHOLE database (replicated on every
@@ -191,6 +196,13 @@ int sod_hough_allreduce_enqueue(sod_ctx* ctx);
  * (main.py:121-132), their member lists in match order, and the PoseBin running means
  * (centroid x,y, angle, scale, img_size w,h) in vote order. */
 int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold);
+/* main.py:89-132 as one call: sod_hough_enqueue over this rank's shard (all rows on one
+ * rank), the all-reduce, sod_select_enqueue.  One image of <= 2048 queries on one rank runs
+ * as ONE kernel (pose, votes, valid bins, members, the affine inputs) without the dense bin
+ * histogram, which readers that need it (sod_bins_*, another threshold, the host exchange)
+ * build on demand; results identical either way.  sod_pipeline_enqueue uses it. */
+int sod_hough_select_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w,
+                             const int32_t bins[4], int32_t vote_threshold);
 int sod_valid_counts(sod_ctx* ctx, int64_t* n_valid, int64_t* n_members);
 int sod_valid_get(sod_ctx* ctx, int32_t* keys /* [V*4] */, int32_t* votes /* [V] */,
                   int64_t* offsets /* [V+1] */, int32_t* members /* [M] query idx */,

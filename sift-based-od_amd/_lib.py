@@ -50,6 +50,7 @@ SIGNATURES = {
     "sod_match_times": (C.c_int, [c_ctx, C.c_int, c_f32p]),
     "sod_last_stage_ms": (C.c_int, [c_ctx, c_f32p, C.c_int]),
     "sod_set_stage_timing": (C.c_int, [c_ctx, C.c_int]),
+    "sod_set_match_timing": (C.c_int, [c_ctx, C.c_int]),
     "sod_db_set_keypoints": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_i32p,
                                        C.c_int32, c_f64p, c_i32p]),
     "sod_db_upload_descriptors": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int64, C.c_int64]),
@@ -76,6 +77,7 @@ SIGNATURES = {
     "sod_hough_enqueue": (C.c_int, [c_ctx, C.c_int32, C.c_int32, c_i32p, C.c_int64, C.c_int64]),
     "sod_hough_allreduce_enqueue": (C.c_int, [c_ctx]),
     "sod_select_enqueue": (C.c_int, [c_ctx, C.c_int32]),
+    "sod_hough_select_enqueue": (C.c_int, [c_ctx, C.c_int32, C.c_int32, c_i32p, C.c_int32]),
     "sod_valid_counts": (C.c_int, [c_ctx, c_i64p, c_i64p]),
     "sod_valid_get": (C.c_int, [c_ctx, c_i32p, c_i32p, c_i64p, c_i32p, c_f64p]),
     "sod_bins_count": (C.c_int, [c_ctx, c_i64p]),
@@ -325,6 +327,15 @@ class Context:
     def select(self, vote_threshold=5):
         self._chk(self._L.sod_select_enqueue(self._h, int(vote_threshold)))
 
+    def hough_select(self, query_shape, bins, vote_threshold=5):
+        """Hough + select in one call (sod_hough_select_enqueue): one fused launch for one image
+        of <= 2048 queries on one rank, else hough() + select()."""
+        b = np.ascontiguousarray(bins4(bins), np.int32)
+        self._chk(self._L.sod_hough_select_enqueue(self._h, int(query_shape[0]),
+                                                   int(query_shape[1]), ptr(b, C.c_int32),
+                                                   int(vote_threshold)))
+        self.bins = tuple(int(v) for v in b)
+
     def valid_counts(self):
         v, m = C.c_int64(), C.c_int64()
         self._chk(self._L.sod_valid_counts(self._h, C.byref(v), C.byref(m)))
@@ -396,6 +407,11 @@ class Context:
         out = np.zeros(int(n), np.float32)
         self._chk(self._L.sod_match_times(self._h, int(n), ptr(out, C.c_float)))
         return out
+
+    def set_match_timing(self, on):
+        """Matcher launch events (sod_set_match_timing; default on): off removes them from
+        context-stream launches, the one-image latency path."""
+        self._chk(self._L.sod_set_match_timing(self._h, 1 if on else 0))
 
     def set_stage_timing(self, on):
         """Record the per-stage events read by stage_ms (default on; off in timed loops)."""

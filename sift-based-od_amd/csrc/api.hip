@@ -83,12 +83,18 @@ int sod_inputs_end(sod_ctx* ctx) {
   SOD_HIP(ctx, hipEventRecord(ctx->ev_inputs, ctx->stream));
   return SOD_OK;
 }
+static bool stream_idle(hipStream_t s) {
+  const hipError_t q = hipStreamQuery(s);
+  if (q == hipSuccess) return true;
+  (void)hipGetLastError();   // hipErrorNotReady (or an error the next call reports)
+  return false;
+}
 int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1, int32_t** idx,
                            float** d2) {
   const int nslot = ctx->overlap ? 2 : 1;
   if (ctx->pd1.n < (size_t)(nslot * n)) {   // growing: no kernel or merge may still use them
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+    SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   }
   SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(nslot * n)));
   SOD_TRY(sod_reserve(ctx, ctx->pd2, (size_t)(nslot * n)));
@@ -99,11 +105,25 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
   *d1 = ctx->pd1.p + ctx->pslot * n;
   *d2 = ctx->pd2.p + ctx->pslot * n;
   *idx = ctx->pidx.p + ctx->pslot * n;
-  if (!ctx->overlap) {
+  // The matcher stream buys overlap with an earlier step's tail.  Without the CU split and with
+  // both streams idle there is nothing to overlap: the kernel goes on the context stream, so
+  // the merge after it needs no cross-stream wait (~10 us on the one-image path, where the
+  // whole step is ~0.1 ms).  The slot protocol below is unchanged either way.
+  ctx->mk_main = !ctx->overlap ||
+                 (ctx->cu_reserve == 0 && stream_idle(ctx->stream) && stream_idle(ctx->mstream));
+  if (ctx->mk_main) {
     *ks = ctx->stream;
+    if (ctx->overlap) SOD_HIP(ctx, hipEventSynchronize(ctx->ev_merged[ctx->pslot]));
     return SOD_OK;
   }
   *ks = ctx->mstream;
+  // merges that ran on the context stream right after a context-stream matcher released
+  // their slot without an event (sod_merge_done_event): mark them now
+  for (int x = 0; x < 2; ++x)
+    if (ctx->merge_norec[x]) {
+      SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[x], ctx->stream));
+      ctx->merge_norec[x] = false;
+    }
   SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_inputs));
   // the slot's previous merge (two launches back) must be done before the kernel rewrites
   // it: the host waits for it here rather than the matcher stream (a satisfied barrier packet
@@ -122,13 +142,15 @@ int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end) {
   if (end) ++ctx->nmatch;
   return SOD_OK;
 }
-int sod_partials_merged(sod_ctx* ctx) {
-  SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[ctx->pslot], ctx->stream));
-  return SOD_OK;
-}
 // begin / end events of the next matcher launch, recorded by the launch itself
 // (hipExtLaunchKernelGGL: timestamps in the dispatch, no marker packets around the kernel)
 int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end) {
+  if (!ctx->match_timing && ctx->mk_main) {
+    // untimed launch on the context stream: a dispatch that records an event delays the next
+    // kernel of the stream by ~5 us (rocprofv3, one-image step); nothing waits on these
+    *begin = *end = nullptr;
+    return SOD_OK;
+  }
   hipEvent_t* e = ctx->mev[ctx->nmatch % sod_ctx::kMatchRing];
   for (int i = 0; i < 2; ++i)
     if (!e[i]) SOD_HIP(ctx, hipEventCreate(&e[i]));
@@ -138,13 +160,33 @@ int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end) {
   return SOD_OK;
 }
 int sod_match_stream_end(sod_ctx* ctx, hipEvent_t done) {
-  const hipStream_t ks = ctx->overlap ? ctx->mstream : ctx->stream;
+  const hipStream_t ks = ctx->mk_main ? ctx->stream : ctx->mstream;
+  if (!done && ctx->mk_main) {   // stream order covers every reader: no event
+    ctx->ev_matched_p = nullptr;
+    return SOD_OK;
+  }
   if (!done) {
     SOD_HIP(ctx, hipEventRecord(ctx->ev_matched, ks));
     done = ctx->ev_matched;
   }
   ctx->ev_matched_p = done;
-  if (ctx->overlap) SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, done, 0));
+  if (!ctx->mk_main) SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, done, 0));
+  return SOD_OK;
+}
+
+// the event that releases the partial-result slot after its merge: recorded by the merge's
+// dispatch when the matcher ran on its own stream; after a context-stream matcher none (a
+// dispatch event delays the stream's next kernel ~5 us) -- a later matcher-stream launch
+// records it then (sod_match_stream_begin)
+hipEvent_t sod_merge_done_event(sod_ctx* ctx) {
+  ctx->merge_norec[ctx->pslot] = ctx->mk_main && ctx->overlap;
+  return ctx->mk_main ? nullptr : ctx->ev_merged[ctx->pslot];
+}
+
+int sod_set_match_timing(sod_ctx* ctx, int on) {
+  SOD_TRY(set_dev(ctx));
+  if (on != 0 && on != 1) return sod_fail(ctx, SOD_EINVAL, "match timing must be 0 or 1");
+  ctx->match_timing = on != 0;
   return SOD_OK;
 }
 
@@ -168,9 +210,9 @@ static void db_detach(sod_ctx* ctx) {
 }
 
 static void drain_streams(sod_ctx* ctx) {
-  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
-  if (ctx->mstream) (void)hipStreamSynchronize(ctx->mstream);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->side) (void)sod_stream_sync(ctx->side);
+  if (ctx->mstream) (void)sod_stream_sync(ctx->mstream);
+  if (ctx->stream) (void)sod_stream_sync(ctx->stream);
 }
 
 // Every DB writer calls this first: a source whose DB other contexts alias refuses (their
@@ -246,12 +288,14 @@ int sod_create(int device, sod_ctx** out) {
   }
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  // ev_fork and ev_merged are recorded by kernel dispatches (hipExtLaunchKernelGGL): default
+  // events
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_fork);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->mstream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_inputs, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i)
-    e = hipEventCreateWithFlags(&ctx->ev_merged[i], hipEventDisableTiming);
+    e = hipEventCreate(&ctx->ev_merged[i]);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_matched, hipEventDisableTiming);
   if (e != hipSuccess) {
     g_err = std::string("sod_create: ") + hipGetErrorString(e);
@@ -271,9 +315,9 @@ int sod_create(int device, sod_ctx** out) {
 void sod_destroy(sod_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
-  if (ctx->mstream) (void)hipStreamSynchronize(ctx->mstream);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->side) (void)sod_stream_sync(ctx->side);
+  if (ctx->mstream) (void)sod_stream_sync(ctx->mstream);
+  if (ctx->stream) (void)sod_stream_sync(ctx->stream);
   db_detach(ctx);
   // contexts still aliasing this DB: let their queued work finish, then drop their views
   // (they report "no database" afterwards instead of reading freed memory)
@@ -298,7 +342,7 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->first); sod_release(ctx->basekey); sod_release(ctx->vmask);
   sod_release(ctx->pose); sod_release(ctx->selstat); sod_release(ctx->selticket); sod_release(ctx->scal); sod_release(ctx->vbin);
   sod_release(ctx->voff); sod_release(ctx->members); sod_release(ctx->means);
-  sod_release(ctx->vidx); sod_release(ctx->cursor);
+  sod_release(ctx->vidx); sod_release(ctx->cursor); sod_release(ctx->vfirst_s);
   sod_release(ctx->rtab); sod_release(ctx->msize);
   sod_release(ctx->pose_b); sod_release(ctx->msize_b); sod_release(ctx->scal_b);
   sod_release(ctx->voff_b); sod_release(ctx->members_b); sod_release(ctx->means_b);
@@ -338,8 +382,8 @@ const char* sod_last_error(const sod_ctx* ctx) {
 
 int sod_synchronize(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   return SOD_OK;
 }
 
@@ -377,7 +421,7 @@ int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n) {
   // stage's own launches in the last step
   SOD_TRY(set_dev(ctx));
   if (!ms_out || n < 0) return sod_fail(ctx, SOD_EINVAL, "null output");
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   float acc[kStages] = {};
   if (ctx->matched && ctx->nmatch > 0) {   // the last matcher launch's own begin / end events
     hipEvent_t* m = ctx->mev[(ctx->nmatch - 1) % sod_ctx::kMatchRing];
@@ -416,7 +460,7 @@ int sod_db_set_keypoints(sod_ctx* ctx, int64_t n_total, const float* x, const fl
   SOD_TRY(upload(ctx, ctx->mimg, img, (size_t)n_total));
   SOD_TRY(upload(ctx, ctx->cent, centroid, (size_t)n_images * 2));
   SOD_TRY(upload(ctx, ctx->isize, size, (size_t)n_images * 2));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->n_total = n_total;
   ctx->n_images = n_images;
   return SOD_OK;
@@ -445,7 +489,7 @@ static int upload_descriptors(sod_ctx* ctx, const void* des, int dtype, int64_t 
   SOD_TRY(sod_inputs_end(ctx));
   uint32_t bad = 0;
   SOD_HIP(ctx, hipMemcpyAsync(&bad, ctx->flags.p, 4, hipMemcpyDeviceToHost, ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   // staging is only needed during the upload
   if (dtype == SOD_DTYPE_U8) sod_release(ctx->stage_u8); else sod_release(ctx->stage_f32);
   if (bad)
@@ -496,10 +540,10 @@ int sod_db_share(sod_ctx* dst, sod_ctx* src) {
   dst->nsub = src->nsub;
   dst->nqt = 0;   // queries must be re-uploaded in the (possibly new) layout
   // raw max ||d||^2 for sod_match_exact_order; the source's uploads are complete
-  SOD_HIP(dst, hipStreamSynchronize(src->stream));
+  SOD_HIP(dst, sod_stream_sync(src->stream));
   SOD_HIP(dst, hipMemcpyAsync(dst->flags.p + 1, src->flags.p + 1, 4, hipMemcpyDeviceToDevice,
                               dst->stream));
-  SOD_HIP(dst, hipStreamSynchronize(dst->stream));
+  SOD_HIP(dst, sod_stream_sync(dst->stream));
   dst->matched = dst->ratio_done = dst->houghed = dst->selected = dst->affined = false;
   return SOD_OK;
 }
@@ -562,7 +606,7 @@ int sod_db_export_packed(sod_ctx* ctx, void* out, int64_t bytes) {
                               hipMemcpyDeviceToHost, ctx->stream));
   SOD_HIP(ctx, hipMemcpyAsync(o + sizeof(h) + ctx->nsub * sb, ctx->dn.p, (size_t)nb,
                               hipMemcpyDeviceToHost, ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   std::memcpy(o, &h, sizeof(h));
   return SOD_OK;
 }
@@ -594,7 +638,7 @@ int sod_db_import_packed(sod_ctx* ctx, const void* in, int64_t bytes) {
                               hipMemcpyHostToDevice, ctx->stream));
   SOD_HIP(ctx, hipMemcpyAsync(ctx->flags.p + 1, &h.max_norm, 4, hipMemcpyHostToDevice, ctx->stream));
   SOD_TRY(sod_inputs_end(ctx));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->nsub = h.nsub;
   ctx->n_shard = h.n_rows;
   ctx->row_offset = h.row_offset;
@@ -621,7 +665,7 @@ int sod_query_upload(sod_ctx* ctx, const void* des, int dtype, int32_t nq, const
     SOD_TRY(upload(ctx, ctx->qy, y, (size_t)nq));
     SOD_TRY(upload(ctx, ctx->qang, angle, (size_t)nq));
     SOD_TRY(upload(ctx, ctx->qoct, octave, (size_t)nq));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   }
   ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
@@ -664,7 +708,7 @@ int sod_query_images(sod_ctx* ctx, int32_t n_images, const int32_t* q_offsets,
     for (int32_t q = q_offsets[b]; q < q_offsets[b + 1]; ++q) img[(size_t)q] = b;
   SOD_TRY(upload(ctx, ctx->qimg, img.data(), img.size()));
   SOD_TRY(upload(ctx, ctx->qshape, ctx->qshape_h.data(), ctx->qshape_h.size()));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->n_qimg = n_images;
   ctx->win0 = 0;
   ctx->winn = -1;
@@ -677,7 +721,7 @@ int sod_valid_images_get(sod_ctx* ctx, int32_t* image) {
   SOD_TRY(sod_valid_counts(ctx, &V, &M));
   std::vector<uint32_t> lin((size_t)V);
   SOD_TRY(download(ctx, lin.data(), ctx->vbin.p, (size_t)V));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   for (int64_t v = 0; v < V; ++v) image[v] = (int32_t)(lin[(size_t)v] / ctx->nbins1);
   return SOD_OK;
 }
@@ -700,8 +744,8 @@ int sod_match_set_overlap(sod_ctx* ctx, int on) {
   SOD_TRY(set_dev(ctx));
   if (on != 0 && on != 1) return sod_fail(ctx, SOD_EINVAL, "overlap must be 0 or 1");
   // everything enqueued so far, on either stream, is ordered before the switch
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   if (!on && ctx->cu_reserve)
     return sod_fail(ctx, SOD_ESTATE, "the CU split (sod_set_cu_reserve) needs the matcher stream");
   ctx->overlap = on != 0;
@@ -751,9 +795,9 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
                           std::to_string(per_xcd * nx) +
                           " CUs: call sod_set_cu_reserve before sod_comm_init");
   }
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->side));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->side));
+  SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->side_pending = false;
   const int n = ctx->num_cus, words = (n + 31) / 32, r = per_xcd * nx;
   std::vector<uint32_t> tail, match;
@@ -848,7 +892,7 @@ int sod_match_get(sod_ctx* ctx, int32_t* idx1, float* d1, float* d2, uint8_t* go
   SOD_TRY(download(ctx, d1, ctx->d1.p, n));
   SOD_TRY(download(ctx, d2, ctx->d2.p, n));
   SOD_TRY(download(ctx, good, ctx->good.p, n));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   return SOD_OK;
 }
 
@@ -892,7 +936,7 @@ static int knn_float_indices(sod_ctx* ctx, bool want2, std::vector<int32_t>& f1,
   SOD_TRY(download(ctx, i1.data(), ctx->idx1.p, n));
   SOD_TRY(download(ctx, d1.data(), ctx->d1.p, n));
   SOD_TRY(download(ctx, d2.data(), ctx->d2.p, n));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   DevBuf<float> dlo, dhi;
   DevBuf<int32_t> dex, dfound;
   int rc = SOD_OK;
@@ -906,7 +950,7 @@ static int knn_float_indices(sod_ctx* ctx, bool want2, std::vector<int32_t>& f1,
       rc = ctx->impl == 1 ? launch_find_rows_i8(ctx, dlo.p, dhi.p, dex.p, dfound.p)
                           : launch_find_rows(ctx, dlo.p, dhi.p, dex.p, dfound.p);
     if (rc == SOD_OK) rc = download(ctx, out.data(), dfound.p, np);
-    if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+    if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
       rc = sod_fail(ctx, SOD_EHIP, "knn index pass failed");
   };
   // OpenCV orders by the float distance sqrtf(d^2), ties to the lower trainIdx.  With every
@@ -924,7 +968,7 @@ static int knn_float_indices(sod_ctx* ctx, bool want2, std::vector<int32_t>& f1,
     for (size_t q = 0; q < n; ++q) ex[q] = f1[q];
     pass(d2, f2);
   }
-  (void)hipStreamSynchronize(ctx->stream);
+  (void)sod_stream_sync(ctx->stream);
   sod_release(dlo);
   sod_release(dhi);
   sod_release(dex);
@@ -953,7 +997,7 @@ int sod_match_float_order(sod_ctx* ctx) {
   std::vector<int32_t> f1, f2;
   SOD_TRY(knn_float_indices(ctx, false, f1, f2));
   SOD_TRY(upload(ctx, ctx->idx1, f1.data(), (size_t)ctx->nq));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
 }
@@ -971,7 +1015,7 @@ int sod_matches_set(sod_ctx* ctx, int32_t nq, const int32_t* idx1, const uint8_t
   SOD_TRY(sod_reserve(ctx, ctx->d2, (size_t)nq));
   SOD_HIP(ctx, hipMemsetAsync(ctx->d1.p, 0, (size_t)nq * 4, ctx->stream));
   SOD_HIP(ctx, hipMemsetAsync(ctx->d2.p, 0, (size_t)nq * 4, ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->ratio_fused_valid = false;
   ctx->nseg = 0;
   ctx->seg_open = false;
@@ -985,7 +1029,7 @@ int sod_match_exact_order(sod_ctx* ctx, int* exact) {
   SOD_TRY(set_dev(ctx));
   uint32_t f[4];
   SOD_HIP(ctx, hipMemcpyAsync(f, ctx->flags.p, 16, hipMemcpyDeviceToHost, ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   float dn, qn;
   std::memcpy(&dn, &f[1], 4);
   std::memcpy(&qn, &f[2], 4);
@@ -996,9 +1040,8 @@ int sod_match_exact_order(sod_ctx* ctx, int* exact) {
 }
 
 // ---- hough ----------------------------------------------------------------------------
-int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int32_t bins[4],
-                      int64_t own_lo, int64_t own_hi) {
-  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
+// the argument / state checks of a Hough launch (sod_hough_enqueue and the fused path)
+static int hough_check(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int32_t bins[4]) {
   if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "match + ratio first");
   if (!ctx->n_total || !ctx->qx.p) return sod_fail(ctx, SOD_ESTATE, "keypoints not uploaded");
   if (query_h < 1 || query_w < 1) return sod_fail(ctx, SOD_EINVAL, "bad query image shape");
@@ -1010,6 +1053,13 @@ int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int3
   }
   ctx->qh = query_h;
   ctx->qw = query_w;
+  return SOD_OK;
+}
+
+int sod_hough_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w, const int32_t bins[4],
+                      int64_t own_lo, int64_t own_hi) {
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
+  SOD_TRY(hough_check(ctx, query_h, query_w, bins));
   SOD_TRY(sod_stage_mark(ctx, kStageHough, false));
   SOD_TRY(launch_hough(ctx, own_lo, own_hi));
   SOD_TRY(sod_stage_mark(ctx, kStageHough, true));
@@ -1023,6 +1073,7 @@ int sod_hough_allreduce_enqueue(sod_ctx* ctx) {
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
   if (ctx->nranks <= 1 && !ctx->comm) return SOD_OK;   // a 1-rank communicator still runs
   if (!ctx->comm) return sod_fail(ctx, SOD_ECOMM, "no communicator");
+  SOD_TRY(sod_hist_dense(ctx));
   SOD_TRY(sod_stage_mark(ctx, kStageAllreduce, false));
   ncclResult_t r = ncclGroupStart();
   if (r == ncclSuccess)
@@ -1037,9 +1088,31 @@ int sod_hough_allreduce_enqueue(sod_ctx* ctx) {
   return SOD_OK;
 }
 
+int sod_hough_select_enqueue(sod_ctx* ctx, int32_t query_h, int32_t query_w,
+                             const int32_t bins[4], int32_t vote_threshold) {
+  SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
+  if (sod_hough_small_ok(ctx)) {
+    // one image of <= 2048 queries on one rank: vote + select + affine gather in one launch
+    SOD_TRY(hough_check(ctx, query_h, query_w, bins));
+    SOD_TRY(sod_stage_mark(ctx, kStageHough, false));
+    SOD_TRY(launch_hough_small(ctx, vote_threshold));
+    SOD_TRY(sod_stage_mark(ctx, kStageHough, true));
+    ctx->houghed = ctx->selected = true;
+    ctx->affined = false;
+    ctx->vote_thr = vote_threshold;
+    return SOD_OK;
+  }
+  const int64_t lo = ctx->nranks > 1 ? ctx->row_offset : 0;
+  const int64_t hi = ctx->nranks > 1 ? ctx->row_offset + ctx->n_shard : ctx->n_total;
+  SOD_TRY(sod_hough_enqueue(ctx, query_h, query_w, bins, lo, hi));
+  SOD_TRY(sod_hough_allreduce_enqueue(ctx));
+  return sod_select_enqueue(ctx, vote_threshold);
+}
+
 int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold) {
   SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  SOD_TRY(sod_hist_dense(ctx));
   SOD_TRY(sod_stage_mark(ctx, kStageSelect, false));
   SOD_TRY(launch_select(ctx, vote_threshold));
   SOD_TRY(sod_stage_mark(ctx, kStageSelect, true));
@@ -1055,7 +1128,7 @@ int sod_valid_counts(sod_ctx* ctx, int64_t* n_valid, int64_t* n_members) {
   SOD_TRY(sod_guard_resolve(ctx));
   uint32_t s[2];
   SOD_HIP(ctx, hipMemcpyAsync(s, ctx->scal.p, 8, hipMemcpyDeviceToHost, ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   if (n_valid) *n_valid = s[0];
   if (n_members) *n_members = s[1];
   return SOD_OK;
@@ -1082,7 +1155,7 @@ int sod_valid_get(sod_ctx* ctx, int32_t* keys, int32_t* votes, int64_t* offsets,
   SOD_TRY(download(ctx, off.data(), ctx->voff.p, (size_t)V + 1));
   SOD_TRY(download(ctx, members, ctx->members.p, (size_t)M));
   SOD_TRY(download(ctx, means, ctx->means.p, (size_t)V * 6));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   if (keys) decode_keys(ctx, lin, keys);
   if (votes)
     for (int64_t i = 0; i < V; ++i) votes[i] = (int32_t)(off[i + 1] - off[i]);
@@ -1094,10 +1167,11 @@ int sod_bins_count(sod_ctx* ctx, int64_t* n_bins) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
   SOD_TRY(sod_guard_resolve(ctx));
+  SOD_TRY(sod_hist_dense(ctx));
   SOD_TRY(launch_all_bins(ctx));
   uint32_t b = 0;
   SOD_HIP(ctx, hipMemcpyAsync(&b, ctx->scal.p + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   *n_bins = b;
   return SOD_OK;
 }
@@ -1107,10 +1181,10 @@ int sod_bins_get(sod_ctx* ctx, int32_t* keys, int32_t* votes) {
   SOD_TRY(sod_bins_count(ctx, &B));
   std::vector<uint32_t> lin((size_t)B);
   SOD_TRY(download(ctx, lin.data(), ctx->allbin.p, (size_t)B));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   std::vector<uint32_t> cnt((size_t)ctx->nbins);
   SOD_TRY(download(ctx, cnt.data(), ctx->counts.p, (size_t)ctx->nbins));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   if (keys) decode_keys(ctx, lin, keys);
   if (votes)
     for (int64_t i = 0; i < B; ++i) votes[i] = (int32_t)cnt[lin[i]];
@@ -1140,7 +1214,7 @@ int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_
   ctx->aff_yf = y_factor;
   ctx->aff_thr = threshold;
   SOD_TRY(sod_stage_mark(ctx, kStageAffine, false));
-  SOD_TRY(launch_affine_gather(ctx));
+  if (!ctx->gathered) SOD_TRY(launch_affine_gather(ctx));   // the fused path gathered them
   SOD_TRY(sod_reserve(ctx, ctx->surv, (size_t)ctx->vmax));
   SOD_TRY(sod_reserve(ctx, ctx->fvotes, (size_t)ctx->vmax));
   SOD_TRY(sod_reserve(ctx, ctx->params, (size_t)ctx->vmax * 6));
@@ -1164,7 +1238,7 @@ int sod_affine_get(sod_ctx* ctx, uint8_t* survived, int32_t* votes, double* para
   SOD_TRY(download(ctx, votes, ctx->fvotes.p, (size_t)V));
   SOD_TRY(download(ctx, params, ctx->params.p, (size_t)V * 6));
   SOD_TRY(download(ctx, member_alive, ctx->alive.p, (size_t)M));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   return SOD_OK;
 }
 
@@ -1180,11 +1254,7 @@ int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* a) {
   ctx->fuse_ratio = -1.0;
   SOD_TRY(rc);
   SOD_TRY(sod_ratio_enqueue(ctx, a->ratio));
-  const int64_t lo = ctx->nranks > 1 ? ctx->row_offset : 0;
-  const int64_t hi = ctx->nranks > 1 ? ctx->row_offset + ctx->n_shard : ctx->n_total;
-  SOD_TRY(sod_hough_enqueue(ctx, a->query_h, a->query_w, a->bins, lo, hi));
-  SOD_TRY(sod_hough_allreduce_enqueue(ctx));
-  SOD_TRY(sod_select_enqueue(ctx, a->vote_threshold));
+  SOD_TRY(sod_hough_select_enqueue(ctx, a->query_h, a->query_w, a->bins, a->vote_threshold));
   if (a->run_affine)
     SOD_TRY(sod_affine_enqueue(ctx, a->query_w, a->query_h, a->x_factor, a->y_factor,
                                a->affine_threshold));
@@ -1227,14 +1297,14 @@ int sod_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my, co
   if (rc == SOD_OK) rc = download(ctx, idx, di.p, (size_t)n * 4);
   uint32_t ng = 0;
   if (rc == SOD_OK) rc = download(ctx, &ng, gst.p, 1);
-  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+  if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
     rc = sod_fail(ctx, SOD_EHIP, "pose batch failed");
-  (void)hipStreamSynchronize(ctx->stream);
+  (void)sod_stream_sync(ctx->stream);
   // boundary guard (hough.hip): the listed elements' x, y and x / y bins with glibc cos / sin
   if (rc == SOD_OK && ng) {
     std::vector<double> rec((size_t)ng * 8);
     rc = download(ctx, rec.data(), grec.p, rec.size());
-    if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+    if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
       rc = sod_fail(ctx, SOD_EHIP, "guard records download failed");
     int64_t changed = 0;
     for (uint32_t i = 0; rc == SOD_OK && i < ng; ++i) {
@@ -1297,9 +1367,9 @@ int sod_affine_batch(sod_ctx* ctx, int64_t n_bins, const int64_t* offsets, const
   if (rc == SOD_OK) rc = download(ctx, votes, vo.p, (size_t)n_bins);
   if (rc == SOD_OK) rc = download(ctx, params, pr.p, (size_t)n_bins * 6);
   if (rc == SOD_OK) rc = download(ctx, member_alive, al.p, (size_t)M);
-  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+  if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
     rc = sod_fail(ctx, SOD_EHIP, "affine batch failed");
-  (void)hipStreamSynchronize(ctx->stream);
+  (void)sod_stream_sync(ctx->stream);
   sod_release(off);
   for (auto& b : p) sod_release(b);
   sod_release(is); sod_release(vo); sod_release(sv); sod_release(al); sod_release(pr);
@@ -1322,9 +1392,9 @@ int sod_bin_index_batch(sod_ctx* ctx, int64_t n, const double* pose, int32_t que
   if (rc == SOD_OK) rc = sod_reserve(ctx, di, (size_t)n * 4);
   if (rc == SOD_OK) rc = launch_bin_index_batch(ctx, n, dp.p, di.p);
   if (rc == SOD_OK) rc = download(ctx, idx, di.p, (size_t)n * 4);
-  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+  if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
     rc = sod_fail(ctx, SOD_EHIP, "bin index batch failed");
-  (void)hipStreamSynchronize(ctx->stream);
+  (void)sod_stream_sync(ctx->stream);
   sod_release(dp);
   sod_release(di);
   return rc;
@@ -1338,7 +1408,7 @@ int sod_match_candidates_get(sod_ctx* ctx, float* d1sq, int32_t* idx, float* d2s
   SOD_TRY(download(ctx, d1sq, ctx->cd1.p, n));
   SOD_TRY(download(ctx, idx, ctx->cidx.p, n));
   SOD_TRY(download(ctx, d2sq, ctx->cd2.p, n));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   return SOD_OK;
 }
 
@@ -1356,7 +1426,7 @@ int sod_match_candidates_merge(sod_ctx* ctx, int32_t nparts, const float* d1sq,
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
   SOD_TRY(launch_merge(ctx, ctx->gd1.p, ctx->gidx.p, ctx->gd2.p, nparts, (int64_t)n));
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, true));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
   return SOD_OK;
 }
@@ -1364,9 +1434,10 @@ int sod_match_candidates_merge(sod_ctx* ctx, int32_t nparts, const float* d1sq,
 int sod_hough_partial_get(sod_ctx* ctx, uint32_t* counts, uint32_t* first) {
   SOD_TRY(set_dev(ctx));
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
+  SOD_TRY(sod_hist_dense(ctx));
   SOD_TRY(download(ctx, counts, ctx->counts.p, (size_t)ctx->nbins));
   SOD_TRY(download(ctx, first, ctx->first.p, (size_t)ctx->nbins));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   return SOD_OK;
 }
 
@@ -1374,11 +1445,14 @@ int sod_hough_partial_set(sod_ctx* ctx, const uint32_t* counts, const uint32_t* 
   SOD_TRY(set_dev(ctx));
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
   if (!counts || !first) return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  SOD_TRY(sod_reserve(ctx, ctx->counts, (size_t)ctx->nbins));
+  SOD_TRY(sod_reserve(ctx, ctx->first, (size_t)ctx->nbins));
+  ctx->hist_dense = true;
   SOD_TRY(sod_stage_mark(ctx, kStageAllreduce, false));
   SOD_HIP(ctx, hipMemcpyAsync(ctx->counts.p, counts, ctx->nbins * 4, hipMemcpyHostToDevice, ctx->stream));
   SOD_HIP(ctx, hipMemcpyAsync(ctx->first.p, first, ctx->nbins * 4, hipMemcpyHostToDevice, ctx->stream));
   SOD_TRY(sod_stage_mark(ctx, kStageAllreduce, true));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->selected = ctx->affined = false;
   return SOD_OK;
 }

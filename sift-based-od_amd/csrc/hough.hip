@@ -29,6 +29,8 @@
 #include <cstdlib>
 #include <utility>
 
+#include <hip/hip_ext.h>
+
 #include "sod_internal.h"
 
 namespace {
@@ -861,6 +863,8 @@ constexpr int kSmallQ = 2048;
 // diagnostic build only: s_memrealtime (100 MHz) at the phase boundaries of the last 64 launches
 __device__ unsigned long long g_selst[64][5];
 __device__ unsigned int g_selst_n;
+__device__ unsigned long long g_fust[64][8];   // hough_small_kernel phase boundaries
+__device__ unsigned int g_fust_n;
 #define SEL_STAMP(i) \
   if (tid == 0) st[i] = __builtin_amdgcn_s_memrealtime();
 #else
@@ -1004,6 +1008,342 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
     g_selst[k][4] = (unsigned long long)V;
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------------------
+// One query image of <= kFusedQ queries in ONE work-group: pose + votes + valid bins + member
+// lists + the affine gather -- pose_kernel, hist_kernel, select_small_kernel and
+// affine_gather_kernel in one launch (main.py's own regime, one image of ~500 keypoints: those
+// four launches took ~37 us of a ~0.2 ms step, rocprofv3 r04 lat1).  Same outputs, bit for bit.
+//
+// No dense bin table.  Query q votes the 2x2x2x2 box above its base bin K(q), each vote kept
+// when every index is < bins -- a property of the bin, not of the query (vote_mask).  So the
+// votes of bin B come from the queries whose base key is B - e, e in {0,1}^4, and
+//   count(B) = sum_e n(B - e),   first(B) = min_e 16 q0(B - e) + slot(e)
+// (slot(e) = 8 e0 + 4 e1 + 2 e2 + e3; first = main.py:113-119's dict insertion ordinal, as
+// hist_kernel computes it), with n(K) / q0(K) = the number / the lowest index of the voting
+// queries whose base key is K: an LDS hash over at most kFusedQ distinct base keys, instead of
+// 98 304 bins (C3) that do not fit LDS.  A voting query then finds, for each of its votes, the
+// bin's count and first touch from 16 lookups; a vote that is its bin's first touch of a bin
+// with >= thr votes emits the bin (valid bins in first-touch order); members in query order as
+// select_small_kernel finds them (one wave per bin from its first touch), and the member's
+// model / query points for affine_kernel from LDS.
+constexpr int kFusedT = 1024;
+constexpr int kFusedQ = 1024;                   // one query per thread
+constexpr int kFusedHash = 2048;                // >= 2 slots per distinct base key
+constexpr uint32_t kNoKey = 0xFFFFFFFFu;        // indices are <= 254: never a base key
+
+__device__ __forceinline__ uint32_t key_hash(uint32_t k) {
+  return (k * 0x9E3779B1u) >> (32 - 11);        // log2(kFusedHash) = 11
+}
+
+// count and first-touch ordinal of vote slot sl of a query with base key `key`: bin B = key +
+// e(sl); its voters are the queries with base key B - e for the e in {0,1}^4 that keep every
+// index >= 0, each contributing n(B - e) votes, the first at ordinal 16 q0(B - e) + slot(e)
+__device__ __forceinline__ void bin_votes(uint32_t key, uint32_t sl, const uint32_t* hk,
+                                          const uint32_t* hn, const uint32_t* hq,
+                                          uint32_t* cnt_out, uint32_t* fst_out) {
+  const int bx = (int)(key & 0xFF) + (int)((sl >> 3) & 1), by = (int)((key >> 8) & 0xFF) + (int)((sl >> 2) & 1),
+            bt = (int)((key >> 16) & 0xFF) + (int)((sl >> 1) & 1), bs = (int)(key >> 24) + (int)(sl & 1);
+  uint32_t h[16], k2[16], kv[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {   // every first probe in flight at once
+    const int kx = bx - ((e >> 3) & 1), ky = by - ((e >> 2) & 1), kt = bt - ((e >> 1) & 1),
+              ks = bs - (e & 1);
+    k2[e] = (kx | ky | kt | ks) < 0 ? kNoKey
+                                     : (uint32_t)kx | ((uint32_t)ky << 8) | ((uint32_t)kt << 16) |
+                                           ((uint32_t)ks << 24);
+    h[e] = key_hash(k2[e]);
+    kv[e] = hk[h[e]];
+  }
+  uint32_t cnt = 0u, fst = 0xFFFFFFFFu;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    if (k2[e] == kNoKey) continue;
+    uint32_t hh = h[e], kk = kv[e];
+    while (kk != k2[e] && kk != kNoKey) {   // collision: linear probe
+      hh = (hh + 1) & (kFusedHash - 1);
+      kk = hk[hh];
+    }
+    if (kk == k2[e]) {
+      cnt += hn[hh];
+      fst = min(fst, hq[hh] * 16u + (uint32_t)e);
+    }
+  }
+  *cnt_out = cnt;
+  *fst_out = fst;
+}
+
+__global__ __launch_bounds__(kFusedT) void hough_small_kernel(
+    int64_t nq, const uint8_t* __restrict__ good, const int* __restrict__ idx1,
+    const float* __restrict__ qx, const float* __restrict__ qy, const float* __restrict__ qa,
+    const int* __restrict__ qo, const float* __restrict__ mx, const float* __restrict__ my,
+    const float* __restrict__ ma, const int* __restrict__ mo, const int* __restrict__ mimg,
+    const double* __restrict__ cent, const int* __restrict__ isize, int H, int W, Bins b,
+    const int* __restrict__ lut, uint32_t thr, double* __restrict__ pose,
+    uint32_t* __restrict__ basekey, uint32_t* __restrict__ vmask, int2* __restrict__ msize,
+    double* __restrict__ grec, uint32_t* __restrict__ gstat, uint32_t* __restrict__ vbin,
+    uint32_t* __restrict__ vcnt, uint32_t* __restrict__ vfirst, uint32_t* __restrict__ scal,
+    int64_t* __restrict__ voff, int32_t* __restrict__ members, float* __restrict__ amx,
+    float* __restrict__ amy, float* __restrict__ aqx, float* __restrict__ aqy,
+    int32_t* __restrict__ aisig) {
+  __shared__ uint32_t skey[kFusedQ], smask[kFusedQ];
+  __shared__ float smx[kFusedQ], smy[kFusedQ], sqx[kFusedQ], sqy[kFusedQ];
+  __shared__ uint32_t hk[kFusedHash], hn[kFusedHash], hq[kFusedHash];
+  __shared__ uint32_t vb_lb[kSmallV], vb_need[kSmallV], vb_first[kSmallV], vb_off[kSmallV];
+  __shared__ uint16_t vlist[kFusedQ];   // voting queries in order
+  __shared__ uint32_t vfm[kFusedQ];     // their valid-first-touch slot masks
+  __shared__ uint32_t vbase[kFusedQ];   // valid index of their first valid-first slot
+  __shared__ uint16_t vfc[kFusedQ * 16];   // vote count of each valid-first vote
+  __shared__ uint32_t sh[kFusedT / 64];
+  __shared__ uint32_t carry_s;
+  __shared__ int64_t carry64_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int kW = kFusedT / 64;
+#ifdef SOD_SEL_STAMP
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // [7]: emission start
+#define FU_STAMP(i) \
+  if (tid == 0) st[i] = __builtin_amdgcn_s_memrealtime();
+#else
+#define FU_STAMP(i)
+#endif
+  FU_STAMP(0)
+  for (int i = tid; i < kFusedHash; i += kFusedT) {
+    hk[i] = kNoKey;
+    hn[i] = 0u;
+    hq[i] = 0xFFFFFFFFu;
+  }
+  if (tid == 0) {
+    carry_s = 0;
+    carry64_s = 0;
+  }
+  __syncthreads();
+  // 1. pose + base key + vote mask per query (pose_kernel); the voting queries' base keys
+  //    into the hash (count, lowest query)
+  for (int64_t q = tid; q < nq; q += kFusedT) {
+    uint32_t key = 0u, mask = 0u;
+    float fmx = 0.f, fmy = 0.f;
+    const bool g = good[q] != 0;
+    const float fqx = qx[q], fqy = qy[q];
+    if (g) {
+      const int m = idx1[q];
+      const int im = mimg[m];
+      double p[4], t[2];
+      int ix[4];
+      fmx = mx[m];
+      fmy = my[m];
+      pose_bins(fmx, fmy, ma[m], mo[m], fqx, fqy, qa[q], qo[q], cent[2 * im], cent[2 * im + 1],
+                H, W, b, lut, p, ix, t);
+      if (guard_flag(p, t, fqx, fqy, H, W, b)) guard_push(grec, gstat, q, p, t, fqx, fqy, H, W);
+      pose[4 * q + 0] = p[0];
+      pose[4 * q + 1] = p[1];
+      pose[4 * q + 2] = p[2];
+      pose[4 * q + 3] = p[3];
+      msize[q] = make_int2(isize[2 * im], isize[2 * im + 1]);
+      key = (uint32_t)ix[0] | ((uint32_t)ix[1] << 8) | ((uint32_t)ix[2] << 16) |
+            ((uint32_t)ix[3] << 24);
+      mask = vote_mask(ix, b);   // one rank: every match's DB row is this shard's
+      basekey[q] = key;
+    }
+    vmask[q] = mask ? (mask | 0x10000u) : 0u;
+    skey[q] = key;
+    smask[q] = mask;
+    smx[q] = fmx;
+    smy[q] = fmy;
+    sqx[q] = fqx;
+    sqy[q] = fqy;
+    if (mask) {
+      for (uint32_t h = key_hash(key);; h = (h + 1) & (kFusedHash - 1)) {
+        const uint32_t old = atomicCAS(&hk[h], kNoKey, key);
+        if (old == kNoKey || old == key) {
+          atomicAdd(&hn[h], 1u);
+          atomicMin(&hq[h], (uint32_t)q);
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  FU_STAMP(1)
+  // the voting queries, in query order (the votes' ordinals follow it)
+  for (int64_t q0 = 0; q0 < nq; q0 += kFusedT) {
+    const int64_t q = q0 + tid;
+    const bool vote = q < nq && smask[q] != 0u;
+    const uint64_t bal = __ballot(vote);
+    if (lane == 0) sh[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t off = carry_s, tot = 0;
+    for (int i = 0; i < kW; ++i) {
+      if (i < w) off += sh[i];
+      tot += sh[i];
+    }
+    if (vote) {
+      const uint32_t pos = off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      vlist[pos] = (uint16_t)q;
+      vfm[pos] = 0u;
+    }
+    __syncthreads();
+    if (tid == 0) carry_s += tot;
+    __syncthreads();
+  }
+  const uint32_t nv = carry_s;
+  __syncthreads();
+  FU_STAMP(2)
+  if (tid == 0) carry_s = 0;
+  // 2. one thread per vote (voting query i, slot s): its bin's count and first touch from 16
+  //    hash lookups; the first touch of a bin with >= thr votes sets bit s of vfm[i]
+  for (uint32_t it = tid; it < nv * 16u; it += kFusedT) {
+    const uint32_t i = it >> 4, sl = it & 15u;
+    const uint32_t q = vlist[i];
+    const uint32_t m = smask[q];
+    if (!((m >> sl) & 1u)) continue;
+    const uint32_t key = skey[q];
+    uint32_t cnt, fst;
+    bin_votes(key, sl, hk, hn, hq, &cnt, &fst);
+    if (cnt >= thr && fst == q * 16u + sl) {
+      atomicOr(&vfm[i], 1u << sl);
+      vfc[it] = (uint16_t)cnt;   // <= voting queries <= kFusedQ
+    }
+  }
+  __syncthreads();
+  FU_STAMP(3)
+  // valid bins in first-touch order (voting query, then slot): the first valid index of each
+  // voting query = the scan of the masks' popcounts (nv <= kFusedT: one round) ...
+  {
+    const uint32_t i = tid;
+    const uint32_t fm = i < nv ? vfm[i] : 0u;
+    const uint32_t n = (uint32_t)__popc(fm);
+    uint32_t x = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int k = 0; k < kW; ++k) {
+      if (k < w) off += sh[k];
+      tot += sh[k];
+    }
+    if (i < nv) vbase[i] = off + x - n;
+    if (tid == 0) carry_s = tot;
+    FU_STAMP(7)
+  }
+  __syncthreads();
+  // ... and every valid-first vote writes its bin there, one thread per vote
+  for (uint32_t it = tid; it < nv * 16u; it += kFusedT) {
+    const uint32_t i = it >> 4, sl = it & 15u;
+    const uint32_t fm = vfm[i];
+    if (!((fm >> sl) & 1u)) continue;
+    const uint32_t v = vbase[i] + (uint32_t)__popc(fm & ((1u << sl) - 1u));
+    const uint32_t key = skey[vlist[i]];
+    const uint32_t lb = lin_bin((int)(key & 0xFF) + (int)((sl >> 3) & 1),
+                                (int)((key >> 8) & 0xFF) + (int)((sl >> 2) & 1),
+                                (int)((key >> 16) & 0xFF) + (int)((sl >> 1) & 1),
+                                (int)(key >> 24) + (int)(sl & 1), b);
+    const uint32_t cnt = vfc[it];
+    vbin[v] = lb;
+    aisig[v] = (int32_t)(lb % (uint32_t)b.s);   // affine_gather_kernel's i_sigma
+    if (v < (uint32_t)kSmallV) {
+      vb_lb[v] = lb;
+      vb_need[v] = cnt;
+      vb_first[v] = i;   // the bin's first voting query (its index in vlist)
+    } else {
+      vcnt[v] = cnt;
+      vfirst[v] = i;
+    }
+  }
+  __syncthreads();
+  const int64_t V = carry_s;
+  FU_STAMP(4)
+  // 3. member offsets (exclusive scan of the counts, in valid order)
+  for (int64_t v0 = 0; v0 < V; v0 += kFusedT) {
+    const int64_t v = v0 + tid;
+    uint32_t c = 0u;
+    if (v < V)
+      c = v < kSmallV ? vb_need[v]
+                      : __hip_atomic_load(&vcnt[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int i = 0; i < kW; ++i) {
+      if (i < w) off += sh[i];
+      tot += sh[i];
+    }
+    const int64_t base = carry64_s;
+    if (v < V) {
+      voff[v] = base + off + x - c;
+      if (v < kSmallV) vb_off[v] = (uint32_t)(base + off + x - c);   // < 16 * kFusedQ
+    }
+    __syncthreads();
+    if (tid == 0) carry64_s = base + tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    scal[0] = (uint32_t)V;
+    scal[1] = (uint32_t)carry64_s;
+    voff[V] = carry64_s;
+  }
+  __syncthreads();   // voff (global) past the LDS copy is read by other waves below
+  FU_STAMP(5)
+  // 4. members in query order, one wave per bin from its first voting query, with the affine
+  //    inputs of each member
+  for (int64_t v = w; v < V; v += kW) {
+    const bool lds_v = v < kSmallV;
+    const uint32_t lb = lds_v ? vb_lb[v] : __hip_atomic_load(&vbin[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t need = lds_v ? vb_need[v] : __hip_atomic_load(&vcnt[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t off = lds_v ? (int64_t)vb_off[v]
+                              : __hip_atomic_load(&voff[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int jf = (int)(lds_v ? vb_first[v]
+                               : __hip_atomic_load(&vfirst[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const int bs_ = lb % b.s, bt_ = (lb / b.s) % b.t, by_ = (lb / (b.s * b.t)) % b.y,
+              bx_ = lb / (b.s * b.t * b.y);
+    uint32_t got = 0;
+    const int jn = (int)nv;
+    // over the voting queries only (in query order), from the bin's first one
+    for (int j0 = jf; got < need && j0 < jn; j0 += 64) {
+      const int j = j0 + lane;
+      const int q = vlist[min(j, jn - 1)];
+      const uint32_t mm = smask[q], key = skey[q];
+      const uint32_t dx = (uint32_t)(bx_ - (int)(key & 0xFF)), dy = (uint32_t)(by_ - (int)((key >> 8) & 0xFF)),
+                     dt = (uint32_t)(bt_ - (int)((key >> 16) & 0xFF)), ds = (uint32_t)(bs_ - (int)(key >> 24));
+      const bool win = (dx | dy | dt | ds) <= 1u;
+      const bool mem = (j < jn) & win & (((mm >> ((dx * 8 + dy * 4 + dt * 2 + ds) & 15u)) & 1u) != 0u);
+      const uint64_t bal = __ballot(mem);
+      if (mem) {
+        const int64_t jj = off + got + __popcll(bal & ((1ull << lane) - 1ull));
+        members[jj] = (int32_t)q;
+        amx[jj] = smx[q];
+        amy[jj] = smy[q];
+        aqx[jj] = sqx[q];
+        aqy[jj] = sqy[q];
+      }
+      got += __popcll(bal);
+    }
+  }
+  // 5. the guard records listed above: their count to the slot the host reads, and the append
+  //    counter back to 0 for the next launch (hist_kernel's handover)
+  __syncthreads();
+  FU_STAMP(6)
+  if (tid == 0) {
+    const uint32_t g = __hip_atomic_load(&gstat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gstat[1] = g;
+    gstat[0] = 0u;
+  }
+#ifdef SOD_SEL_STAMP
+  if (tid == 0) {
+    const unsigned k = atomicAdd(&g_fust_n, 1u) % 64u;
+    for (int i = 0; i < 8; ++i) g_fust[k][i] = st[i];
+  }
+#endif
+#undef FU_STAMP
 }
 
 // PoseBin running means in vote order (PoseBin.py:19-43).  The recurrence
@@ -1332,7 +1672,7 @@ int sod_build_sigma_lut(sod_ctx* ctx, int32_t bs) {
   SOD_TRY(sod_reserve(ctx, ctx->sig_lut, kSigmaLutSize));
   SOD_HIP(ctx, hipMemcpyAsync(ctx->sig_lut.p, lut, sizeof(lut), hipMemcpyHostToDevice, ctx->stream));
   // the host array dies with this frame: make the copy complete before returning
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   return SOD_OK;
 }
 
@@ -1401,7 +1741,7 @@ static int launch_hist(sod_ctx* ctx) {
     SOD_TRY(sod_reserve(ctx, ctx->hist_rng, r.size()));
     SOD_HIP(ctx, hipMemcpyAsync(ctx->hist_rng.p, r.data(), r.size() * 4, hipMemcpyHostToDevice,
                                 ctx->stream));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));   // r is a host temporary
+    SOD_HIP(ctx, sod_stream_sync(ctx->stream));   // r is a host temporary
     grid.x = (unsigned)span;
     rng = ctx->hist_rng.p;
   }
@@ -1448,6 +1788,7 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(launch_hist(ctx));
   ctx->guard_done = false;
+  ctx->hist_dense = true;
   return SOD_OK;
 }
 
@@ -1466,13 +1807,13 @@ void sod_guard_host_pose(const double r[8], const int32_t bins[4], double* x, do
 
 int sod_guard_resolve(sod_ctx* ctx) {
   if (ctx->guard_done || !ctx->houghed) return SOD_OK;
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   // every copy here is ordered on the context stream and waited for on it: a null-stream copy
   // would also wait for the matcher stream (CU-masked streams are blocking streams), i.e. for
   // the next step's matcher when the caller reads step N while step N+1 is in flight
   uint32_t n = 0;
   SOD_HIP(ctx, hipMemcpyAsync(&n, ctx->gstat.p + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->guard_flagged = n;
   ctx->guard_patched = 0;
   ctx->guard_flagged_total += n;
@@ -1487,7 +1828,7 @@ int sod_guard_resolve(sod_ctx* ctx) {
                               ctx->stream));
   SOD_HIP(ctx, hipMemcpyAsync(key.data(), ctx->basekey.p, key.size() * 4, hipMemcpyDeviceToHost,
                               ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   std::vector<int32_t> pq(n);
   std::vector<uint32_t> pkey(n);
   std::vector<double> pxy(2 * (size_t)n);
@@ -1527,11 +1868,14 @@ int sod_guard_resolve(sod_ctx* ctx) {
     hipLaunchKernelGGL(own_all_kernel, dim3((unsigned)std::min<int64_t>(cdiv(nq, 256), 1024)),
                        dim3(256), 0, ctx->stream, nq, ctx->vmask.p);
     if (hipGetLastError() != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, "own_all_kernel launch");
+    if (rc == SOD_OK) rc = sod_reserve(ctx, ctx->counts, (size_t)ctx->nbins);
+    if (rc == SOD_OK) rc = sod_reserve(ctx, ctx->first, (size_t)ctx->nbins);
     if (rc == SOD_OK &&
         (hipMemsetAsync(ctx->counts.p, 0, (size_t)ctx->nbins * 4, ctx->stream) != hipSuccess ||
          hipMemsetAsync(ctx->first.p, 0xFF, (size_t)ctx->nbins * 4, ctx->stream) != hipSuccess))
       rc = sod_fail(ctx, SOD_EHIP, "guard histogram reset failed");
     if (rc == SOD_OK) rc = launch_hist(ctx);
+    if (rc == SOD_OK) ctx->hist_dense = true;
     if (rc == SOD_OK && ctx->selected) rc = launch_select(ctx, ctx->vote_thr);
     if (rc == SOD_OK && ctx->affined) rc = launch_affine_gather(ctx);
     if (rc == SOD_OK && ctx->affined)
@@ -1540,9 +1884,9 @@ int sod_guard_resolve(sod_ctx* ctx) {
                          ctx->aff_xf, ctx->aff_yf, ctx->aff_thr, 1 << 30, nullptr, ctx->surv.p,
                          ctx->fvotes.p, ctx->params.p, ctx->alive.p, ctx->scal.p);
   }
-  if (rc == SOD_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+  if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
     rc = sod_fail(ctx, SOD_EHIP, "guard re-run failed");
-  (void)hipStreamSynchronize(ctx->stream);
+  (void)sod_stream_sync(ctx->stream);
   sod_release(dq);
   sod_release(dk);
   sod_release(dxy);
@@ -1583,7 +1927,7 @@ static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* t
 }
 
 static int launch_members_multi(sod_ctx* ctx, uint32_t thr, int64_t nq);
-static int launch_means(sod_ctx* ctx);
+static int launch_means(sod_ctx* ctx, bool on_main = false);
 // SOD_SELECT_MULTI=1: small windows take the multi-kernel path too (parity tests of both)
 static bool select_multi_forced() {
   const char* e = std::getenv("SOD_SELECT_MULTI");
@@ -1597,6 +1941,7 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
   std::swap(ctx->members, ctx->members_b);
   std::swap(ctx->means, ctx->means_b);
   SOD_TRY(next_parity(ctx, ctx->spar, ctx->ev_sread, ctx->sread_id));
+  ctx->gathered = false;
   if (thr < 1) thr = 1;  // a bin exists only once voted for
   ctx->vmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * nq));
   ctx->mmax = std::max<int64_t>(1, 16 * nq);
@@ -1610,11 +1955,13 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
     SOD_TRY(sod_reserve(ctx, ctx->vidx, (size_t)ctx->nbins));
     SOD_HIP(ctx, hipMemsetAsync(ctx->vidx.p, 0xFF, ctx->vidx.n * 4, ctx->stream));
   }
+  // the last kernel of the selection records ev_fork (the PoseBin means' start on the side
+  // stream) in its own dispatch: a marker packet after it cost the stream a ~8 us gap
   if (nq <= kSmallQ && !select_multi_forced()) {   // one work-group, one launch
-    hipLaunchKernelGGL(select_small_kernel, dim3(1), dim3(kSmallT), 0, ctx->stream, nq,
-                       ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
-                       qimg_p(ctx), ctx->nbins1, (uint32_t)thr, ctx->vbin.p, ctx->scal.p,
-                       ctx->voff.p, ctx->members.p);
+    hipExtLaunchKernelGGL(select_small_kernel, dim3(1), dim3(kSmallT), 0, ctx->stream, nullptr,
+                          ctx->ev_fork, 0, nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p,
+                          ctx->first.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, (uint32_t)thr,
+                          ctx->vbin.p, ctx->scal.p, ctx->voff.p, ctx->members.p);
     SOD_HIP(ctx, hipGetLastError());
   } else {
     SOD_TRY(launch_members_multi(ctx, (uint32_t)thr, nq));
@@ -1637,20 +1984,23 @@ static int launch_members_multi(sod_ctx* ctx, uint32_t thr, int64_t nq) {
                      0, ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, ctx->vidx.p,
                      ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->tail_cus() * 2)), dim3(kOrderT), 0,
-                     ctx->stream, ctx->scal.p, ctx->voff.p, nq, ctx->members.p);
+  const bool rebuild = nq > kBitQ;   // beyond the LDS bitmap of member_order_kernel only
+  hipExtLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->tail_cus() * 2)), dim3(kOrderT),
+                        0, ctx->stream, nullptr, rebuild ? nullptr : ctx->ev_fork, 0, ctx->scal.p,
+                        ctx->voff.p, nq, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  if (nq > kBitQ) {   // beyond the LDS bitmap of member_order_kernel only (a no-op otherwise)
+  if (rebuild) {
     const int wg = std::max(1, ctx->tail_cus() * 4);
-    hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
-                       ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
-                       ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->members.p);
+    hipExtLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nullptr,
+                          ctx->ev_fork, 0, nq, ctx->scal.p, ctx->vbin.p, ctx->voff.p,
+                          ctx->counts.p, ctx->first.p, ctx->basekey.p, ctx->vmask.p,
+                          ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->members.p);
     SOD_HIP(ctx, hipGetLastError());
   }
   return SOD_OK;
 }
 
-static int launch_means(sod_ctx* ctx) {
+static int launch_means(sod_ctx* ctx, bool on_main) {
   // PoseBin means depend only on the member lists: they run on the side stream, beside the
   // affine verification and the next step's matcher tail (their inputs are double-buffered);
   // entry points that read results join them (set_dev)
@@ -1658,7 +2008,25 @@ static int launch_means(sod_ctx* ctx) {
   // (a bin's chain reads entry n for its member n)
   const bool new_rtab = ctx->rtab.n < (size_t)ctx->mmax;
   SOD_TRY(sod_reserve(ctx, ctx->rtab, (size_t)ctx->mmax));
-  SOD_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+  if (on_main) {
+    // the fused one-image path: on the context stream, no fork / join events (an event on a
+    // dispatch delays the next kernel ~5 us, about what these means take at this size); the
+    // buffers it reads are then ordered before every later writer by the stream itself
+    if (new_rtab) {
+      hipLaunchKernelGGL(recip_table_kernel, dim3((unsigned)std::min<int64_t>(cdiv(ctx->rtab.n, 256), 4096)),
+                         dim3(256), 0, ctx->stream, (int64_t)ctx->rtab.n, ctx->rtab.p);
+      SOD_HIP(ctx, hipGetLastError());
+    }
+    hipLaunchKernelGGL(means_kernel, dim3(std::max(1, ctx->tail_cus() * 11)), dim3(64), 0,
+                       ctx->stream, ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->pose.p,
+                       reinterpret_cast<const int2*>(ctx->msize.p), ctx->rtab.p, ctx->means.p);
+    SOD_HIP(ctx, hipGetLastError());
+    ++ctx->means_id;
+    ctx->hread_id[ctx->hpar] = 0;   // nothing to wait for: stream order
+    ctx->sread_id[ctx->spar] = 0;
+    return SOD_OK;
+  }
+  // ev_fork: recorded by the selection's last dispatch (launch_select)
   SOD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
   if (new_rtab) {
     hipLaunchKernelGGL(recip_table_kernel, dim3((unsigned)std::min<int64_t>(cdiv(ctx->rtab.n, 256), 4096)),
@@ -1676,6 +2044,81 @@ static int launch_means(sod_ctx* ctx) {
   SOD_TRY(mark_read(ctx, ctx->side, ctx->spar, ctx->ev_sread, ctx->sread_id));
   SOD_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
   ctx->side_pending = true;
+  return SOD_OK;
+}
+
+// The fused one-image path (hough_small_kernel): what launch_hough + launch_select +
+// launch_affine_gather do for a window of <= kFusedQ queries of one image on one rank, in one
+// launch; the dense histogram is built only if something reads it (sod_hist_dense).
+bool sod_hough_small_ok(const sod_ctx* ctx) {
+  if (const char* e = std::getenv("SOD_HOUGH_FUSED"))
+    if (e[0] == '0') return false;
+  return ctx->nranks <= 1 && !ctx->comm && ctx->n_qimg == 0 && sod_win_n(ctx) <= kFusedQ &&
+         sod_win_n(ctx) >= 1;
+}
+
+int launch_hough_small(sod_ctx* ctx, int32_t thr) {
+  const int64_t nq = sod_win_n(ctx), q0 = sod_win0(ctx);
+  // launch_hough's buffers (pose / model sizes alternate per step, see next_parity)
+  std::swap(ctx->pose, ctx->pose_b);
+  std::swap(ctx->msize, ctx->msize_b);
+  SOD_TRY(next_parity(ctx, ctx->hpar, ctx->ev_hread, ctx->hread_id));
+  SOD_TRY(sod_reserve(ctx, ctx->pose, (size_t)nq * 4));
+  SOD_TRY(sod_reserve(ctx, ctx->basekey, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->vmask, (size_t)nq));
+  SOD_TRY(sod_reserve(ctx, ctx->msize, (size_t)nq * 2));
+  SOD_TRY(guard_reserve(ctx, nq));
+  // launch_select's
+  std::swap(ctx->scal, ctx->scal_b);
+  std::swap(ctx->voff, ctx->voff_b);
+  std::swap(ctx->members, ctx->members_b);
+  std::swap(ctx->means, ctx->means_b);
+  SOD_TRY(next_parity(ctx, ctx->spar, ctx->ev_sread, ctx->sread_id));
+  if (thr < 1) thr = 1;
+  ctx->vmax = std::max<int64_t>(1, std::min<int64_t>(ctx->nbins, 16 * nq));
+  ctx->mmax = std::max<int64_t>(1, 16 * nq);
+  SOD_TRY(sod_reserve(ctx, ctx->scal, 4));
+  SOD_TRY(sod_reserve(ctx, ctx->vbin, (size_t)ctx->vmax));
+  SOD_TRY(sod_reserve(ctx, ctx->voff, (size_t)ctx->vmax + 1));
+  SOD_TRY(sod_reserve(ctx, ctx->members, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->means, (size_t)ctx->vmax * 6));
+  SOD_TRY(sod_reserve(ctx, ctx->cursor, (size_t)ctx->vmax));   // counts past the LDS copy
+  SOD_TRY(sod_reserve(ctx, ctx->vfirst_s, (size_t)ctx->vmax)); // first queries past it
+  // launch_affine_gather's
+  SOD_TRY(sod_reserve(ctx, ctx->amx, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->amy, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->aqx, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->aqy, (size_t)ctx->mmax));
+  SOD_TRY(sod_reserve(ctx, ctx->aisig, (size_t)ctx->vmax));
+  hipLaunchKernelGGL(hough_small_kernel, dim3(1), dim3(kFusedT), 0, ctx->stream, nq,
+                        ctx->good.p + q0, ctx->idx1.p + q0, ctx->qx.p + q0, ctx->qy.p + q0, ctx->qang.p + q0, ctx->qoct.p + q0, ctx->mx.p, ctx->my.p,
+                        ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p, ctx->isize.p, ctx->qh,
+                        ctx->qw, ctx_bins(ctx), ctx->sig_lut.p, (uint32_t)thr, ctx->pose.p,
+                        ctx->basekey.p, ctx->vmask.p, reinterpret_cast<int2*>(ctx->msize.p),
+                        ctx->grec.p, ctx->gstat.p, ctx->vbin.p, ctx->cursor.p, ctx->vfirst_s.p,
+                        ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->amx.p, ctx->amy.p,
+                        ctx->aqx.p, ctx->aqy.p, ctx->aisig.p);
+  SOD_HIP(ctx, hipGetLastError());
+  ctx->guard_done = false;
+  ctx->hist_dense = false;
+  ctx->gathered = true;
+  return launch_means(ctx, true);
+}
+
+// the dense histogram (counts / first touch of every bin) after the fused path, for the
+// readers that need it: all bins, another vote threshold, the host exchange
+int sod_hist_dense(sod_ctx* ctx) {
+  if (ctx->hist_dense) return SOD_OK;
+  // the guard reads the record count the fused kernel handed over; hist_kernel hands over
+  // again (0 records), so resolve first (a changed bin builds the dense table itself)
+  SOD_TRY(sod_guard_resolve(ctx));
+  if (ctx->hist_dense) return SOD_OK;
+  SOD_TRY(sod_reserve(ctx, ctx->counts, (size_t)ctx->nbins));
+  SOD_TRY(sod_reserve(ctx, ctx->first, (size_t)ctx->nbins));
+  SOD_HIP(ctx, hipMemsetAsync(ctx->counts.p, 0, (size_t)ctx->nbins * 4, ctx->stream));
+  SOD_HIP(ctx, hipMemsetAsync(ctx->first.p, 0xFF, (size_t)ctx->nbins * 4, ctx->stream));
+  SOD_TRY(launch_hist(ctx));
+  ctx->hist_dense = true;
   return SOD_OK;
 }
 
@@ -1718,5 +2161,8 @@ int launch_affine(sod_ctx* ctx, int64_t nb_host, bool count_on_device, const int
 #ifdef SOD_SEL_STAMP
 extern "C" int sod_debug_selstamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_selst), sizeof(g_selst)) == hipSuccess ? 0 : 1;
+}
+extern "C" int sod_debug_fusedstamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fust), sizeof(g_fust)) == hipSuccess ? 0 : 1;
 }
 #endif

@@ -235,9 +235,6 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
 #ifndef SOD_I8_XCD
 #define SOD_I8_XCD 1       // XCD-aware work-group -> (chunk, query block) order
 #endif
-#ifndef SOD_I8_EXP
-#define SOD_I8_EXP 0       // timing experiments only (wrong results): 1 no refill DMA,
-#endif                     // 2 no prefilter, 4 no stage wait/barrier
 #ifndef SOD_I8_SLOTS
 #define SOD_I8_SLOTS 1     // shared bound from the best rows of the even / odd DB chunks
 #endif
@@ -378,31 +375,6 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
                                             int (&id)[QT], bool early = false, int mode = 0,
                                             bool vmem = false) {
-#if SOD_I8_EXP & 8
-  // timing bound only: one flat max over the lane's 4*QT values (v_max3 tree) + ONE compare
-  // per subtile, the cost of a prefilter whose thresholds live in C; cheap slow body
-  {
-    int v[4 * QT];
-#pragma unroll
-    for (int t = 0; t < QT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[4 * t + r] = acc[t][r];
-    const int vmax = MaxTree<4 * QT>::f(v);
-    const uint64_t h = __builtin_amdgcn_ballot_w64(vmax >= t2[0]);
-#if SOD_I8_SGB
-    constexpr int nv = 2 * QT + 1;
-#pragma unroll
-    for (int i = 0; i < 2 * QT; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-      if (2 * i < nv) __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);
-      if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-    }
-#endif
-    if (__builtin_expect(h != 0, 0)) t2[0] = max(t2[0], vmax);
-    return;
-  }
-#endif
   uint64_t hit[QT];
   uint64_t any = 0;
 #pragma unroll
@@ -596,18 +568,17 @@ __device__ __forceinline__ void match_unit(
     // the wave's loads of stage s are complete when at most the later prefetched stages'
     // loads remain in flight (vector memory returns in order)
     const int64_t younger = min<int64_t>(kRing - 2, nst - 1 - s);   // stages issued after s
-    if (SOD_I8_EXP & 4) {
-    } else if (kRing >= 4 && younger >= 2)
+    if (kRing >= 4 && younger >= 2)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kLoadsPerStage) : "memory");
     else if (kRing >= 3 && younger >= 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLoadsPerStage) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!(SOD_I8_EXP & 4)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     // every wave has finished stage s-1, so its slot takes stage s+kRing-1
 #if SOD_I8_DMA
     // (descriptor pieces spread over this stage's first subtiles below; norms now)
-    if (!(SOD_I8_EXP & 1) && s + 1 < nst)
+    if (s + 1 < nst)
       issue_norms<NW16, kStageRows>(dn, npad, (s_lo + (s + 1) * SPS) * kSubRows,
                                     nring + ((s + 1) % kNormRing) * kStageNorm, wave, lane);
     // the last stage re-reads itself into the free slot (never read again): the pieces stay
@@ -617,7 +588,7 @@ __device__ __forceinline__ void match_unit(
     const uint32_t refill_off =
         (uint32_t)(min<int64_t>(s + 1, nst - 1) * kStageBytes + wv * kPiecesPerWave * 1024);
 #else
-    if (!(SOD_I8_EXP & 1) && s + kRing - 1 < nst) {
+    if (s + kRing - 1 < nst) {
       const int ns = slot == 0 ? kRing - 1 : slot - 1;
       issue_stage(dbpack, dn, npad, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageBytes,
                   nring + ((s + kRing - 1) % kNormRing) * kStageNorm, wave, lane);
@@ -734,7 +705,7 @@ __device__ __forceinline__ void match_unit(
 #if SOD_I8_DMA
       // piece u of the next stage (wave-uniform branch; u is a constant after unrolling)
       const bool piece_here = u < kPiecesPerWave;
-      if (piece_here && !(SOD_I8_EXP & 1))
+      if (piece_here)
         issue_piece(rs, refill + u * 1024, refill_off + u * 1024, lane);
 #else
       const bool piece_here = false;
@@ -752,16 +723,7 @@ __device__ __forceinline__ void match_unit(
       for (int t = 0; t < QT; ++t)
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq[t][1], acc[t], 0, 0, 0);
       const int rowb = rowl + (int)((s * SPS + u) * kSubRows);
-#if SOD_I8_EXP & 2
-#pragma unroll
-      for (int t = 0; t < QT; ++t) y1[t] = max(y1[t], acc[t][(u & 3)]);
-#pragma unroll
-      for (int i = 0; i < 2 * QT; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-        if (i < QT / 2) __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);
-        if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-#elif SOD_I8_PIPE
+#if SOD_I8_PIPE
       {
         // the pending subtile's index in the chunk decides dense / final / prefilter
         const int64_t kp = s * SPS + u - 1;
@@ -1359,8 +1321,8 @@ int launch_match_i8(sod_ctx* ctx) {
     const int64_t gslot = kThrWords * nq_pad;   // words of one slot
     if (ctx->gthr.n < (size_t)(2 * gslot) || ctx->gthr_n != nq_pad) {
       if (ctx->gthr.n < (size_t)(2 * gslot)) {
-        SOD_HIP(ctx, hipStreamSynchronize(ctx->mstream));
-        SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+        SOD_HIP(ctx, sod_stream_sync(ctx->stream));
         SOD_TRY(sod_reserve(ctx, ctx->gthr, (size_t)(2 * gslot)));
       }
       SOD_HIP(ctx, hipMemsetAsync(ctx->gthr.p, 0x80, (size_t)(2 * gslot) * 4, ks));
@@ -1398,7 +1360,7 @@ int launch_match_i8(sod_ctx* ctx) {
   SOD_TRY(sod_match_stream_end(ctx, ee));
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
   SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, gthr,
-                       ctx->nranks <= 1 && !ctx->comm));   // no exchange follows: final
+                       ctx->nranks <= 1 && !ctx->comm, sod_merge_done_event(ctx)));   // no exchange follows: final
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, true));
-  return sod_partials_merged(ctx);   // the slot is free again
+  return SOD_OK;   // the slot is free again once ev_merged[pslot] (the merge's dispatch) fires
 }

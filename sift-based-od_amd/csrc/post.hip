@@ -117,7 +117,7 @@ int run_post(sod_ctx* ctx, int32_t n, const double* means_host, const int32_t* i
       e = hipMemcpyAsync(pos.data(), dpos.p, pos.size() * 8, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(ori.data(), dori.p, ori.size() * 8, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = sod_stream_sync(ctx->stream);
     if (e != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, std::string("post-processing: ") + hipGetErrorString(e));
   }
   if (rc != SOD_OK) return rc;
@@ -251,14 +251,14 @@ int sod_postprocess(sod_ctx* ctx, int32_t* n_bins, int32_t* bin_index, int32_t* 
     if (ctx->affined)   // main.py:155: post_process runs on the bins that survived
       SOD_HIP(ctx, hipMemcpyAsync(surv.data(), ctx->surv.p, (size_t)V, hipMemcpyDeviceToHost,
                                   ctx->stream));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   }
   std::vector<uint32_t> lin;
   if (ctx->n_qimg && V) {   // batch of query images: post-process each image's bins apart
     lin.resize((size_t)V);
     SOD_HIP(ctx, hipMemcpyAsync(lin.data(), ctx->vbin.p, (size_t)V * 4, hipMemcpyDeviceToHost,
                                 ctx->stream));
-    SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   }
   std::vector<double> sel;
   std::vector<int32_t> idx, img;

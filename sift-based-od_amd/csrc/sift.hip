@@ -41,9 +41,6 @@ namespace {
 #else
 #define SOD_SIFT_WAVE_ORDER_ARCH 0
 #endif
-#ifndef SOD_SIFT_EXP
-#define SOD_SIFT_EXP 0   // timing experiments only (wrong results): 1 no descriptor adds,
-#endif                   // 2 no orientation adds, 4 no small-octave extrema
 constexpr int kBorder = 5;              // SIFT_IMG_BORDER
 constexpr int kMaxInterp = 5;           // SIFT_MAX_INTERP_STEPS
 constexpr int kOriBins = 36;            // SIFT_ORI_HIST_BINS
@@ -573,7 +570,6 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
       cur = nxt;
       nxt = t2;
     }
-    if (SOD_SIFT_EXP & 4) continue;
     // extrema of this octave (extrema_all_kernel's test) on the LDS DoG layers
     const int iw = w - 2 * kBorder, ih = h - 2 * kBorder;
     if (iw > 0 && ih > 0) {
@@ -851,11 +847,11 @@ __global__ __launch_bounds__(kOT) void orient_kernel(const float* __restrict__ g
       // tools/lds_atomic_order.hip, 2000 order-sensitive trials; checked again per context by
       // lds_order_probe_kernel), and the instructions of a wave in program order -- so every
       // bin still sums in OpenCV's sample order
-      if (tid < 64 && !(SOD_SIFT_EXP & 2)) {
+      if (tid < 64) {
         for (int t0 = 0; t0 < nv; t0 += 64)
           if (t0 + tid < nv) atomicAdd(&temphist[sbin[t0 + tid]], sval[t0 + tid]);
       }
-      } else if (tid == 0 && !(SOD_SIFT_EXP & 2)) {
+      } else if (tid == 0) {
         for (int t0 = 0; t0 < nv; t0 += 16) {
           int4 b4[4];
           float4 v4[4];
@@ -1295,10 +1291,7 @@ __global__ __launch_bounds__(kDT) void descriptor_kernel(const float* __restrict
               const int bn = sidx[pb][sg][tn] + offe;
               const float vn = svalT[pb][sg][e][tn];
               if (t0 + s8 < n && inner_bin(b)) {
-                if (SOD_SIFT_EXP & 1)   // timing build: a plain store (wrong sums)
-                  hist[b] = v;
-                else
-                  atomicAdd(&hist[b], v);
+                atomicAdd(&hist[b], v);
               }
               b = bn;
               v = vn;
@@ -1462,7 +1455,7 @@ struct SiftWork {
 };
 
 static void free_slot(SiftSlot* S) {
-  if (S->stream) (void)hipStreamSynchronize(S->stream);
+  if (S->stream) (void)sod_stream_sync(S->stream);
   sod_release(S->gray);
   sod_release(S->bgr);
   sod_release(S->gauss);
@@ -1480,7 +1473,7 @@ static void free_slot(SiftSlot* S) {
   sod_release(S->rdesc);
   sod_release(S->src);
   if (S->hcnt) (void)hipHostFree(S->hcnt);
-  if (S->side) (void)hipStreamSynchronize(S->side);
+  if (S->side) (void)sod_stream_sync(S->side);
   if (S->fork) (void)hipEventDestroy(S->fork);
   if (S->join) (void)hipEventDestroy(S->join);
   if (S->side) (void)hipStreamDestroy(S->side);
@@ -1575,7 +1568,7 @@ int lds_order_probe(sod_ctx* ctx, int* ok) {
                        dout.p, kTrials);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(o.data(), dout.p, o.size() * 4, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess)
+        sod_stream_sync(ctx->stream) != hipSuccess)
       rc = sod_fail(ctx, SOD_EHIP, "lds order probe failed");
   }
   sod_release(dv);
@@ -1625,7 +1618,7 @@ int set_kernels(sod_ctx* ctx, SiftWork& W) {
   SOD_TRY(sod_reserve(ctx, W.rad, (size_t)kMaxLayers));
   SOD_HIP(ctx, hipMemcpyAsync(W.kern.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
   SOD_HIP(ctx, hipMemcpyAsync(W.rad.p, W.radius, sizeof(W.radius), hipMemcpyHostToDevice, ctx->stream));
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   W.kern_ok = true;
   return SOD_OK;
 }
@@ -1884,12 +1877,12 @@ int grow_results(sod_ctx* ctx, SiftWork& W, int64_t need) {
   DevBuf<float> nd;
   SOD_TRY(sod_reserve(ctx, nk, (size_t)n));
   SOD_TRY(sod_reserve(ctx, nd, (size_t)n * 128));
-  for (SiftSlot* S : W.slots) SOD_HIP(ctx, hipStreamSynchronize(S->stream));
+  for (SiftSlot* S : W.slots) SOD_HIP(ctx, sod_stream_sync(S->stream));
   if (have > 0) {   // on slot 0's stream, not the null stream (see lds_order_probe)
     hipStream_t s0 = W.slots[0]->stream;
     SOD_HIP(ctx, hipMemcpyAsync(nk.p, W.all_kp.p, (size_t)have * sizeof(Kp), hipMemcpyDeviceToDevice, s0));
     SOD_HIP(ctx, hipMemcpyAsync(nd.p, W.all_desc.p, (size_t)have * 512, hipMemcpyDeviceToDevice, s0));
-    SOD_HIP(ctx, hipStreamSynchronize(s0));
+    SOD_HIP(ctx, sod_stream_sync(s0));
   }
   sod_release(W.all_kp);
   sod_release(W.all_desc);
@@ -1941,7 +1934,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
       SiftSlot* S = W.slots[(size_t)j];
       const int i = i0 + j;
       for (int attempt = 0;; ++attempt) {
-        SOD_HIP(ctx, hipStreamSynchronize(S->stream));
+        SOD_HIP(ctx, sod_stream_sync(S->stream));
         const unsigned c0 = S->hcnt[0], c1 = S->hcnt[1];
         if (c0 <= (unsigned)S->cap && c1 <= (unsigned)S->cap) break;
         if (attempt >= 3) return sod_fail(ctx, SOD_ENOMEM, "SIFT: candidate list did not fit after growing");
@@ -1953,7 +1946,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
       if (S->rank_deferred && (int64_t)S->hcnt[1] > sort_max()) {   // the list did not fit one work-group
         SOD_TRY(enqueue_rank(ctx, *S, sort_max()));
         SOD_TRY(enqueue_describe(ctx, *S, W.lane_order));
-        SOD_HIP(ctx, hipStreamSynchronize(S->stream));
+        SOD_HIP(ctx, sod_stream_sync(S->stream));
       }
       const int64_t cnt = S->hcnt[2];
       const int64_t at = W.off.back();
@@ -1970,7 +1963,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
       if (counts) counts[i] = (int32_t)cnt;
     }
   }
-  for (int j = 0; j < K; ++j) SOD_HIP(ctx, hipStreamSynchronize(W.slots[(size_t)j]->stream));
+  for (int j = 0; j < K; ++j) SOD_HIP(ctx, sod_stream_sync(W.slots[(size_t)j]->stream));
   W.valid = true;
   return SOD_OK;
 }
@@ -2061,12 +2054,12 @@ int sod_sift_get(sod_ctx* ctx, int64_t cap, float* x, float* y, float* size, flo
     std::vector<Kp> h((size_t)n);
     // the detection's streams are done (its count sync); the copies go on slot 0's stream
     // rather than the null stream, which would wait for every blocking stream of the process
-    for (SiftSlot* S : W->slots) SOD_HIP(ctx, hipStreamSynchronize(S->stream));
+    for (SiftSlot* S : W->slots) SOD_HIP(ctx, sod_stream_sync(S->stream));
     hipStream_t s0 = W->slots[0]->stream;
     SOD_HIP(ctx, hipMemcpyAsync(h.data(), W->all_kp.p, (size_t)n * sizeof(Kp), hipMemcpyDeviceToHost, s0));
     if (descriptors)
       SOD_HIP(ctx, hipMemcpyAsync(descriptors, W->all_desc.p, (size_t)n * 512, hipMemcpyDeviceToHost, s0));
-    SOD_HIP(ctx, hipStreamSynchronize(s0));
+    SOD_HIP(ctx, sod_stream_sync(s0));
     for (int64_t i = 0; i < n; ++i) {
       const Kp& k = h[(size_t)i];
       if (x) x[i] = k.x;
@@ -2111,7 +2104,7 @@ int sod_sift_to_queries(sod_ctx* ctx) {
   hipLaunchKernelGGL(unpack_kp_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ctx->stream,
                      W->all_kp.p, ctx->scal.p + 3, ctx->qx.p, ctx->qy.p, ctx->qang.p, ctx->qoct.p);
   SOD_HIP(ctx, hipGetLastError());
-  SOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->nq = nq;
   ctx->win0 = 0;
   ctx->winn = -1;

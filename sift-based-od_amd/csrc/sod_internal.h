@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
+
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -114,6 +116,8 @@ struct sod_ctx {
   DevBuf<double> pose_b;        // the other step parity of pose / msize
   DevBuf<int32_t> msize_b;
   bool houghed = false;
+  bool hist_dense = true;       // counts / first hold the vote histogram (not after the fused
+                                // one-image path, hough_small_kernel: sod_hist_dense builds it)
   // boundary guard (hough.hip): records of the matches whose x / y bin may depend on the
   // last ulp of cos / sin [nq * 8], their count ([0] appended by pose_kernel, [1] handed over
   // by hist_kernel); resolved once per Hough launch, before any result is read
@@ -145,6 +149,8 @@ struct sod_ctx {
   int64_t vmax = 0, mmax = 0;
   int32_t vote_thr = 0;
   bool selected = false;
+  bool gathered = false;        // amx / amy / aqx / aqy / aisig already hold the members' points
+  DevBuf<uint32_t> vfirst_s;    // hough_small_kernel: first voting query of valid bins past LDS
 
   // ---- affine ----
   DevBuf<float> amx, amy, aqx, aqy;  // per-member points [mmax]
@@ -201,6 +207,9 @@ struct sod_ctx {
   hipEvent_t ev_matched_p = nullptr;   // the last matcher launch's completion event
   bool stage_timing = true;   // sod_set_stage_timing: ev[2..5] around the tail stages
   bool overlap = false;
+  bool mk_main = true;        // the last matcher launch went on the context stream (idle, no split)
+  bool merge_norec[2] = {false, false};   // a slot's last merge released it without an event
+  bool match_timing = true;   // sod_set_match_timing: begin/end events of every matcher launch
   // sod_set_cu_reserve: the top `reserved_cus` CU-mask bits (cu_reserve per XCD, mask bit i
   // is on XCD i % 8) run the context / side streams; the matcher stream gets the rest
   int cu_reserve = 0;
@@ -226,6 +235,24 @@ struct sod_ctx {
   int64_t nmatch = 0;
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
 };
+
+// Host wait for a stream: poll it for up to kSpinUs, then block.  A blocking
+// hipStreamSynchronize returned ~20-30 us after the last kernel of a short step had ended
+// (one query image: 0.20 ms of latency for a 0.14 ms device span, rocprofv3 HIP-API trace);
+// polling returns within a query's cost of the end.  Longer waits (C3's 3.7 ms matcher)
+// fall back to the blocking call after the spin.
+constexpr int kSpinUs = 400;
+inline hipError_t sod_stream_sync(hipStream_t s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return hipSuccess;
+    if (q != hipErrorNotReady) return q;
+    (void)hipGetLastError();   // hipErrorNotReady is an answer, not an error
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) break;
+  }
+  return hipStreamSynchronize(s);
+}
 
 // error helpers ---------------------------------------------------------------------------
 int sod_fail(sod_ctx* ctx, int code, const std::string& msg);
@@ -306,15 +333,21 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
                            float** d2);
 int sod_match_stream_end(sod_ctx* ctx, hipEvent_t done = nullptr);
 int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end);
-int sod_partials_merged(sod_ctx* ctx);
+hipEvent_t sod_merge_done_event(sod_ctx* ctx);
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2,
-                 int nparts, int64_t stride, int32_t* reset = nullptr, bool final_merge = false);
+                 int nparts, int64_t stride, int32_t* reset = nullptr, bool final_merge = false,
+                 hipEvent_t done = nullptr);
 int launch_ratio(sod_ctx* ctx, double ratio);
 int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi);
 // boundary guard: redo the listed matches' x / y bins with glibc cos / sin and, when one
 // changes, the histogram and every stage after it (call before reading any Hough result)
 int sod_guard_resolve(sod_ctx* ctx);
 int launch_select(sod_ctx* ctx, int32_t thr);
+// the fused one-image Hough + select + gather (hough.hip hough_small_kernel) and the lazy
+// dense histogram after it
+bool sod_hough_small_ok(const sod_ctx* ctx);
+int launch_hough_small(sod_ctx* ctx, int32_t thr);
+int sod_hist_dense(sod_ctx* ctx);
 int launch_all_bins(sod_ctx* ctx);
 int launch_affine_gather(sod_ctx* ctx);
 int launch_affine(sod_ctx* ctx, int64_t nbins_dev_scalar_or_host, bool count_on_device,

@@ -407,3 +407,92 @@ def test_member_order_at_scale(ctx, nq):
         seg = mem[off[i]:off[i + 1]]
         assert np.all(np.diff(seg) > 0), "bin %d members not in query order" % i
     ctx.set_impl("bf16")
+
+
+def _hough_state(c, shape, bins, thr, fused, monkeypatch, affine=True):
+    monkeypatch.setenv("SOD_HOUGH_FUSED", "1" if fused else "0")
+    c.hough_select(shape, bins, thr)
+    if affine:
+        c.affine((shape[1], shape[0]), 128.0, 128.0, 4)
+    out = {"valid": c.valid_result(), "bins": c.all_bins(), "guard": c.guard_stats()[:2]}
+    if affine:
+        out["affine"] = c.affine_result()
+    # another threshold on the same votes (needs the dense histogram the fused path skips)
+    c.select(max(1, thr - 2))
+    out["valid_lo"] = c.valid_result()
+    return out
+
+
+def _same_hough(a, b):
+    for k in ("keys", "votes", "offsets", "members"):
+        assert np.array_equal(a["valid"][k], b["valid"][k]), k
+        assert np.array_equal(a["valid_lo"][k], b["valid_lo"][k]), k
+    assert np.array_equal(a["valid"]["means"], b["valid"]["means"])
+    assert np.array_equal(a["bins"][0], b["bins"][0]) and np.array_equal(a["bins"][1], b["bins"][1])
+    assert a["guard"] == b["guard"]
+    if "affine" in a:
+        for k in ("survived", "votes", "params", "alive"):
+            assert np.array_equal(a["affine"][k], b["affine"][k]), k
+
+
+@pytest.mark.parametrize("name,ngroups", [("near_edge_b15", 78), ("near_edge_b32", 78),
+                                          ("edge_b15", 0), ("edge_b6", 0)])
+def test_fused_hough_select_equals_dense(ctx, monkeypatch, name, ngroups):
+    """The fused one-image launch (hough_small_kernel: pose, votes from a base-key hash, valid
+    bins, members, affine inputs) equals the dense path (pose_kernel + hist_kernel +
+    select_small_kernel + affine_gather_kernel) bit for bit -- bin table, valid bins, members,
+    means, affine results, a second threshold -- on the reference's edge fixtures, including
+    matches on bin edges that the boundary guard re-does on the host (<= 1024 of them)."""
+    g = golden(name)
+    q, m = g["match_q"], g["match_m"]
+    if ngroups:
+        keep = q < ngroups * 13
+        q, m = q[keep], m[keep]
+    nq = int(q.max()) + 1
+    kq = kp(g, "q_").slice(0, nq)
+    shape = tuple(int(v) for v in g["shape"])
+    outs = []
+    for fused in (True, False):
+        ctx.set_keypoints(kp(g, "db_"), g["db_img"], g["centroid"], g["size"])
+        ctx.upload_queries(None, kq)
+        idx1 = np.zeros(nq, np.int32)
+        idx1[q] = m
+        good = np.zeros(nq, bool)
+        good[q] = True
+        ctx.set_matches(idx1, good)
+        outs.append(_hough_state(ctx, shape, int(g["bins"]), 5, fused, monkeypatch))
+    _same_hough(*outs)
+    if name.startswith("near_edge"):
+        assert outs[0]["guard"][0] == len(q)
+
+
+@pytest.mark.parametrize("nq,thr,n_objects,decoy", [(500, 5, 4, 0.05), (1024, 5, 2, 0.05),
+                                                    (1024, 1, 4, 0.6), (700, 2, 0, 0.05),
+                                                    (1, 1, 1, 0.0)])
+def test_fused_pipeline_equals_dense(ctx, monkeypatch, nq, thr, n_objects, decoy):
+    """One query image through the whole pipeline, fused vs dense Hough / select, against
+    the 1M-row-shaped DB of 200 images: identical bins, members, means, affine results and
+    a second threshold.  thr 1 with many decoys (good matches at random poses) makes
+    thousands of valid bins (past the fused kernel's LDS copy of 2048: its global spill
+    path); n_objects 0 = no planted object (random votes only)."""
+    db = synthetic.make_database(200, 1000, seed=0)
+    qs = synthetic.make_queries(nq, seed=9, db_seed=0, kp_per_image=1000,
+                                n_objects=max(1, n_objects), planted_frac=0.3 if n_objects else 0.0,
+                                decoy_frac=decoy)
+    ctx.set_impl("i8")
+    ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
+    ctx.upload_db(db.des)
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setenv("SOD_HOUGH_FUSED", "1" if fused else "0")
+        ctx.upload_queries(qs.des, qs.kp)
+        ctx.pipeline(qs.shape, (32, 32, 8, 12), ratio=0.75, vote_threshold=thr, affine_threshold=4)
+        o = {"valid": ctx.valid_result(), "bins": ctx.all_bins(), "guard": ctx.guard_stats()[:2],
+             "affine": ctx.affine_result(), "post": ctx.postprocess()}
+        ctx.select(max(1, thr - 1))
+        o["valid_lo"] = ctx.valid_result()
+        outs.append(o)
+    _same_hough(*outs)
+    assert np.array_equal(outs[0]["post"]["final_pose"], outs[1]["post"]["final_pose"])
+    if thr == 1 and nq > 1:
+        assert len(outs[0]["valid"]["keys"]) > 2048

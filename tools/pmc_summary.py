@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc passes of the matcher (tools/gpu_pmc.sh) into one JSON under
 profiles/: per-launch averages, HBM bytes = 2*FETCH_SIZE*1024 (gfx950 reports half of a
 wide coalesced stream, MI355X_MICROARCH.md §HBM) + WRITE_SIZE*1024, the effective clock
-GRBM_GUI_ACTIVE/8/t and the MFMA-busy fraction.
+GRBM_GUI_ACTIVE/8 over each profiled dispatch's own duration and the MFMA-busy fraction.
     python tools/pmc_summary.py gpurun_out/pmc_<kernel>_c3 profiles/r01_pmc_<kernel>_c3.json \
         <kernel_ms> <kernel>"""
 import collections
@@ -30,17 +30,29 @@ for sub in sorted(os.listdir(src)):
 avg = {k: sum(v) / len(v) for k, v in vals.items()}
 out = {"kernel": kernel, "counters_per_launch": avg}
 if gui_clock:   # the profiled dispatches' own clock (MI355X_MICROARCH.md, DVFS)
-    out["clock_ghz_profiled"] = sum(gui_clock) / len(gui_clock)
+    c = sum(gui_clock) / len(gui_clock)
+    if c <= 2.4:
+        out["clock_ghz_profiled"] = c
+    else:
+        # GRBM_GUI_ACTIVE spans a little more than the dispatch's own timestamps: on short
+        # dispatches (one query image, ~70 us) the ratio exceeds the chip's 2.4 GHz, so it
+        # is no clock measurement there
+        out["clock_ghz_profiled"] = None
+        out["clock_note"] = ("GRBM_GUI_ACTIVE/8 over the dispatch duration = %.3f GHz > 2.4: the "
+                             "counter window exceeds a short dispatch; not a clock" % c)
 if "FETCH_SIZE" in avg:
     out["hbm_read_bytes"] = 2 * avg["FETCH_SIZE"] * 1024
 if "WRITE_SIZE" in avg:
     out["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
 if "hbm_read_bytes" in out and "hbm_write_bytes" in out:
     out["hbm_bytes"] = out["hbm_read_bytes"] + out["hbm_write_bytes"]
-if kernel_ms and "GRBM_GUI_ACTIVE" in avg:
+if "GRBM_GUI_ACTIVE" in avg:
+    # the clock is the profiled dispatches' own (cycles over their own duration, above);
+    # dividing their cycles by an UNprofiled launch time (rounds 1-3) mixed two runs and gave
+    # clocks above the chip's 2.4 GHz
     cyc = avg["GRBM_GUI_ACTIVE"] / 8
-    out["kernel_ms"] = kernel_ms
-    out["clock_ghz"] = cyc / (kernel_ms * 1e-3) / 1e9
+    if kernel_ms:
+        out["kernel_ms_unprofiled"] = kernel_ms
     if "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
         out["mfma_busy_frac"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc)
 json.dump(out, open(dst, "w"), indent=1)
