@@ -501,15 +501,20 @@ def main():
     # one query image alone, start to finish: host clock around one step between two device
     # syncs, tail on the whole chip -- the latency a single main.py query sees (the timed
     # steps above overlap each image's tail with the next image's matcher)
+    # (no timing events on the matcher launch either: with the split undone and the streams
+    # idle the matcher runs on the context stream, where an event on its dispatch would delay
+    # the merge ~5 us)
     lat = []
     ctx.set_stage_timing(False)
-    for _ in range(5):
+    ctx.set_match_timing(False)
+    for _ in range(max(5, min(a.steps, 20))):
         turn[0] = 0
         ctx.synchronize()
         t0 = time.perf_counter()
         step()
         ctx.synchronize()
         lat.append((time.perf_counter() - t0) * 1000.0)
+    ctx.set_match_timing(True)
     ctx.set_stage_timing(True)
     latency_ms = float(np.median(lat))
 

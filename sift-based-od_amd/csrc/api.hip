@@ -17,9 +17,10 @@ thread_local std::string g_err;  // errors before a ctx exists
 
 // Every entry point starts here; by default it also joins the side stream (PoseBin means),
 // so whatever comes next on the main stream sees their results.
-int set_dev(sod_ctx* ctx, bool join = true) {
+int set_dev(sod_ctx* ctx, bool join = true, bool flush = true) {
   if (!ctx) return SOD_EINVAL;
   SOD_HIP(ctx, hipSetDevice(ctx->device));
+  if (flush) SOD_TRY(sod_means_flush(ctx));
   if (join && ctx->side_pending) {
     SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
     ctx->side_pending = false;
@@ -1205,7 +1206,7 @@ int sod_hough_guard_stats(sod_ctx* ctx, int64_t* flagged, int64_t* changed,
 // ---- affine ---------------------------------------------------------------------------
 int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_factor,
                        double y_factor, int32_t threshold) {
-  SOD_TRY(set_dev(ctx, false));   // runs beside the means on the side stream
+  SOD_TRY(set_dev(ctx, false, false));   // runs beside the means (side stream or same launch)
   if (!ctx->selected) return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
   if (!(x_factor != 0.0) || !(y_factor != 0.0)) return sod_fail(ctx, SOD_EINVAL, "zero factor");
   ctx->aff_qw = query_w;
@@ -1219,6 +1220,12 @@ int sod_affine_enqueue(sod_ctx* ctx, int32_t query_w, int32_t query_h, double x_
   SOD_TRY(sod_reserve(ctx, ctx->fvotes, (size_t)ctx->vmax));
   SOD_TRY(sod_reserve(ctx, ctx->params, (size_t)ctx->vmax * 6));
   SOD_TRY(sod_reserve(ctx, ctx->alive, (size_t)ctx->mmax));
+  if (ctx->means_deferred) {   // the fused one-image path: means and affine in one launch
+    SOD_TRY(launch_means_affine(ctx, query_w, query_h, x_factor, y_factor, threshold));
+    SOD_TRY(sod_stage_mark(ctx, kStageAffine, true));
+    ctx->affined = true;
+    return SOD_OK;
+  }
   SOD_TRY(launch_affine(ctx, 0, true, ctx->voff.p, ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p,
                         ctx->aisig.p, query_w, query_h, ctx->n_qimg ? ctx->bwh.p : nullptr,
                         x_factor, y_factor, threshold, 1 << 30,

@@ -1056,18 +1056,36 @@ __device__ __forceinline__ void bin_votes(uint32_t key, uint32_t sl, const uint3
     h[e] = key_hash(k2[e]);
     kv[e] = hk[h[e]];
   }
-  uint32_t cnt = 0u, fst = 0xFFFFFFFFu;
+  // nearly every probe ends at its first slot (a hit or an empty slot: <= 50 % load); the
+  // values of all 16 first slots are read together, and only a collision walks on
+  uint32_t nv_[16], qv_[16];
+  bool coll = false;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    if (k2[e] == kNoKey) continue;
-    uint32_t hh = h[e], kk = kv[e];
-    while (kk != k2[e] && kk != kNoKey) {   // collision: linear probe
-      hh = (hh + 1) & (kFusedHash - 1);
-      kk = hk[hh];
+    nv_[e] = hn[h[e]];
+    qv_[e] = hq[h[e]];
+    coll |= k2[e] != kNoKey && kv[e] != k2[e] && kv[e] != kNoKey;
+  }
+  uint32_t cnt = 0u, fst = 0xFFFFFFFFu;
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+    if (k2[e] != kNoKey && kv[e] == k2[e]) {
+      cnt += nv_[e];
+      fst = min(fst, qv_[e] * 16u + (uint32_t)e);
     }
-    if (kk == k2[e]) {
-      cnt += hn[hh];
-      fst = min(fst, hq[hh] * 16u + (uint32_t)e);
+  if (__builtin_expect(coll, 0)) {
+#pragma unroll 1
+    for (int e = 0; e < 16; ++e) {
+      if (k2[e] == kNoKey || kv[e] == k2[e] || kv[e] == kNoKey) continue;
+      uint32_t hh = h[e], kk = kv[e];
+      while (kk != k2[e] && kk != kNoKey) {   // linear probe past the collision
+        hh = (hh + 1) & (kFusedHash - 1);
+        kk = hk[hh];
+      }
+      if (kk == k2[e]) {
+        cnt += hn[hh];
+        fst = min(fst, hq[hh] * 16u + (uint32_t)e);
+      }
     }
   }
   *cnt_out = cnt;
@@ -1367,19 +1385,19 @@ __global__ void recip_table_kernel(int64_t M, double* __restrict__ rtab) {
 constexpr int kMeansU = 4;                  // members per lane per fetch: 256 per batch
 constexpr int kMeansB = 64 * kMeansU;
 
-__global__ __launch_bounds__(64) void means_kernel(const uint32_t* __restrict__ scal,
-                                                   const int64_t* __restrict__ voff,
-                                                   const int32_t* __restrict__ members,
-                                                   const double* __restrict__ pose,
-                                                   const int2* __restrict__ msize,
-                                                   const double* __restrict__ rtab,
-                                                   double* __restrict__ means) {
-  // one buffer: the wave stores a batch, runs its chains, and only then stores the next
-  __shared__ double xs[7][kMeansB];   // [quantity 0-5, 1/(n+1)][member]
-  const int lane = threadIdx.x;
+// one wave: the bins v0, v0 + stride, ... (xs: the wave's LDS batch buffer)
+__device__ __forceinline__ void means_wave(int64_t v0, int64_t stride, double (*xs)[kMeansB],
+                                           const uint32_t* __restrict__ scal,
+                                           const int64_t* __restrict__ voff,
+                                           const int32_t* __restrict__ members,
+                                           const double* __restrict__ pose,
+                                           const int2* __restrict__ msize,
+                                           const double* __restrict__ rtab,
+                                           double* __restrict__ means) {
+  const int lane = threadIdx.x & 63;
   const int k = lane < 6 ? lane : 0;
   const int64_t V = scal[0];
-  for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
+  for (int64_t v = v0; v < V; v += stride) {
     const int64_t a = voff[v], e = voff[v + 1];
     // batch b covers members a+256b ... ; n of member j is j - a (the first one sets the mean)
     double nx[kMeansU][7];
@@ -1440,6 +1458,18 @@ __global__ __launch_bounds__(64) void means_kernel(const uint32_t* __restrict__ 
     }
     if (lane < 6) means[6 * v + k] = m;
   }
+}
+
+__global__ __launch_bounds__(64) void means_kernel(const uint32_t* __restrict__ scal,
+                                                   const int64_t* __restrict__ voff,
+                                                   const int32_t* __restrict__ members,
+                                                   const double* __restrict__ pose,
+                                                   const int2* __restrict__ msize,
+                                                   const double* __restrict__ rtab,
+                                                   double* __restrict__ means) {
+  // one buffer: the wave stores a batch, runs its chains, and only then stores the next
+  __shared__ double xs[7][kMeansB];   // [quantity 0-5, 1/(n+1)][member]
+  means_wave(blockIdx.x, gridDim.x, xs, scal, voff, members, pose, msize, rtab, means);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1559,19 +1589,17 @@ __device__ __forceinline__ int group_sum_i(int x) {
 // (sod_set_cu_reserve) hold 64 / kAffG times as many chains in flight.
 constexpr int kAffG = 64;   // 16 measured slower at C3: the large bins' member loops lengthen
 
-__global__ __launch_bounds__(256) void affine_kernel(
-    int64_t nb_host, const uint32_t* __restrict__ nb_dev, const int64_t* __restrict__ off,
-    const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
-    const float* __restrict__ qy, const int32_t* __restrict__ isig, int qw, int qh,
-    const int32_t* __restrict__ bwh, double xf, double yf, int thr, int max_iter,
-    const double* __restrict__ params_in,
-    uint8_t* __restrict__ surv, int32_t* __restrict__ votes, double* __restrict__ params,
-    uint8_t* __restrict__ alive) {
-  constexpr int G = kAffG;
+// lane groups of G lanes: group g0 of ngroups takes the bins g0, g0 + ngroups, ...
+template <int G>
+__device__ __forceinline__ void affine_groups(
+    int64_t g0, int64_t ngroups, int64_t nb_host, const uint32_t* __restrict__ nb_dev,
+    const int64_t* __restrict__ off, const float* __restrict__ mx, const float* __restrict__ my,
+    const float* __restrict__ qx, const float* __restrict__ qy, const int32_t* __restrict__ isig,
+    int qw, int qh, const int32_t* __restrict__ bwh, double xf, double yf, int thr, int max_iter,
+    const double* __restrict__ params_in, uint8_t* __restrict__ surv,
+    int32_t* __restrict__ votes, double* __restrict__ params, uint8_t* __restrict__ alive) {
   const int lane = threadIdx.x & (G - 1);                 // lane within the bin's group
-  const int64_t ngroups = (int64_t)gridDim.x * (blockDim.x / G);
   const int64_t NB = nb_dev ? (int64_t)nb_dev[0] : nb_host;
-  const int64_t g0 = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
   // every group of the wave runs the loop the same number of times (shuffles need the
   // whole wave): groups past the last bin idle with an empty member range
   const int64_t wave_first = g0 - (threadIdx.x & 63) / G;
@@ -1646,6 +1674,39 @@ __global__ __launch_bounds__(256) void affine_kernel(
       for (int k = 0; k < 6; ++k) params[6 * v + k] = prm[k];
     }
   }
+}
+
+__global__ __launch_bounds__(256) void affine_kernel(
+    int64_t nb_host, const uint32_t* __restrict__ nb_dev, const int64_t* __restrict__ off,
+    const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
+    const float* __restrict__ qy, const int32_t* __restrict__ isig, int qw, int qh,
+    const int32_t* __restrict__ bwh, double xf, double yf, int thr, int max_iter,
+    const double* __restrict__ params_in,
+    uint8_t* __restrict__ surv, int32_t* __restrict__ votes, double* __restrict__ params,
+    uint8_t* __restrict__ alive) {
+  constexpr int G = kAffG;
+  affine_groups<G>((int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G,
+                   (int64_t)gridDim.x * (blockDim.x / G), nb_host, nb_dev, off, mx, my, qx, qy,
+                   isig, qw, qh, bwh, xf, yf, thr, max_iter, params_in, surv, votes, params, alive);
+}
+
+// The fused one-image path's last launch: the PoseBin means (blocks nA..) beside the affine
+// verification (blocks 0..nA-1), one wave per bin each -- independent stages, so one launch
+// instead of two serial ones on the context stream
+__global__ __launch_bounds__(64) void means_affine_kernel(
+    int nA, const uint32_t* __restrict__ scal, const int64_t* __restrict__ voff,
+    const int32_t* __restrict__ members, const double* __restrict__ pose,
+    const int2* __restrict__ msize, const double* __restrict__ rtab, double* __restrict__ means,
+    const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
+    const float* __restrict__ qy, const int32_t* __restrict__ isig, int qw, int qh, double xf,
+    double yf, int thr, uint8_t* __restrict__ surv, int32_t* __restrict__ votes,
+    double* __restrict__ params, uint8_t* __restrict__ alive) {
+  __shared__ double xs[7][kMeansB];
+  if ((int)blockIdx.x < nA)
+    affine_groups<64>(blockIdx.x, nA, 0, scal, voff, mx, my, qx, qy, isig, qw, qh, nullptr, xf,
+                      yf, thr, 1 << 30, nullptr, surv, votes, params, alive);
+  else
+    means_wave(blockIdx.x - nA, gridDim.x - nA, xs, scal, voff, members, pose, msize, rtab, means);
 }
 
 }  // namespace
@@ -2102,7 +2163,39 @@ int launch_hough_small(sod_ctx* ctx, int32_t thr) {
   ctx->guard_done = false;
   ctx->hist_dense = false;
   ctx->gathered = true;
+  // the PoseBin means wait for the affine enqueue, which runs them in the same launch
+  // (means_affine_kernel); any other next call runs them alone first (sod_means_flush)
+  ctx->means_deferred = true;
+  return SOD_OK;
+}
+
+int sod_means_flush(sod_ctx* ctx) {
+  if (!ctx->means_deferred) return SOD_OK;
+  ctx->means_deferred = false;
   return launch_means(ctx, true);
+}
+
+// the fused path's affine verification with its deferred PoseBin means in one launch
+int launch_means_affine(sod_ctx* ctx, int32_t qw, int32_t qh, double xf, double yf, int32_t thr) {
+  ctx->means_deferred = false;
+  const bool new_rtab = ctx->rtab.n < (size_t)ctx->mmax;
+  SOD_TRY(sod_reserve(ctx, ctx->rtab, (size_t)ctx->mmax));
+  if (new_rtab) {
+    hipLaunchKernelGGL(recip_table_kernel, dim3((unsigned)std::min<int64_t>(cdiv(ctx->rtab.n, 256), 4096)),
+                       dim3(256), 0, ctx->stream, (int64_t)ctx->rtab.n, ctx->rtab.p);
+    SOD_HIP(ctx, hipGetLastError());
+  }
+  const int nA = std::max(1, ctx->tail_cus() * 8), nM = std::max(1, ctx->tail_cus() * 8);
+  hipLaunchKernelGGL(means_affine_kernel, dim3((unsigned)(nA + nM)), dim3(64), 0, ctx->stream, nA,
+                     ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->pose.p,
+                     reinterpret_cast<const int2*>(ctx->msize.p), ctx->rtab.p, ctx->means.p,
+                     ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p, ctx->aisig.p, qw, qh, xf, yf,
+                     thr, ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p);
+  SOD_HIP(ctx, hipGetLastError());
+  ++ctx->means_id;
+  ctx->hread_id[ctx->hpar] = 0;   // stream order, as launch_means(ctx, true)
+  ctx->sread_id[ctx->spar] = 0;
+  return SOD_OK;
 }
 
 // the dense histogram (counts / first touch of every bin) after the fused path, for the

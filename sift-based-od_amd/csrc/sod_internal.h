@@ -150,6 +150,7 @@ struct sod_ctx {
   int32_t vote_thr = 0;
   bool selected = false;
   bool gathered = false;        // amx / amy / aqx / aqy / aisig already hold the members' points
+  bool means_deferred = false;  // the fused path's PoseBin means are not launched yet
   DevBuf<uint32_t> vfirst_s;    // hough_small_kernel: first voting query of valid bins past LDS
 
   // ---- affine ----
@@ -348,6 +349,10 @@ int launch_select(sod_ctx* ctx, int32_t thr);
 bool sod_hough_small_ok(const sod_ctx* ctx);
 int launch_hough_small(sod_ctx* ctx, int32_t thr);
 int sod_hist_dense(sod_ctx* ctx);
+// the fused path's PoseBin means run with its affine launch; alone when anything else comes
+// first (every entry point but sod_affine_enqueue)
+int sod_means_flush(sod_ctx* ctx);
+int launch_means_affine(sod_ctx* ctx, int32_t qw, int32_t qh, double xf, double yf, int32_t thr);
 int launch_all_bins(sod_ctx* ctx);
 int launch_affine_gather(sod_ctx* ctx);
 int launch_affine(sod_ctx* ctx, int64_t nbins_dev_scalar_or_host, bool count_on_device,
