@@ -1438,13 +1438,38 @@ __device__ __forceinline__ void means_wave(int64_t v0, int64_t stride, double (*
           m = xs[k][0];
           i = 1;
         }
-        for (; i + 16 <= cnt; i += 16) {   // unrolled: LDS reads run ahead of the chain
+        // 16 steps per block, the block's LDS operands in registers before its chain and the
+        // next block's loads issued before it: the chain never waits on LDS (reading each
+        // step's operands one step ahead put an LDS round trip on the chain every two steps,
+        // ~2.5x the chain's own dependent f64 latency)
+        double xv[16], iv[16];
+        if (i + 16 <= cnt) {
 #pragma unroll
           for (int t = 0; t < 16; ++t) {
-            const double n = n0 + (i + t), d = n + 1.0, inv = xs[6][i + t];
-            const double r = m * n + xs[k][i + t];   // -ffp-contract=off: 2 roundings
+            xv[t] = xs[k][i + t];
+            iv[t] = xs[6][i + t];
+          }
+        }
+        for (; i + 16 <= cnt; i += 16) {
+          double xn[16], in_[16];
+          const bool more = i + 32 <= cnt;
+#pragma unroll
+          for (int t = 0; t < 16; ++t) {   // (clamped: a read past the batch is never used)
+            const int jn = more ? i + 16 + t : i + t;
+            xn[t] = xs[k][jn];
+            in_[t] = xs[6][jn];
+          }
+#pragma unroll
+          for (int t = 0; t < 16; ++t) {
+            const double n = n0 + (i + t), d = n + 1.0, inv = iv[t];
+            const double r = m * n + xv[t];   // -ffp-contract=off: 2 roundings
             const double q0 = r * inv;
             m = __builtin_fma(__builtin_fma(-q0, d, r), inv, q0);
+          }
+#pragma unroll
+          for (int t = 0; t < 16; ++t) {
+            xv[t] = xn[t];
+            iv[t] = in_[t];
           }
         }
         for (; i < cnt; ++i) {
@@ -1588,6 +1613,7 @@ __device__ __forceinline__ int group_sum_i(int x) {
 // wave run their chains in the same instructions -- the few reserved CUs of a chip split
 // (sod_set_cu_reserve) hold 64 / kAffG times as many chains in flight.
 constexpr int kAffG = 64;   // 16 measured slower at C3: the large bins' member loops lengthen
+constexpr int kAffU = 8;    // members per lane per round of loads
 
 // lane groups of G lanes: group g0 of ngroups takes the bins g0, g0 + ngroups, ...
 template <int G>
@@ -1620,11 +1646,29 @@ __device__ __forceinline__ void affine_groups(
     const int rounds = max_iter < 1 ? 1 : max_iter;   // max_iter 0: solve once, remove nothing
     for (int it = 0; it < rounds; ++it) {
       double s[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (int64_t j = a + lane; j < e; j += G) {
-        if (!alive[j]) continue;
-        const double x = mx[j], y = my[j], u = qx[j], w = qy[j];
-        s[0] += x * x; s[1] += x * y; s[2] += x; s[3] += y * y; s[4] += y; s[5] += 1.0;
-        s[6] += x * u; s[7] += y * u; s[8] += u; s[9] += x * w; s[10] += y * w; s[11] += w;
+      // kAffU members of the lane per round, all loads in flight before the sums (a load
+      // under the alive test was one dependent round trip per member: a C3 bin of ~2 700
+      // members took ~42 of them per pass); same order of additions as one at a time
+      for (int64_t j0 = a + lane; j0 < e; j0 += (int64_t)G * kAffU) {
+        float fx[kAffU], fy[kAffU], fu[kAffU], fw[kAffU];
+        uint8_t al[kAffU];
+#pragma unroll
+        for (int t = 0; t < kAffU; ++t) {
+          const int64_t j = j0 + (int64_t)t * G;
+          const int64_t jc = j < e ? j : j0;   // clamped: an unused, valid address
+          al[t] = j < e ? alive[jc] : 0;
+          fx[t] = mx[jc];
+          fy[t] = my[jc];
+          fu[t] = qx[jc];
+          fw[t] = qy[jc];
+        }
+#pragma unroll
+        for (int t = 0; t < kAffU; ++t) {
+          if (!al[t]) continue;
+          const double x = fx[t], y = fy[t], u = fu[t], w = fw[t];
+          s[0] += x * x; s[1] += x * y; s[2] += x; s[3] += y * y; s[4] += y; s[5] += 1.0;
+          s[6] += x * u; s[7] += y * u; s[8] += u; s[9] += x * w; s[10] += y * w; s[11] += w;
+        }
       }
 #pragma unroll
       for (int k = 0; k < 12; ++k) s[k] = group_sum<G>(s[k]);
@@ -1649,14 +1693,29 @@ __device__ __forceinline__ void affine_groups(
       }
       // remove_outliers, AffineParameters.py:134-159
       int dropped = 0;
-      for (int64_t j = a + lane; j < e; j += G) {
-        if (!alive[j]) continue;
-        const double x = mx[j], y = my[j];
-        const double up = (prm[0] * x + prm[1] * y) + prm[4];
-        const double vp = (prm[2] * x + prm[3] * y) + prm[5];
-        if (fabs(up - (double)qx[j]) > xref || fabs(vp - (double)qy[j]) > yref) {
-          alive[j] = 0;
-          ++dropped;
+      for (int64_t j0 = a + lane; j0 < e; j0 += (int64_t)G * kAffU) {
+        float fx[kAffU], fy[kAffU], fu[kAffU], fw[kAffU];
+        uint8_t al[kAffU];
+#pragma unroll
+        for (int t = 0; t < kAffU; ++t) {
+          const int64_t j = j0 + (int64_t)t * G;
+          const int64_t jc = j < e ? j : j0;
+          al[t] = j < e ? alive[jc] : 0;
+          fx[t] = mx[jc];
+          fy[t] = my[jc];
+          fu[t] = qx[jc];
+          fw[t] = qy[jc];
+        }
+#pragma unroll
+        for (int t = 0; t < kAffU; ++t) {
+          if (!al[t]) continue;
+          const double x = fx[t], y = fy[t];
+          const double up = (prm[0] * x + prm[1] * y) + prm[4];
+          const double vp = (prm[2] * x + prm[3] * y) + prm[5];
+          if (fabs(up - (double)fu[t]) > xref || fabs(vp - (double)fw[t]) > yref) {
+            alive[j0 + (int64_t)t * G] = 0;
+            ++dropped;
+          }
         }
       }
       dropped = group_sum_i<G>(dropped);

@@ -1514,10 +1514,12 @@ int get_slot(sod_ctx* ctx, SiftWork& W, int i, SiftSlot** out) {
     // tail streams among them -- and the image's stream and its side stream on ONE queue
     // serialise and stall on their cross-stream events: 0.65 -> 1.2-1.5 ms per image
     // measured); the mask leaves out CU 0, the side stream's leaves out the last CU.  Only
-    // slot 0, the one a lone image (and so the side stream) uses: a batch of 16 on four
-    // masked streams ran 7.43 ms against 6.29 unmasked (SOD_SIFT_STREAM_MASK=0: none masked,
-    // 2: all four)
-    int masked = S->stream == nullptr && W.slots.size() == 1 ? 1 : 0;
+    // slot kSlots, the lone image's (the one with the side stream): batches run on slots
+    // 0..kSlots-1, unmasked -- in a bench-like process (r04 siftmask1, 3 interleaved rounds)
+    // a batch of 16 took 5.8-7.3 ms with no slot masked, 7.6-7.9 ms with its slot 0 masked
+    // (round 3's layout: the lone image and the batches shared slot 0) and 7.3-7.5 ms with all
+    // masked (SOD_SIFT_STREAM_MASK=0: none masked, 2: all)
+    int masked = (int)W.slots.size() == kSlots + 1 ? 1 : 0;
     if (const char* e = std::getenv("SOD_SIFT_STREAM_MASK"))
       masked = std::atoi(e) == 2 ? 1 : std::atoi(e) == 0 ? 0 : masked;
     if (masked && ctx->num_cus > 2) {
@@ -1922,16 +1924,18 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
   if (const char* e = std::getenv("SOD_SIFT_DIRECT")) direct = std::atoi(e) != 0;
   for (int i0 = 0; i0 < n; i0 += K) {
     const int m = std::min(K, n - i0);
+    // a lone image (a round of one) on its own CU-masked slot, batches on the unmasked ones
+    auto slot_of = [&](int j) { return m == 1 ? kSlots : j; };
     for (int j = 0; j < m; ++j) {
       SiftSlot* S;
-      SOD_TRY(get_slot(ctx, W, j, &S));
+      SOD_TRY(get_slot(ctx, W, slot_of(j), &S));
       const int i = i0 + j;
       SOD_TRY(slot_upload(ctx, *S, imgs[i], ws[i], hs[i], chans ? chans[i] : 1));
       SOD_TRY(set_direct(ctx, W, *S, m == 1 && direct));
       SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], true, m == 1));
     }
     for (int j = 0; j < m; ++j) {
-      SiftSlot* S = W.slots[(size_t)j];
+      SiftSlot* S = W.slots[(size_t)slot_of(j)];
       const int i = i0 + j;
       for (int attempt = 0;; ++attempt) {
         SOD_HIP(ctx, sod_stream_sync(S->stream));
@@ -1963,7 +1967,7 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
       if (counts) counts[i] = (int32_t)cnt;
     }
   }
-  for (int j = 0; j < K; ++j) SOD_HIP(ctx, sod_stream_sync(W.slots[(size_t)j]->stream));
+  for (SiftSlot* S : W.slots) SOD_HIP(ctx, sod_stream_sync(S->stream));
   W.valid = true;
   return SOD_OK;
 }
