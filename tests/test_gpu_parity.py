@@ -496,3 +496,24 @@ def test_fused_pipeline_equals_dense(ctx, monkeypatch, nq, thr, n_objects, decoy
     assert np.array_equal(outs[0]["post"]["final_pose"], outs[1]["post"]["final_pose"])
     if thr == 1 and nq > 1:
         assert len(outs[0]["valid"]["keys"]) > 2048
+
+
+def test_knn_indices_refused_after_matches_set(ctx):
+    """sod_match_knn_indices after sod_matches_set (matches without distances) is refused
+    with SOD_ESTATE instead of returning the caller's indices and a search at distance 0."""
+    from sift_based_od_amd.database import Keypoints
+    g = golden("matcher_edges")
+    n = len(g["db_des"])
+    z = np.zeros(n, np.float32)
+    ctx.set_keypoints(Keypoints(z, z, z, np.zeros(n, np.int32)), np.zeros(n, np.int32),
+                      np.zeros((1, 2)), np.array([[1500, 1000]], np.int32))
+    ctx.upload_db(g["db_des"])
+    ctx.upload_queries(g["q_des"])
+    ctx.set_matches(g["idx1"], g["good"])
+    with pytest.raises(_lib.SodError) as e:
+        ctx.knn_indices()
+    assert e.value.code == _lib.SOD_ESTATE
+    ctx.match()                     # a real match makes them available again
+    ctx.ratio(0.75)
+    i1, i2 = ctx.knn_indices()
+    assert np.array_equal(i1, g["idx1"])
