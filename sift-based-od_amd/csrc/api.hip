@@ -119,7 +119,7 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
   }
   *ks = ctx->mstream;
   // merges that ran on the context stream right after a context-stream matcher released
-  // their slot without an event (sod_merge_done_event): mark them now
+  // their slot without an event (sod_partials_merged): mark them now
   for (int x = 0; x < 2; ++x)
     if (ctx->merge_norec[x]) {
       SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[x], ctx->stream));
@@ -175,13 +175,14 @@ int sod_match_stream_end(sod_ctx* ctx, hipEvent_t done) {
   return SOD_OK;
 }
 
-// the event that releases the partial-result slot after its merge: recorded by the merge's
-// dispatch when the matcher ran on its own stream; after a context-stream matcher none (a
-// dispatch event delays the stream's next kernel ~5 us) -- a later matcher-stream launch
-// records it then (sod_match_stream_begin)
-hipEvent_t sod_merge_done_event(sod_ctx* ctx) {
+// the partial-result slot's release after its merge (recorded on the context stream by
+// sod_partials_merged); after a context-stream matcher none -- an event there delays the
+// stream's next kernel ~5 us -- and a later matcher-stream launch records it then
+// (sod_match_stream_begin)
+int sod_partials_merged(sod_ctx* ctx) {
   ctx->merge_norec[ctx->pslot] = ctx->mk_main && ctx->overlap;
-  return ctx->mk_main ? nullptr : ctx->ev_merged[ctx->pslot];
+  if (!ctx->mk_main) SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[ctx->pslot], ctx->stream));
+  return SOD_OK;
 }
 
 int sod_set_match_timing(sod_ctx* ctx, int on) {
@@ -289,14 +290,12 @@ int sod_create(int device, sod_ctx** out) {
   }
   for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
-  // ev_fork and ev_merged are recorded by kernel dispatches (hipExtLaunchKernelGGL): default
-  // events
-  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_fork);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->mstream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_inputs, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i)
-    e = hipEventCreate(&ctx->ev_merged[i]);
+    e = hipEventCreateWithFlags(&ctx->ev_merged[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_matched, hipEventDisableTiming);
   if (e != hipSuccess) {
     g_err = std::string("sod_create: ") + hipGetErrorString(e);
@@ -796,10 +795,15 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
                           std::to_string(per_xcd * nx) +
                           " CUs: call sod_set_cu_reserve before sod_comm_init");
   }
+  if (std::getenv("SOD_DEBUG_SYNC"))
+    std::fprintf(stderr, "sod: cu_reserve %d -> %d: stream %p side %p mstream %p\n", ctx->cu_reserve,
+                 per_xcd, (void*)ctx->stream, (void*)ctx->side, (void*)ctx->mstream);
   SOD_HIP(ctx, sod_stream_sync(ctx->side));
   SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
   SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   ctx->side_pending = false;
+  const bool dbg = std::getenv("SOD_DEBUG_SYNC") != nullptr;
+  if (dbg) std::fprintf(stderr, "sod: cu_reserve streams idle\n");
   const int n = ctx->num_cus, words = (n + 31) / 32, r = per_xcd * nx;
   std::vector<uint32_t> tail, match;
   if (per_xcd > 0) {
@@ -816,9 +820,11 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
     if (sd) (void)hipStreamDestroy(sd);
     return sod_fail(ctx, SOD_EHIP, std::string("cu reserve: ") + hipGetErrorString(e));
   }
+  if (dbg) std::fprintf(stderr, "sod: cu_reserve new streams %p %p %p\n", (void*)s, (void*)sd, (void*)ms);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->mstream);
+  if (dbg) std::fprintf(stderr, "sod: cu_reserve old streams destroyed\n");
   ctx->stream = s;
   ctx->side = sd;
   ctx->mstream = ms;

@@ -2075,13 +2075,11 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
     SOD_TRY(sod_reserve(ctx, ctx->vidx, (size_t)ctx->nbins));
     SOD_HIP(ctx, hipMemsetAsync(ctx->vidx.p, 0xFF, ctx->vidx.n * 4, ctx->stream));
   }
-  // the last kernel of the selection records ev_fork (the PoseBin means' start on the side
-  // stream) in its own dispatch: a marker packet after it cost the stream a ~8 us gap
   if (nq <= kSmallQ && !select_multi_forced()) {   // one work-group, one launch
-    hipExtLaunchKernelGGL(select_small_kernel, dim3(1), dim3(kSmallT), 0, ctx->stream, nullptr,
-                          ctx->ev_fork, 0, nq, ctx->basekey.p, ctx->vmask.p, ctx->counts.p,
-                          ctx->first.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, (uint32_t)thr,
-                          ctx->vbin.p, ctx->scal.p, ctx->voff.p, ctx->members.p);
+    hipLaunchKernelGGL(select_small_kernel, dim3(1), dim3(kSmallT), 0, ctx->stream, nq,
+                       ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
+                       qimg_p(ctx), ctx->nbins1, (uint32_t)thr, ctx->vbin.p, ctx->scal.p,
+                       ctx->voff.p, ctx->members.p);
     SOD_HIP(ctx, hipGetLastError());
   } else {
     SOD_TRY(launch_members_multi(ctx, (uint32_t)thr, nq));
@@ -2104,17 +2102,14 @@ static int launch_members_multi(sod_ctx* ctx, uint32_t thr, int64_t nq) {
                      0, ctx->stream, ctx->scal.p, ctx->vbin.p, ctx->voff.p, ctx->vidx.p,
                      ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  const bool rebuild = nq > kBitQ;   // beyond the LDS bitmap of member_order_kernel only
-  hipExtLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->tail_cus() * 2)), dim3(kOrderT),
-                        0, ctx->stream, nullptr, rebuild ? nullptr : ctx->ev_fork, 0, ctx->scal.p,
-                        ctx->voff.p, nq, ctx->members.p);
+  hipLaunchKernelGGL(member_order_kernel, dim3(std::max(1, ctx->tail_cus() * 2)), dim3(kOrderT), 0,
+                     ctx->stream, ctx->scal.p, ctx->voff.p, nq, ctx->members.p);
   SOD_HIP(ctx, hipGetLastError());
-  if (rebuild) {
+  if (nq > kBitQ) {   // beyond the LDS bitmap of member_order_kernel only (a no-op otherwise)
     const int wg = std::max(1, ctx->tail_cus() * 4);
-    hipExtLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nullptr,
-                          ctx->ev_fork, 0, nq, ctx->scal.p, ctx->vbin.p, ctx->voff.p,
-                          ctx->counts.p, ctx->first.p, ctx->basekey.p, ctx->vmask.p,
-                          ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->members.p);
+    hipLaunchKernelGGL(members_kernel, dim3(wg), dim3(256), 0, ctx->stream, nq, ctx->scal.p,
+                       ctx->vbin.p, ctx->voff.p, ctx->counts.p, ctx->first.p, ctx->basekey.p,
+                       ctx->vmask.p, ctx_bins(ctx), qimg_p(ctx), ctx->nbins1, ctx->members.p);
     SOD_HIP(ctx, hipGetLastError());
   }
   return SOD_OK;
@@ -2146,7 +2141,7 @@ static int launch_means(sod_ctx* ctx, bool on_main) {
     ctx->sread_id[ctx->spar] = 0;
     return SOD_OK;
   }
-  // ev_fork: recorded by the selection's last dispatch (launch_select)
+  SOD_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
   SOD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
   if (new_rtab) {
     hipLaunchKernelGGL(recip_table_kernel, dim3((unsigned)std::min<int64_t>(cdiv(ctx->rtab.n, 256), 4096)),

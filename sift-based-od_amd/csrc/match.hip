@@ -531,9 +531,9 @@ int launch_match(sod_ctx* ctx) {
   SOD_TRY(sod_match_stream_end(ctx));
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
   SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, nullptr,
-                       ctx->nranks <= 1 && !ctx->comm, sod_merge_done_event(ctx)));
+                       ctx->nranks <= 1 && !ctx->comm));
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, true));
-  return SOD_OK;   // the slot is free again once ev_merged[pslot] (the merge's dispatch) fires
+  return sod_partials_merged(ctx);   // the slot is free again
 }
 
 // per query the lowest row other than excl[q] whose exact squared distance lies in
@@ -558,7 +558,7 @@ int launch_find_rows(sod_ctx* ctx, const float* flo, const float* fhi, const int
 }
 
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2, int nparts,
-                 int64_t stride, int32_t* reset, bool final_merge, hipEvent_t done) {
+                 int64_t stride, int32_t* reset, bool final_merge) {
   const int64_t nq_pad = sod_nq_pad(ctx);
   // sod_pipeline_enqueue announces its ratio: the final merge applies it as well
   const bool fuse = final_merge && ctx->fuse_ratio >= 0.0;
@@ -570,13 +570,10 @@ int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float*
   }
   // waves per 64 queries: one per part up to kMergeW (a few parts: one wave, no LDS step)
   const int wv = std::max(1, std::min(kMergeW, nparts));
-  // `done` (the partial-result slot's release) is recorded by the dispatch itself: a marker
-  // packet after the kernel left a ~8 us gap before the next kernel of the stream
-  hipExtLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, 64)), dim3(64 * wv), 0,
-                        ctx->stream, nullptr, done, 0, d1, idx, d2, nparts, stride, nq_pad,
-                        ctx->cd1.p, ctx->cidx.p, ctx->cd2.p, reset,
-                        fuse ? ctx->fuse_ratio : -1.0, (int64_t)ctx->nq, ctx->d1.p, ctx->d2.p,
-                        ctx->idx1.p, ctx->good.p);
+  hipLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, 64)), dim3(64 * wv), 0,
+                     ctx->stream, d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p,
+                     ctx->cd2.p, reset, fuse ? ctx->fuse_ratio : -1.0, (int64_t)ctx->nq, ctx->d1.p,
+                     ctx->d2.p, ctx->idx1.p, ctx->good.p);
   ctx->ratio_fused_valid = fuse;
   if (fuse) ctx->ratio_fused = ctx->fuse_ratio;
   SOD_HIP(ctx, hipGetLastError());

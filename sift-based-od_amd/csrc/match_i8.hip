@@ -1360,7 +1360,7 @@ int launch_match_i8(sod_ctx* ctx) {
   SOD_TRY(sod_match_stream_end(ctx, ee));
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
   SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, gthr,
-                       ctx->nranks <= 1 && !ctx->comm, sod_merge_done_event(ctx)));   // no exchange follows: final
+                       ctx->nranks <= 1 && !ctx->comm));   // no exchange follows: final
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, true));
-  return SOD_OK;   // the slot is free again once ev_merged[pslot] (the merge's dispatch) fires
+  return sod_partials_merged(ctx);   // the slot is free again
 }

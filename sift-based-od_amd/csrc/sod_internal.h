@@ -5,6 +5,9 @@
 #include <stdint.h>
 
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -252,6 +255,19 @@ inline hipError_t sod_stream_sync(hipStream_t s) {
     (void)hipGetLastError();   // hipErrorNotReady is an answer, not an error
     if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) break;
   }
+  if (std::getenv("SOD_DEBUG_SYNC")) {   // diagnostics: say which stream a long wait is on
+    for (int k = 0; k < 50000; ++k) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) return hipSuccess;
+      if (q != hipErrorNotReady) return q;
+      (void)hipGetLastError();
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    std::fprintf(stderr, "sod: stream %p still busy after ~5 s of queries; blocking sync\n", (void*)s);
+    const hipError_t e = hipStreamSynchronize(s);
+    std::fprintf(stderr, "sod: stream %p blocking sync returned %d\n", (void*)s, (int)e);
+    return e;
+  }
   return hipStreamSynchronize(s);
 }
 
@@ -334,10 +350,9 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
                            float** d2);
 int sod_match_stream_end(sod_ctx* ctx, hipEvent_t done = nullptr);
 int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end);
-hipEvent_t sod_merge_done_event(sod_ctx* ctx);
+int sod_partials_merged(sod_ctx* ctx);
 int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float* d2,
-                 int nparts, int64_t stride, int32_t* reset = nullptr, bool final_merge = false,
-                 hipEvent_t done = nullptr);
+                 int nparts, int64_t stride, int32_t* reset = nullptr, bool final_merge = false);
 int launch_ratio(sod_ctx* ctx, double ratio);
 int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi);
 // boundary guard: redo the listed matches' x / y bins with glibc cos / sin and, when one
