@@ -355,6 +355,12 @@ def pmc_traffic(kernel, config):
     return d, os.path.relpath(best, REPO)
 
 
+def _progress(rank, msg):
+    # progress on stderr (stdout carries only the JSON line): a long run that prints nothing
+    # reads as hung to a supervisor
+    print("bench rank %d: %s" % (rank, msg), file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     D = Dist(a.gpus)
@@ -384,6 +390,7 @@ def main():
     size = np.concatenate([p[3] for p in parts])
     qs = synthetic.make_queries(nq, seed=1, db_seed=0, kp_per_image=kpi)
     gen_s = time.time() - t0
+    _progress(rank, "%s data generated (%.1f s)" % (a.config, gen_s))
 
     dev = D.local
     if world > 1:
@@ -446,9 +453,11 @@ def main():
 
     for c in ctxs:
         c.set_stage_timing(False)   # stage events are marker packets on the tail's path
+    _progress(rank, "DB resident, %d warmup steps" % a.warmup)
     for _ in range(a.warmup):
         step()
     sync_all()
+    _progress(rank, "timing %d steps" % a.steps)
 
     # ---- timed region ----------------------------------------------------------------
     stage = []
@@ -504,6 +513,7 @@ def main():
     # (no timing events on the matcher launch either: with the split undone and the streams
     # idle the matcher runs on the context stream, where an event on its dispatch would delay
     # the merge ~5 us)
+    _progress(rank, "stage timing and latency")
     lat = []
     ctx.set_stage_timing(False)
     ctx.set_match_timing(False)
@@ -633,12 +643,14 @@ def main():
             ec = _lib.Context(dev)
             ec.set_impl(a.impl)
             ec.share_db(ctx)
+        _progress(rank, "extras")
         out["extras"] = extras(ec, ctx, shard, bins)
         if a.config in ("c3", "c5"):
             from sift_based_od_amd import SiftDatabase
             c3db = SiftDatabase(shard, Keypoints(x, y, ang, octv), img, cent, size)
             out["extras"]["main_path"] = main_path_extras(dev, a.impl, (c3db, qs, bins))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        _progress(rank, "cpu baseline")
         out["cpu_baseline"] = cpu_baseline(qs.des, shard, a.cpu_queries)
         out["cpu_baseline_hough"] = cpu_hough_baseline(qs, (x, y, ang, octv), img, cent, size,
                                                        idx1, good, bins)

@@ -212,9 +212,9 @@ static void db_detach(sod_ctx* ctx) {
 }
 
 static void drain_streams(sod_ctx* ctx) {
-  if (ctx->side) (void)sod_stream_sync(ctx->side);
-  if (ctx->mstream) (void)sod_stream_sync(ctx->mstream);
-  if (ctx->stream) (void)sod_stream_sync(ctx->stream);
+  if (ctx->side) (void)sod_stream_drain(ctx->side);
+  if (ctx->mstream) (void)sod_stream_drain(ctx->mstream);
+  if (ctx->stream) (void)sod_stream_drain(ctx->stream);
 }
 
 // Every DB writer calls this first: a source whose DB other contexts alias refuses (their
@@ -315,9 +315,9 @@ int sod_create(int device, sod_ctx** out) {
 void sod_destroy(sod_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->side) (void)sod_stream_sync(ctx->side);
-  if (ctx->mstream) (void)sod_stream_sync(ctx->mstream);
-  if (ctx->stream) (void)sod_stream_sync(ctx->stream);
+  if (ctx->side) (void)sod_stream_drain(ctx->side);
+  if (ctx->mstream) (void)sod_stream_drain(ctx->mstream);
+  if (ctx->stream) (void)sod_stream_drain(ctx->stream);
   db_detach(ctx);
   // contexts still aliasing this DB: let their queued work finish, then drop their views
   // (they report "no database" afterwards instead of reading freed memory)
@@ -798,9 +798,9 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
   if (std::getenv("SOD_DEBUG_SYNC"))
     std::fprintf(stderr, "sod: cu_reserve %d -> %d: stream %p side %p mstream %p\n", ctx->cu_reserve,
                  per_xcd, (void*)ctx->stream, (void*)ctx->side, (void*)ctx->mstream);
-  SOD_HIP(ctx, sod_stream_sync(ctx->side));
-  SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
-  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
+  SOD_HIP(ctx, sod_stream_drain(ctx->side));
+  SOD_HIP(ctx, sod_stream_drain(ctx->mstream));
+  SOD_HIP(ctx, sod_stream_drain(ctx->stream));
   ctx->side_pending = false;
   const bool dbg = std::getenv("SOD_DEBUG_SYNC") != nullptr;
   if (dbg) std::fprintf(stderr, "sod: cu_reserve streams idle\n");

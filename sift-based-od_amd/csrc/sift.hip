@@ -1455,7 +1455,7 @@ struct SiftWork {
 };
 
 static void free_slot(SiftSlot* S) {
-  if (S->stream) (void)sod_stream_sync(S->stream);
+  if (S->stream) (void)sod_stream_drain(S->stream);
   sod_release(S->gray);
   sod_release(S->bgr);
   sod_release(S->gauss);
@@ -1473,7 +1473,7 @@ static void free_slot(SiftSlot* S) {
   sod_release(S->rdesc);
   sod_release(S->src);
   if (S->hcnt) (void)hipHostFree(S->hcnt);
-  if (S->side) (void)sod_stream_sync(S->side);
+  if (S->side) (void)sod_stream_drain(S->side);
   if (S->fork) (void)hipEventDestroy(S->fork);
   if (S->join) (void)hipEventDestroy(S->join);
   if (S->side) (void)hipStreamDestroy(S->side);

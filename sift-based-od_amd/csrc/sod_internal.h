@@ -271,6 +271,14 @@ inline hipError_t sod_stream_sync(hipStream_t s) {
   return hipStreamSynchronize(s);
 }
 
+// Blocking wait for a stream that is about to be destroyed (or whose buffers are about to be
+// freed): hipStreamSynchronize, never the polling sod_stream_sync.  A CU-masked stream that
+// sod_stream_sync had found idle (hipStreamQuery) and that was then destroyed hung in
+// hipStreamDestroy (round 4, sod_set_cu_reserve(1 -> 0) after overlapped pipelines, about one
+// run in three); the blocking synchronize before the destroy is what round 3 did, and never
+// hung.
+inline hipError_t sod_stream_drain(hipStream_t s) { return hipStreamSynchronize(s); }
+
 // error helpers ---------------------------------------------------------------------------
 int sod_fail(sod_ctx* ctx, int code, const std::string& msg);
 #define SOD_HIP(ctx, call)                                                          \
