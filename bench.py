@@ -498,6 +498,13 @@ def main():
     stage_full = None
     if reserve:
         ctx.set_cu_reserve(0)      # post-processing and extras below on the whole chip
+        # warm the whole-chip configuration as the timed run was warmed: after the idle gaps
+        # of the isolated steps the matcher's clock ramps again (rocprofv3, r03zh: whole-chip
+        # C3 launches 4.52, 4.35, 4.21 ... 3.78 ms over the first ten)
+        for _ in range(a.warmup):
+            turn[0] = 0
+            step()
+        ctx.synchronize()
         # the same stages on the whole chip (the timed run keeps them on the reserved CUs,
         # beside the next query's matcher)
         full = []
