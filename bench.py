@@ -74,6 +74,10 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the SURVEY 8(f) side measurements (query batching, packed DB upload)")
     p.add_argument("--cpu-queries", type=int, default=4096)
+    # events on a dispatch delay the stream's next kernel (~3 us per one-image step measured:
+    # 0.0733 ms per step with every launch timed, 0.0714 every 4th, 0.0704 none; r04 strideab1)
+    p.add_argument("--match-timing-stride", type=int, default=4,
+                   help="HIP begin/end events on every S-th matcher launch of the timed region")
     p.add_argument("--contexts", type=int, default=0,
                    help="query streams over the one resident DB (sod_db_share): consecutive "
                         "query images alternate between them, so one image's Hough/select/"
@@ -451,6 +455,7 @@ def main():
         for c in ctxs:
             c.synchronize()
 
+    stride = max(1, a.match_timing_stride)
     for c in ctxs:
         c.set_stage_timing(False)   # stage events are marker packets on the tail's path
     _progress(rank, "DB resident, %d warmup steps" % a.warmup)
@@ -463,6 +468,8 @@ def main():
     stage = []
     D.barrier()
     sync_all()
+    for c in ctxs:
+        c.set_match_timing(stride)  # counted from the first timed launch
     t0 = time.perf_counter()
     host = 0.0                      # host time spent enqueueing (the calls return unsynced)
     for _ in range(a.steps):
@@ -480,8 +487,10 @@ def main():
     live = []
     for k, c in enumerate(ctxs):
         n_k = len(range(k, a.steps, ncontexts))      # timed launches of context k
-        if n_k:
-            live.extend(c.match_times(min(n_k, 64)).tolist())
+        n_rec = len(range(0, n_k, stride))           # ... that recorded events
+        if n_rec:
+            live.extend(c.match_times(min(n_rec, 64)).tolist())
+        c.set_match_timing(True)
     match_ms = float(np.mean(live))
 
     # ---- per-stage timing (HIP events on the ctx stream), separate untimed steps --------
@@ -637,7 +646,9 @@ def main():
                      "clock_ghz_pmc_profiled": pmc.get("clock_ghz_profiled") if pmc else None,
                      "algorithmic_bytes": alg_bytes,
                      "kernel": kernel,
-                     "algorithmic": "256 op/pair x %d x %d pairs per launch" % (nq, n_shard)},
+                     "algorithmic": "256 op/pair x %d x %d pairs per launch" % (nq, n_shard),
+                     "timed_launches": "HIP begin/end events on one matcher launch in %d of "
+                                       "the timed region" % stride},
         "matcher_impl": a.impl,
         "exact_order": ctx.exact_order(),
         "datagen_s": gen_s,

@@ -69,10 +69,10 @@ int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n);
  * a marker packet on the tail's critical path, so a timed loop turns them off.  With them
  * off, sod_last_stage_ms reports 0 for the stages after the matcher. */
 int sod_set_stage_timing(sod_ctx* ctx, int on);
-/* Begin / end events of every matcher launch (1, the default; sod_match_times and
- * sod_last_match_ms read them) or none (0) when the launch runs on the context stream: a
- * dispatch that records an event delays the stream's next kernel by ~5 us, a share of a
- * one-image step.  Launches on the matcher stream (overlap / CU split) keep their events. */
+/* Begin / end events of every `on`-th int8 matcher launch, counted from this call (1, the
+ * default: every launch; 0: none; sod_match_times and sod_last_match_ms read the recorded
+ * ones): a dispatch that records an event delays its stream's next kernel by ~5 us, a share
+ * of a one-image step.  An untimed matcher-stream launch is joined by a marker event. */
 int sod_set_match_timing(sod_ctx* ctx, int on);
 
 /* ---- database (replaces main.py:36-66 flattening + GenerateDatabaseInfo.py format) --

@@ -409,9 +409,10 @@ class Context:
         return out
 
     def set_match_timing(self, on):
-        """Matcher launch events (sod_set_match_timing; default on): off removes them from
-        context-stream launches, the one-image latency path."""
-        self._chk(self._L.sod_set_match_timing(self._h, 1 if on else 0))
+        """Matcher launch events (sod_set_match_timing; default on = every launch): False / 0
+        records none, an int s every s-th launch from now on."""
+        stride = int(on) if not isinstance(on, bool) else (1 if on else 0)
+        self._chk(self._L.sod_set_match_timing(self._h, stride))
 
     def set_stage_timing(self, on):
         """Record the per-stage events read by stage_ms (default on; off in timed loops)."""

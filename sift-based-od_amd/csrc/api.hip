@@ -146,9 +146,12 @@ int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end) {
 // begin / end events of the next matcher launch, recorded by the launch itself
 // (hipExtLaunchKernelGGL: timestamps in the dispatch, no marker packets around the kernel)
 int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end) {
-  if (!ctx->match_timing && ctx->mk_main) {
-    // untimed launch on the context stream: a dispatch that records an event delays the next
-    // kernel of the stream by ~5 us (rocprofv3, one-image step); nothing waits on these
+  const bool timed = ctx->match_stride > 0 && ctx->mlaunch % ctx->match_stride == 0;
+  ++ctx->mlaunch;
+  if (!timed) {
+    // untimed launch: a dispatch that records an event delays the next kernel of its stream
+    // by ~5 us (rocprofv3, one-image step); the context stream's wait for a matcher-stream
+    // launch then uses a marker (sod_match_stream_end)
     *begin = *end = nullptr;
     return SOD_OK;
   }
@@ -187,8 +190,9 @@ int sod_partials_merged(sod_ctx* ctx) {
 
 int sod_set_match_timing(sod_ctx* ctx, int on) {
   SOD_TRY(set_dev(ctx));
-  if (on != 0 && on != 1) return sod_fail(ctx, SOD_EINVAL, "match timing must be 0 or 1");
-  ctx->match_timing = on != 0;
+  if (on < 0 || on > 1 << 20) return sod_fail(ctx, SOD_EINVAL, "match timing stride must be in [0, 2^20]");
+  ctx->match_stride = on;
+  ctx->mlaunch = 0;
   return SOD_OK;
 }
 

@@ -213,7 +213,10 @@ struct sod_ctx {
   bool overlap = false;
   bool mk_main = true;        // the last matcher launch went on the context stream (idle, no split)
   bool merge_norec[2] = {false, false};   // a slot's last merge released it without an event
-  bool match_timing = true;   // sod_set_match_timing: begin/end events of every matcher launch
+  // sod_set_match_timing: begin/end events of every match_stride-th int8 matcher launch
+  // (0: none); mlaunch counts the launches since the last setting
+  int match_stride = 1;
+  int64_t mlaunch = 0;
   // sod_set_cu_reserve: the top `reserved_cus` CU-mask bits (cu_reserve per XCD, mask bit i
   // is on XCD i % 8) run the context / side streams; the matcher stream gets the rest
   int cu_reserve = 0;
