@@ -1125,7 +1125,7 @@ int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold) {
   if (!ctx->houghed) return sod_fail(ctx, SOD_ESTATE, "sod_hough_enqueue first");
   SOD_TRY(sod_hist_dense(ctx));
   SOD_TRY(sod_stage_mark(ctx, kStageSelect, false));
-  SOD_TRY(launch_select(ctx, vote_threshold));
+  SOD_TRY(launch_select(ctx, vote_threshold, true));
   SOD_TRY(sod_stage_mark(ctx, kStageSelect, true));
   ctx->vote_thr = vote_threshold;
   ctx->selected = true;

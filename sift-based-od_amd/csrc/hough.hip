@@ -494,28 +494,46 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(
   const uint32_t n = q < nq ? first_touch_slots(q, basekey, vmask, gcount, gfirst, b, qb, thr, tmp) : 0;
   uint32_t tot;
   const uint32_t loc = block_excl_scan(n, sh, &tot);
-  if (threadIdx.x == 0) {
-    const uint64_t e4 = (uint64_t)(epoch << 2);
+  if (threadIdx.x < 64) {   // the look-back, by the first wave: 64 predecessors per round
+    const int lane = threadIdx.x;
+    const uint32_t e4 = epoch << 2;
     uint32_t ex = 0;
     if (blk > 0) {
-      __hip_atomic_store(&status[blk], ((e4 | 1u) << 32) | tot, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      for (int j = blk - 1; j >= 0;) {
-        const uint64_t st = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0)
+        __hip_atomic_store(&status[blk], ((uint64_t)(e4 | 1u) << 32) | tot, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      // lane l reads block hi - l; "before block 0" reads as an inclusive prefix of 0.  A
+      // round ends at the nearest inclusive prefix in its window (lowest such lane) once every
+      // word up to it is published, and adds the values up to it; a window with no inclusive
+      // prefix adds all 64 aggregates and moves 64 blocks back.  (One round trip per 64
+      // predecessors: a block-by-block walk was 47 us of C3's one-image tail.)
+      for (int hi = blk - 1;;) {
+        const int j = hi - lane;
+        uint64_t st = (uint64_t)(e4 | 2u) << 32;
+        if (j >= 0) st = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t h = (uint32_t)(st >> 32);
-        if ((h & ~3u) != (uint32_t)e4 || (h & 3u) == 0u) {   // not published yet
+        const uint32_t flag = (h & ~3u) == e4 ? (h & 3u) : 0u;
+        const uint64_t incl = __ballot(flag == 2u), unpub = __ballot(flag == 0u);
+        const int stop = incl ? __builtin_ctzll(incl) : 63;
+        const uint64_t need = stop == 63 ? ~0ull : ((2ull << stop) - 1ull);
+        if (unpub & need) {   // a word the round needs is not published yet
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
-        ex += (uint32_t)st;
-        if ((h & 3u) == 2u) break;
-        --j;
+        uint32_t v = lane <= stop ? (uint32_t)st : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+        ex += v;
+        if (incl) break;
+        hi -= 64;
       }
     }
-    __hip_atomic_store(&status[blk], ((e4 | 2u) << 32) | (ex + tot), __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    if (blk == (int)gridDim.x - 1) *total = ex + tot;
-    excl_s = ex;
+    if (lane == 0) {
+      __hip_atomic_store(&status[blk], ((uint64_t)(e4 | 2u) << 32) | (ex + tot), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if (blk == (int)gridDim.x - 1) *total = ex + tot;
+      excl_s = ex;
+    }
   }
   __syncthreads();
   const uint32_t pos = excl_s + loc;
@@ -1753,11 +1771,13 @@ __global__ __launch_bounds__(256) void affine_kernel(
                    isig, qw, qh, bwh, xf, yf, thr, max_iter, params_in, surv, votes, params, alive);
 }
 
-// The fused one-image path's last launch: the PoseBin means (blocks nA..) beside the affine
-// verification (blocks 0..nA-1), one wave per bin each -- independent stages, so one launch
-// instead of two serial ones on the context stream
+// The PoseBin means (blocks 0..nM-1) beside the affine verification (blocks nM..), one wave
+// per bin each -- independent stages, so one launch on the context stream instead of two
+// serial ones there or a fork to the side stream and back (the fused one-image path, and the
+// staged path when the context has nothing to overlap).  The means go first: their serial
+// chains are the longer stage, and blocks are dispatched in index order.
 __global__ __launch_bounds__(64) void means_affine_kernel(
-    int nA, const uint32_t* __restrict__ scal, const int64_t* __restrict__ voff,
+    int nM, const uint32_t* __restrict__ scal, const int64_t* __restrict__ voff,
     const int32_t* __restrict__ members, const double* __restrict__ pose,
     const int2* __restrict__ msize, const double* __restrict__ rtab, double* __restrict__ means,
     const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
@@ -1765,11 +1785,11 @@ __global__ __launch_bounds__(64) void means_affine_kernel(
     double yf, int thr, uint8_t* __restrict__ surv, int32_t* __restrict__ votes,
     double* __restrict__ params, uint8_t* __restrict__ alive) {
   __shared__ double xs[7][kMeansB];
-  if ((int)blockIdx.x < nA)
-    affine_groups<64>(blockIdx.x, nA, 0, scal, voff, mx, my, qx, qy, isig, qw, qh, nullptr, xf,
-                      yf, thr, 1 << 30, nullptr, surv, votes, params, alive);
+  if ((int)blockIdx.x < nM)
+    means_wave(blockIdx.x, nM, xs, scal, voff, members, pose, msize, rtab, means);
   else
-    means_wave(blockIdx.x - nA, gridDim.x - nA, xs, scal, voff, members, pose, msize, rtab, means);
+    affine_groups<64>(blockIdx.x - nM, gridDim.x - nM, 0, scal, voff, mx, my, qx, qy, isig, qw, qh,
+                      nullptr, xf, yf, thr, 1 << 30, nullptr, surv, votes, params, alive);
 }
 
 }  // namespace
@@ -2058,7 +2078,7 @@ static bool select_multi_forced() {
   return e && e[0] == '1';
 }
 
-int launch_select(sod_ctx* ctx, int32_t thr) {
+int launch_select(sod_ctx* ctx, int32_t thr, bool may_defer_means) {
   const int64_t nq = sod_win_n(ctx);
   std::swap(ctx->scal, ctx->scal_b);
   std::swap(ctx->voff, ctx->voff_b);
@@ -2087,6 +2107,14 @@ int launch_select(sod_ctx* ctx, int32_t thr) {
     SOD_HIP(ctx, hipGetLastError());
   } else {
     SOD_TRY(launch_members_multi(ctx, (uint32_t)thr, nq));
+  }
+  if (may_defer_means && ctx->mk_main && !ctx->n_qimg) {
+    // nothing to overlap (the matcher ran on the context stream): the means wait for the
+    // affine enqueue and run in its launch (means_affine_kernel), with no fork to the side
+    // stream and join back (~8 us of marker on the context stream, and the reader's
+    // cross-stream wait); any other next call runs them alone first (sod_means_flush)
+    ctx->means_deferred = true;
+    return SOD_OK;
   }
   return launch_means(ctx);
 }
@@ -2244,7 +2272,7 @@ int launch_means_affine(sod_ctx* ctx, int32_t qw, int32_t qh, double xf, double 
     SOD_HIP(ctx, hipGetLastError());
   }
   const int nA = std::max(1, ctx->tail_cus() * 8), nM = std::max(1, ctx->tail_cus() * 8);
-  hipLaunchKernelGGL(means_affine_kernel, dim3((unsigned)(nA + nM)), dim3(64), 0, ctx->stream, nA,
+  hipLaunchKernelGGL(means_affine_kernel, dim3((unsigned)(nA + nM)), dim3(64), 0, ctx->stream, nM,
                      ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->pose.p,
                      reinterpret_cast<const int2*>(ctx->msize.p), ctx->rtab.p, ctx->means.p,
                      ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p, ctx->aisig.p, qw, qh, xf, yf,

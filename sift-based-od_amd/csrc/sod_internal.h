@@ -369,7 +369,7 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi);
 // boundary guard: redo the listed matches' x / y bins with glibc cos / sin and, when one
 // changes, the histogram and every stage after it (call before reading any Hough result)
 int sod_guard_resolve(sod_ctx* ctx);
-int launch_select(sod_ctx* ctx, int32_t thr);
+int launch_select(sod_ctx* ctx, int32_t thr, bool may_defer_means = false);
 // the fused one-image Hough + select + gather (hough.hip hough_small_kernel) and the lazy
 // dense histogram after it
 bool sod_hough_small_ok(const sod_ctx* ctx);
