@@ -253,13 +253,16 @@ class Main:
         if self._device_resident():
             self.ctx.affine(self.image_query_size, POS_FACTOR * 4, POS_FACTOR * 4, threshold)
             a = self.ctx.affine_result()
-            off = self._valid_sel[1]["offsets"]
+            off = np.asarray(self._valid_sel[1]["offsets"]).tolist()
+            alive = a["alive"]
+            votes, params = a["votes"].tolist(), a["params"].tolist()   # Python scalars in bulk
+            survived = a["survived"].tolist()
             out = []
             for i, b in enumerate(self.valid_bins):
-                b.keep_device_members(a["alive"][off[i]:off[i + 1]])
-                b.votes = int(a["votes"][i])
-                b.affine_parameters = [float(v) for v in a["params"][i]]
-                if a["survived"][i]:
+                b.keep_device_members(alive[off[i]:off[i + 1]])
+                b.votes = votes[i]
+                b.affine_parameters = params[i]
+                if survived[i]:
                     out.append(b)
             self.valid_bins = out
             self._valid_sel = None
