@@ -77,3 +77,45 @@ def test_from_cv_hands_back_the_callers_objects():
     # without objects: new ones with every field
     bare = Keypoints(t.x, t.y, t.angle, t.octave, t.size, t.response, t.class_id)
     assert _fields(bare.keypoint(0)) == _fields(kps[0])
+
+
+def test_posebins_from_device_equal_two_call_construction():
+    """hough.posebins_from_device builds each bin's attributes in one dict; it must give the
+    same object as PoseBin(...) followed by bind_device(...) (CPU only: a synthetic
+    selection)."""
+    from sift_based_od_amd.hough import posebins_from_device
+    from sift_based_od_amd.posebin import PoseBin
+    rng = np.random.default_rng(3)
+    V = 40
+    votes = rng.integers(1, 6, V).astype(np.int32)
+    votes[:3] = 1
+    off = np.concatenate([[0], np.cumsum(votes)]).astype(np.int64)
+    res = {"keys": rng.integers(0, 32, (V, 4)).astype(np.int32), "votes": votes,
+           "offsets": off, "members": rng.integers(0, 900, off[-1]).astype(np.int32),
+           "means": rng.random((V, 6))}
+
+    def pair_of(q):
+        return ("m%d" % q, "q%d" % q)
+
+    def size_of(q):
+        return (640 + q % 3, 480)
+
+    got = posebins_from_device(res, pair_of, size_of, token=9)
+    for i, b in enumerate(got):
+        m = res["members"][off[i]:off[i + 1]]
+        mu = res["means"][i]
+        size = size_of(int(m[0])) if votes[i] == 1 else (float(mu[4]), float(mu[5]))
+        ref = PoseBin(tuple(int(v) for v in res["keys"][i]), size, int(votes[i]), None,
+                      tuple(float(v) for v in mu[:4]))
+        ref.bind_device(9, i, m, pair_of)
+        assert sorted(b.__dict__) == sorted(ref.__dict__)
+        for k, v in ref.__dict__.items():
+            w = b.__dict__[k]
+            if k in ("_lazy", "_dev"):
+                assert len(v) == len(w) and all(
+                    (x is y) or np.array_equal(x, y) if isinstance(x, np.ndarray) else x == y
+                    for x, y in zip(v, w)), k
+            else:
+                assert type(w) is type(v) and w == v, k
+        assert b.device_index(9) == i and b.keypoint_pairs == ref.keypoint_pairs
+        assert type(b.votes) is int and all(type(x) is float for x in b.centroid)
