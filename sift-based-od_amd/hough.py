@@ -8,6 +8,8 @@ device without a host round trip.
 """
 from __future__ import annotations
 
+import gc
+
 import numpy as np
 
 from . import _lib
@@ -63,7 +65,18 @@ def posebins_from_device(res, pair_of, size_of=None, token=None):
     ``size_of(q)`` the model image size (ints) used when a bin has a single vote (the
     reference keeps the int tuple then).  ``token`` names the device selection the bins
     are bound to (``PoseBin.bind_device``)."""
-    out = []
+    # no cyclic-GC passes while ~10^4 containers are made (they were half the time at C3;
+    # none of these objects forms a cycle)
+    gc_was_on = gc.isenabled()
+    gc.disable()
+    try:
+        return _posebins(res, pair_of, size_of, token)
+    finally:
+        if gc_was_on:
+            gc.enable()
+
+
+def _posebins(res, pair_of, size_of, token):
     mem = res["members"]
     # Python scalars in bulk (tolist): per-element numpy indexing was ~2 us per bin, 3 ms of
     # main.py's get_valid_bins at C3 (1 163 bins)
@@ -75,6 +88,7 @@ def posebins_from_device(res, pair_of, size_of=None, token=None):
     # pair_of), its attributes set in one dict (the two calls cost ~1 us per bin on the host;
     # tests/test_keypoints.py checks the two constructions give equal objects)
     new = object.__new__
+    out = []
     for i, key in enumerate(keys):
         a, e = off[i], off[i + 1]
         m = mem[a:e]

@@ -253,13 +253,18 @@ class Main:
         if self._device_resident():
             self.ctx.affine(self.image_query_size, POS_FACTOR * 4, POS_FACTOR * 4, threshold)
             a = self.ctx.affine_result()
-            off = np.asarray(self._valid_sel[1]["offsets"]).tolist()
-            alive = a["alive"]
+            offs = np.asarray(self._valid_sel[1]["offsets"])
+            off = offs.tolist()
+            alive = a["alive"].astype(bool)
+            # every bin's surviving members with one mask (per-bin masking was ~1 us a bin)
+            kept = np.asarray(self._valid_sel[1]["members"])[alive]
+            koff = np.concatenate([[0], np.cumsum(np.add.reduceat(alive.astype(np.int64), offs[:-1]))]).tolist() \
+                if len(off) > 1 else [0]
             votes, params = a["votes"].tolist(), a["params"].tolist()   # Python scalars in bulk
             survived = a["survived"].tolist()
             out = []
             for i, b in enumerate(self.valid_bins):
-                b.keep_device_members(alive[off[i]:off[i + 1]])
+                b.keep_device_members(alive[off[i]:off[i + 1]], kept[koff[i]:koff[i + 1]])
                 b.votes = votes[i]
                 b.affine_parameters = params[i]
                 if survived[i]:

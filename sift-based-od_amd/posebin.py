@@ -90,16 +90,18 @@ class PoseBin:
                 return None
         return d[1]
 
-    def keep_device_members(self, alive):
+    def keep_device_members(self, alive, kept=None):
         """After a device step on the bound members (the affine outlier removal): keep the
         members where ``alive`` (bool, member order) -- built objects stay the same objects,
-        unbuilt ones stay lazy."""
+        unbuilt ones stay lazy.  ``kept``: the surviving members, when the caller selected
+        them for many bins at once."""
         _, _, members, snap = self._dev
-        alive = np.asarray(alive, bool)
         if self._lazy is None:
-            self._pairs = [p for p, k in zip(self._pairs, alive) if k]
+            self._pairs = [p for p, k in zip(self._pairs, np.asarray(alive, bool)) if k]
         else:
-            self._lazy = (self._lazy[0], np.asarray(members)[alive])
+            if kept is None:
+                kept = np.asarray(members)[np.asarray(alive, bool)]
+            self._lazy = (self._lazy[0], kept)
         self._dev = None
 
     # ---- per-vote updates (PoseBin.py:19-54) --------------------------------------------
