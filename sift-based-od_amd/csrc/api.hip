@@ -149,10 +149,13 @@ int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end) {
   const bool timed = ctx->match_stride > 0 && ctx->mlaunch % ctx->match_stride == 0;
   ++ctx->mlaunch;
   if (!timed) {
-    // untimed launch: a dispatch that records an event delays the next kernel of its stream
-    // by ~5 us (rocprofv3, one-image step); the context stream's wait for a matcher-stream
-    // launch then uses a marker (sod_match_stream_end)
-    *begin = *end = nullptr;
+    // untimed launch: no begin event (a dispatch that records one delays the next kernel of
+    // its stream); a matcher-stream launch still records its completion, which the context
+    // stream waits for -- by the dispatch itself: against a marker packet after the kernel,
+    // one image 0.0694 vs 0.0722 ms per step, C2 0.1203 vs 0.1245 (three A/B rounds on one
+    // box, tools/gpu_endev_ab.sh)
+    *begin = nullptr;
+    *end = ctx->mk_main ? nullptr : ctx->ev_matched;
     return SOD_OK;
   }
   hipEvent_t* e = ctx->mev[ctx->nmatch % sod_ctx::kMatchRing];
@@ -300,7 +303,8 @@ int sod_create(int device, sod_ctx** out) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_inputs, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i)
     e = hipEventCreateWithFlags(&ctx->ev_merged[i], hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_matched, hipEventDisableTiming);
+  // (timing-capable: untimed matcher-stream launches record it as their dispatch's stop event)
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_matched);
   if (e != hipSuccess) {
     g_err = std::string("sod_create: ") + hipGetErrorString(e);
     delete ctx;

@@ -516,6 +516,58 @@ def test_matcher_overlap_equals_serial(use_comm, reserve, affine):
             assert np.array_equal(a0["params"], a1["params"])
 
 
+@pytest.mark.parametrize("nq", [600, 3000])
+def test_untimed_split_launches_equal_serial(nq):
+    """Under the CU split a matcher launch without timing events signals the context stream
+    by the completion event its own dispatch records (no marker packet): back-to-back
+    pipelines with different thresholds and a new query upload in between -- the merge must
+    still wait for the kernel, and the upload for the kernel reading the old queries; every
+    result equals the serial context's."""
+    db = synthetic.make_database(60, 1000, seed=61)
+    qsets = [synthetic.make_queries(nq, seed=62 + k, db_seed=61, kp_per_image=1000)
+             for k in range(3)]
+    bins = (32, 32, 8, 12)
+
+    def collect(c):
+        return c.match_result(), c.valid_result(), c.affine_result(), c.all_bins()
+
+    ref = []
+    with _lib.Context(0) as c:
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        for qs in qsets:
+            c.upload_queries(qs.des, qs.kp)
+            for thr in (3, 5):
+                c.pipeline(qs.shape, bins, vote_threshold=thr)
+                ref.append(collect(c))
+    got = []
+    with _lib.Context(0) as c:
+        c.set_cu_reserve(1)
+        c.set_match_timing(0)
+        c.set_stage_timing(False)
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        for qs in qsets:
+            # right behind the previous set's back-to-back matchers; the first two launches
+            # after it find both partial-result slots holding the previous queries' results
+            # (a merge that did not wait for its kernel would read those)
+            c.upload_queries(qs.des, qs.kp)
+            for thr in (3, 5):
+                c.pipeline(qs.shape, bins, vote_threshold=thr)
+                got.append(collect(c))
+            for _ in range(3):                # back to back, nothing read in between
+                c.pipeline(qs.shape, bins, vote_threshold=5)
+        c.set_cu_reserve(0)
+    for (m0, v0, a0, b0), (m1, v1, a1, b1) in zip(ref, got):
+        for x, y in zip(m0, m1):
+            assert np.array_equal(x, y)
+        for k in ("keys", "votes", "offsets", "members", "means"):
+            assert np.array_equal(v0[k], v1[k]), k
+        assert np.array_equal(b0[0], b1[0]) and np.array_equal(b0[1], b1[1])
+        assert np.array_equal(a0["survived"], a1["survived"])
+        assert np.array_equal(a0["params"], a1["params"])
+
+
 def test_cu_reserve_channel_cap():
     """The CU split runs collectives on the reserved CUs only, so every block of an RCCL
     kernel must fit there: a communicator created under the split gets maxCTAs = the reserved
