@@ -20,6 +20,13 @@ c = _lib.Context(0)
 m = Main(c)
 m.set_database(SiftDatabase(db.des, db.kp, db.img, db.centroid, db.size))
 m.get_query_features(qs.des, qs.kp, qs.shape)
+for rep in range(3):   # run_matcher's parts
+    t = {}
+    t0 = time.perf_counter(); c.match(); c.synchronize(); t["match+sync"] = time.perf_counter() - t0
+    t0 = time.perf_counter(); c.ratio(0.75); c.synchronize(); t["ratio+sync"] = time.perf_counter() - t0
+    t0 = time.perf_counter(); c.float_order(); c.synchronize(); t["float_order"] = time.perf_counter() - t0
+    t0 = time.perf_counter(); r = c.match_result(); t["match_result"] = time.perf_counter() - t0
+    print("matcher parts", {k: round(v * 1e3, 3) for k, v in t.items()}, flush=True)
 for rep in range(4):
     t = {}
     t0 = time.perf_counter(); m.run_matcher(); t["run_matcher"] = time.perf_counter() - t0
