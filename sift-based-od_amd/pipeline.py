@@ -20,6 +20,8 @@ outside.
 """
 from __future__ import annotations
 
+import gc
+
 import numpy as np
 
 from . import _lib
@@ -263,12 +265,18 @@ class Main:
             votes, params = a["votes"].tolist(), a["params"].tolist()   # Python scalars in bulk
             survived = a["survived"].tolist()
             out = []
-            for i, b in enumerate(self.valid_bins):
-                b.keep_device_members(alive[off[i]:off[i + 1]], kept[koff[i]:koff[i + 1]])
-                b.votes = votes[i]
-                b.affine_parameters = params[i]
-                if survived[i]:
-                    out.append(b)
+            gc_was_on = gc.isenabled()
+            gc.disable()          # (no cycles among these; GC passes were a third of the loop)
+            try:
+                for i, b in enumerate(self.valid_bins):
+                    b.keep_device_members(alive[off[i]:off[i + 1]], kept[koff[i]:koff[i + 1]])
+                    b.votes = votes[i]
+                    b.affine_parameters = params[i]
+                    if survived[i]:
+                        out.append(b)
+            finally:
+                if gc_was_on:
+                    gc.enable()
             self.valid_bins = out
             self._valid_sel = None
             self.affine_path = "device-resident"
