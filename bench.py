@@ -76,6 +76,9 @@ def parse():
     p.add_argument("--cpu-queries", type=int, default=4096)
     # events on a dispatch delay the stream's next kernel (~3 us per one-image step measured:
     # 0.0733 ms per step with every launch timed, 0.0714 every 4th, 0.0704 none; r04 strideab1)
+    p.add_argument("--matcher-streams", type=int, default=1, choices=[1, 2],
+                   help="2: one matcher stream per partial-result slot (launches overlap; "
+                        "their events then span the overlap)")
     p.add_argument("--match-timing-stride", type=int, default=4,
                    help="HIP begin/end events on every S-th matcher launch of the timed region")
     p.add_argument("--contexts", type=int, default=0,
@@ -423,6 +426,8 @@ def main():
     if reserve:
         ctx.set_cu_reserve(reserve)
         overlap = 1                 # the split runs the matcher on its own stream
+    if a.matcher_streams != 1:
+        ctx.set_matcher_streams(a.matcher_streams)
     comm = None
     if world > 1 and a.comm == "rccl":
         # created under the split: sod_comm_init gives the communicator maxCTAs = the
@@ -612,7 +617,7 @@ def main():
             "queries": nq, "db_rows_per_gpu": n_shard, "db_rows_total": world * n_shard,
             "bins": list(bins), "parallelism": "db-shard%d" % world,
             "query_streams": ncontexts, "matcher_overlap": bool(overlap),
-            "cu_reserve_per_xcd": reserve,
+            "cu_reserve_per_xcd": reserve, "matcher_streams": a.matcher_streams,
             "comm": a.comm if world > 1 else None},
         "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
         "hough_stage_votes_per_s": n_votes / (t_hough / 1000.0),

@@ -74,6 +74,11 @@ int sod_set_stage_timing(sod_ctx* ctx, int on);
  * ones): a dispatch that records an event delays its stream's next kernel by ~5 us, a share
  * of a one-image step.  An untimed matcher-stream launch is joined by a marker event. */
 int sod_set_match_timing(sod_ctx* ctx, int on);
+/* Matcher streams with sod_match_set_overlap / sod_set_cu_reserve: 1 (default) = one stream
+ * for both partial-result slots; 2 = one per slot, so consecutive launches overlap at their
+ * boundary (higher throughput for mid-size query sets; a launch's events then span the
+ * overlap).  Results are unchanged. */
+int sod_set_matcher_streams(sod_ctx* ctx, int n);
 
 /* ---- database (replaces main.py:36-66 flattening + GenerateDatabaseInfo.py format) --
  * Keypoints and the per-image table cover the WHOLE database (replicated on every

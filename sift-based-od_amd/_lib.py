@@ -51,6 +51,7 @@ SIGNATURES = {
     "sod_last_stage_ms": (C.c_int, [c_ctx, c_f32p, C.c_int]),
     "sod_set_stage_timing": (C.c_int, [c_ctx, C.c_int]),
     "sod_set_match_timing": (C.c_int, [c_ctx, C.c_int]),
+    "sod_set_matcher_streams": (C.c_int, [c_ctx, C.c_int]),
     "sod_db_set_keypoints": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_i32p,
                                        C.c_int32, c_f64p, c_i32p]),
     "sod_db_upload_descriptors": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int64, C.c_int64]),
@@ -413,6 +414,10 @@ class Context:
         records none, an int s every s-th launch from now on."""
         stride = int(on) if not isinstance(on, bool) else (1 if on else 0)
         self._chk(self._L.sod_set_match_timing(self._h, stride))
+
+    def set_matcher_streams(self, n):
+        """1 (default) or 2 matcher streams (sod_set_matcher_streams)."""
+        self._chk(self._L.sod_set_matcher_streams(self._h, int(n)))
 
     def set_stage_timing(self, on):
         """Record the per-stage events read by stage_ms (default on; off in timed loops)."""

@@ -77,7 +77,10 @@ static int wait_unless_done(sod_ctx* ctx, hipStream_t s, hipEvent_t ev) {
   return SOD_OK;
 }
 int sod_inputs_begin(sod_ctx* ctx) {
-  SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_matched_p ? ctx->ev_matched_p : ctx->ev_matched, 0));
+  // every matcher launch still reading the inputs: the last one of each slot (two may be in
+  // flight on the two matcher streams); context-stream launches are ordered already
+  for (int x = 0; x < 2; ++x)
+    if (ctx->ev_done[x]) SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_done[x], 0));
   return SOD_OK;
 }
 int sod_inputs_end(sod_ctx* ctx) {
@@ -95,6 +98,7 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
   const int nslot = ctx->overlap ? 2 : 1;
   if (ctx->pd1.n < (size_t)(nslot * n)) {   // growing: no kernel or merge may still use them
     SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+    SOD_HIP(ctx, sod_stream_sync(ctx->mstream2));
     SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   }
   SOD_TRY(sod_reserve(ctx, ctx->pd1, (size_t)(nslot * n)));
@@ -111,13 +115,14 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
   // the merge after it needs no cross-stream wait (~10 us on the one-image path, where the
   // whole step is ~0.1 ms).  The slot protocol below is unchanged either way.
   ctx->mk_main = !ctx->overlap ||
-                 (ctx->cu_reserve == 0 && stream_idle(ctx->stream) && stream_idle(ctx->mstream));
+                 (ctx->cu_reserve == 0 && stream_idle(ctx->stream) && stream_idle(ctx->mstream) &&
+                  stream_idle(ctx->mstream2));
   if (ctx->mk_main) {
     *ks = ctx->stream;
     if (ctx->overlap) SOD_HIP(ctx, hipEventSynchronize(ctx->ev_merged[ctx->pslot]));
     return SOD_OK;
   }
-  *ks = ctx->mstream;
+  *ks = ctx->mstream_of(ctx->pslot);
   // merges that ran on the context stream right after a context-stream matcher released
   // their slot without an event (sod_partials_merged): mark them now
   for (int x = 0; x < 2; ++x)
@@ -125,7 +130,7 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
       SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[x], ctx->stream));
       ctx->merge_norec[x] = false;
     }
-  SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_inputs));
+  SOD_TRY(wait_unless_done(ctx, *ks, ctx->ev_inputs));
   // the slot's previous merge (two launches back) must be done before the kernel rewrites
   // it: the host waits for it here rather than the matcher stream (a satisfied barrier packet
   // between two back-to-back matcher launches costs ~6 us per launch, C2 0.166 vs 0.160 ms per
@@ -133,7 +138,7 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
   // ran right after the launch before the previous one, so the wait is normally over already
   SOD_HIP(ctx, hipEventSynchronize(ctx->ev_merged[ctx->pslot]));
   // a new slot size moves the slots' boundaries: the other slot's last merge must be done too
-  if (resized) SOD_TRY(wait_unless_done(ctx, ctx->mstream, ctx->ev_merged[ctx->pslot ^ 1]));
+  if (resized) SOD_TRY(wait_unless_done(ctx, *ks, ctx->ev_merged[ctx->pslot ^ 1]));
   return SOD_OK;
 }
 int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end) {
@@ -155,7 +160,7 @@ int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end) {
     // one image 0.0694 vs 0.0722 ms per step, C2 0.1203 vs 0.1245 (three A/B rounds on one
     // box, tools/gpu_endev_ab.sh)
     *begin = nullptr;
-    *end = ctx->mk_main ? nullptr : ctx->ev_matched;
+    *end = ctx->mk_main ? nullptr : (ctx->pslot ? ctx->ev_matched1 : ctx->ev_matched);
     return SOD_OK;
   }
   hipEvent_t* e = ctx->mev[ctx->nmatch % sod_ctx::kMatchRing];
@@ -167,16 +172,19 @@ int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end) {
   return SOD_OK;
 }
 int sod_match_stream_end(sod_ctx* ctx, hipEvent_t done) {
-  const hipStream_t ks = ctx->mk_main ? ctx->stream : ctx->mstream;
+  const hipStream_t ks = ctx->mk_main ? ctx->stream : ctx->mstream_of(ctx->pslot);
+  if (ctx->mk_main) ctx->ev_done[0] = ctx->ev_done[1] = nullptr;   // stream order from here on
   if (!done && ctx->mk_main) {   // stream order covers every reader: no event
     ctx->ev_matched_p = nullptr;
     return SOD_OK;
   }
   if (!done) {
-    SOD_HIP(ctx, hipEventRecord(ctx->ev_matched, ks));
-    done = ctx->ev_matched;
+    hipEvent_t ev = ctx->pslot ? ctx->ev_matched1 : ctx->ev_matched;
+    SOD_HIP(ctx, hipEventRecord(ev, ks));
+    done = ev;
   }
   ctx->ev_matched_p = done;
+  if (!ctx->mk_main) ctx->ev_done[ctx->pslot] = done;
   if (!ctx->mk_main) SOD_HIP(ctx, hipStreamWaitEvent(ctx->stream, done, 0));
   return SOD_OK;
 }
@@ -188,6 +196,22 @@ int sod_match_stream_end(sod_ctx* ctx, hipEvent_t done) {
 int sod_partials_merged(sod_ctx* ctx) {
   ctx->merge_norec[ctx->pslot] = ctx->mk_main && ctx->overlap;
   if (!ctx->mk_main) SOD_HIP(ctx, hipEventRecord(ctx->ev_merged[ctx->pslot], ctx->stream));
+  return SOD_OK;
+}
+
+// One matcher stream for both partial-result slots (1, the default) or one per slot (2):
+// consecutive launches then overlap at their boundary -- the next launch's work-groups start
+// on the CUs the previous one's finished work-groups leave.  Measured (r04 ms1, one box): C2
+// 0.1124 vs 0.1206 ms per step, C3 3.696 vs 3.745, one image 0.0749 vs 0.0678 (worse); a
+// launch's begin/end events then span the overlap, so the per-launch time is not the kernel's.
+int sod_set_matcher_streams(sod_ctx* ctx, int n) {
+  SOD_TRY(set_dev(ctx));
+  if (n != 1 && n != 2) return sod_fail(ctx, SOD_EINVAL, "matcher streams must be 1 or 2");
+  SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->mstream2));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
+  ctx->mtwo = n == 2;
+  ctx->ev_done[0] = ctx->ev_done[1] = nullptr;
   return SOD_OK;
 }
 
@@ -221,6 +245,7 @@ static void db_detach(sod_ctx* ctx) {
 static void drain_streams(sod_ctx* ctx) {
   if (ctx->side) (void)sod_stream_drain(ctx->side);
   if (ctx->mstream) (void)sod_stream_drain(ctx->mstream);
+  if (ctx->mstream2) (void)sod_stream_drain(ctx->mstream2);
   if (ctx->stream) (void)sod_stream_drain(ctx->stream);
 }
 
@@ -300,11 +325,13 @@ int sod_create(int device, sod_ctx** out) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->mstream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->mstream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_inputs, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i)
     e = hipEventCreateWithFlags(&ctx->ev_merged[i], hipEventDisableTiming);
   // (timing-capable: untimed matcher-stream launches record it as their dispatch's stop event)
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_matched);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_matched1);
   if (e != hipSuccess) {
     g_err = std::string("sod_create: ") + hipGetErrorString(e);
     delete ctx;
@@ -325,6 +352,7 @@ void sod_destroy(sod_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->side) (void)sod_stream_drain(ctx->side);
   if (ctx->mstream) (void)sod_stream_drain(ctx->mstream);
+  if (ctx->mstream2) (void)sod_stream_drain(ctx->mstream2);
   if (ctx->stream) (void)sod_stream_drain(ctx->stream);
   db_detach(ctx);
   // contexts still aliasing this DB: let their queued work finish, then drop their views
@@ -379,7 +407,9 @@ void sod_destroy(sod_ctx* ctx) {
   for (auto& ev : ctx->ev_merged)
     if (ev) (void)hipEventDestroy(ev);
   if (ctx->ev_matched) (void)hipEventDestroy(ctx->ev_matched);
+  if (ctx->ev_matched1) (void)hipEventDestroy(ctx->ev_matched1);
   if (ctx->mstream) (void)hipStreamDestroy(ctx->mstream);
+  if (ctx->mstream2) (void)hipStreamDestroy(ctx->mstream2);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -391,6 +421,7 @@ const char* sod_last_error(const sod_ctx* ctx) {
 int sod_synchronize(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx));
   SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->mstream2));
   SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   return SOD_OK;
 }
@@ -751,9 +782,11 @@ int sod_match_enqueue(sod_ctx* ctx) {
 int sod_match_set_overlap(sod_ctx* ctx, int on) {
   SOD_TRY(set_dev(ctx));
   if (on != 0 && on != 1) return sod_fail(ctx, SOD_EINVAL, "overlap must be 0 or 1");
-  // everything enqueued so far, on either stream, is ordered before the switch
+  // everything enqueued so far, on any stream, is ordered before the switch
   SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->mstream2));
   SOD_HIP(ctx, sod_stream_sync(ctx->stream));
+  ctx->ev_done[0] = ctx->ev_done[1] = nullptr;
   if (!on && ctx->cu_reserve)
     return sod_fail(ctx, SOD_ESTATE, "the CU split (sod_set_cu_reserve) needs the matcher stream");
   ctx->overlap = on != 0;
@@ -808,8 +841,10 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
                  per_xcd, (void*)ctx->stream, (void*)ctx->side, (void*)ctx->mstream);
   SOD_HIP(ctx, sod_stream_drain(ctx->side));
   SOD_HIP(ctx, sod_stream_drain(ctx->mstream));
+  SOD_HIP(ctx, sod_stream_drain(ctx->mstream2));
   SOD_HIP(ctx, sod_stream_drain(ctx->stream));
   ctx->side_pending = false;
+  ctx->ev_done[0] = ctx->ev_done[1] = nullptr;
   const bool dbg = std::getenv("SOD_DEBUG_SYNC") != nullptr;
   if (dbg) std::fprintf(stderr, "sod: cu_reserve streams idle\n");
   const int n = ctx->num_cus, words = (n + 31) / 32, r = per_xcd * nx;
@@ -819,23 +854,27 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
     match.assign(words, 0u);
     for (int i = 0; i < n; ++i) (i >= n - r ? tail : match)[i / 32] |= 1u << (i % 32);
   }
-  hipStream_t s = nullptr, sd = nullptr, ms = nullptr;
+  hipStream_t s = nullptr, sd = nullptr, ms = nullptr, ms2 = nullptr;
   hipError_t e = make_stream(&s, tail);
   if (e == hipSuccess) e = make_stream(&sd, tail);
   if (e == hipSuccess) e = make_stream(&ms, match);
+  if (e == hipSuccess) e = make_stream(&ms2, match);
   if (e != hipSuccess) {
     if (s) (void)hipStreamDestroy(s);
     if (sd) (void)hipStreamDestroy(sd);
+    if (ms) (void)hipStreamDestroy(ms);
     return sod_fail(ctx, SOD_EHIP, std::string("cu reserve: ") + hipGetErrorString(e));
   }
   if (dbg) std::fprintf(stderr, "sod: cu_reserve new streams %p %p %p\n", (void*)s, (void*)sd, (void*)ms);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->mstream);
+  (void)hipStreamDestroy(ctx->mstream2);
   if (dbg) std::fprintf(stderr, "sod: cu_reserve old streams destroyed\n");
   ctx->stream = s;
   ctx->side = sd;
   ctx->mstream = ms;
+  ctx->mstream2 = ms2;
   ctx->cu_reserve = per_xcd;
   ctx->reserved_cus = r;
   if (per_xcd > 0) ctx->overlap = true;

@@ -1322,9 +1322,13 @@ int launch_match_i8(sod_ctx* ctx) {
     if (ctx->gthr.n < (size_t)(2 * gslot) || ctx->gthr_n != nq_pad) {
       if (ctx->gthr.n < (size_t)(2 * gslot)) {
         SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
+        SOD_HIP(ctx, sod_stream_sync(ctx->mstream2));
         SOD_HIP(ctx, sod_stream_sync(ctx->stream));
         SOD_TRY(sod_reserve(ctx, ctx->gthr, (size_t)(2 * gslot)));
       }
+      // (a new layout: the other slot's matcher, possibly still running on the other matcher
+      // stream, must not write bounds of the old layout into it)
+      if (ctx->mtwo && !ctx->mk_main) SOD_HIP(ctx, sod_stream_sync(ctx->mstream_of(ctx->pslot ^ 1)));
       SOD_HIP(ctx, hipMemsetAsync(ctx->gthr.p, 0x80, (size_t)(2 * gslot) * 4, ks));
       ctx->gthr_n = nq_pad;
     }

@@ -206,9 +206,16 @@ struct sod_ctx {
   // ---- matcher stream (sod_match_set_overlap): the match kernel runs there and waits only
   // for the last input upload (ev_inputs) and for the merge that last read its partial-result
   // slot (two slots alternate: ev_merged[slot])
-  hipStream_t mstream = nullptr;
-  hipEvent_t ev_inputs = nullptr, ev_matched = nullptr, ev_merged[2] = {nullptr, nullptr};
+  // Optionally two matcher streams, one per partial-result slot (mstream: slot 0, mstream2:
+  // slot 1), so launch k+1's work-groups take the CUs launch k's finished work-groups leave
+  // instead of waiting for its slowest one (sod_set_matcher_streams; mtwo)
+  hipStream_t mstream = nullptr, mstream2 = nullptr;
+  bool mtwo = false;
+  hipEvent_t ev_inputs = nullptr, ev_merged[2] = {nullptr, nullptr};
+  hipEvent_t ev_matched = nullptr, ev_matched1 = nullptr;   // untimed completion, per slot
   hipEvent_t ev_matched_p = nullptr;   // the last matcher launch's completion event
+  hipEvent_t ev_done[2] = {nullptr, nullptr};   // each slot's last matcher-stream completion
+  hipStream_t mstream_of(int slot) const { return mtwo && slot ? mstream2 : mstream; }
   bool stage_timing = true;   // sod_set_stage_timing: ev[2..5] around the tail stages
   bool overlap = false;
   bool mk_main = true;        // the last matcher launch went on the context stream (idle, no split)

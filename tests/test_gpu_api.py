@@ -516,8 +516,8 @@ def test_matcher_overlap_equals_serial(use_comm, reserve, affine):
             assert np.array_equal(a0["params"], a1["params"])
 
 
-@pytest.mark.parametrize("nq", [600, 3000])
-def test_untimed_split_launches_equal_serial(nq):
+@pytest.mark.parametrize("nq,streams", [(600, 1), (3000, 1), (600, 2), (3000, 2)])
+def test_untimed_split_launches_equal_serial(nq, streams):
     """Under the CU split a matcher launch without timing events signals the context stream
     by the completion event its own dispatch records (no marker packet): back-to-back
     pipelines with different thresholds and a new query upload in between -- the merge must
@@ -543,6 +543,7 @@ def test_untimed_split_launches_equal_serial(nq):
     got = []
     with _lib.Context(0) as c:
         c.set_cu_reserve(1)
+        c.set_matcher_streams(streams)   # 2: consecutive launches overlap on two streams
         c.set_match_timing(0)
         c.set_stage_timing(False)
         c.set_keypoints(db.kp, db.img, db.centroid, db.size)
