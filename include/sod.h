@@ -248,6 +248,16 @@ int sod_postprocess(sod_ctx* ctx, int32_t* n_bins, int32_t* bin_index /* [n] val
                     int32_t* n_pos, int32_t* pos_off, int32_t* pos_members, int32_t* n_ori,
                     int32_t* ori_pos_off, int32_t* ori_off, int32_t* ori_members,
                     double* final_orientation, double* final_pose);
+/* sod_postprocess's input means: 1 (default) = the survivors' x / y PoseBin means redone
+ * on the host with glibc cos / sin per member (the calls math.cos / math.sin make,
+ * HoughTransformHelperFunctions.py:31-32), so the position relation's <= thresholds
+ * (PostProcessing.py:24-28) and the final pose see the reference's values bit for bit;
+ * 0 = the device means (device cos / sin: within ~1e-12, no host pass). */
+int sod_set_post_exact(sod_ctx* ctx, int on);
+/* The x / y PoseBin means (PoseBin.py:45-51) of valid bins vbin[0..nb) as the reference
+ * computes them (glibc cos / sin per member pose, HoughTransformHelperFunctions.py:31-32),
+ * into xy[2*nb]; what sod_postprocess uses when sod_set_post_exact is on. */
+int sod_exact_means(sod_ctx* ctx, int32_t nb, const int32_t* vbin, double* xy);
 /* the same on caller-supplied PoseBin means [n*6] = (x, y, angle, scale, w, h) */
 int sod_post_batch(sod_ctx* ctx, int32_t n, const double* means, int32_t* n_pos,
                    int32_t* pos_off, int32_t* pos_members, int32_t* n_ori,

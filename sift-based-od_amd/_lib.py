@@ -52,6 +52,8 @@ SIGNATURES = {
     "sod_set_stage_timing": (C.c_int, [c_ctx, C.c_int]),
     "sod_set_match_timing": (C.c_int, [c_ctx, C.c_int]),
     "sod_set_matcher_streams": (C.c_int, [c_ctx, C.c_int]),
+    "sod_set_post_exact": (C.c_int, [c_ctx, C.c_int]),
+    "sod_exact_means": (C.c_int, [c_ctx, C.c_int32, c_i32p, c_f64p]),
     "sod_db_set_keypoints": (C.c_int, [c_ctx, C.c_int64, c_f32p, c_f32p, c_f32p, c_i32p, c_i32p,
                                        C.c_int32, c_f64p, c_i32p]),
     "sod_db_upload_descriptors": (C.c_int, [c_ctx, c_vp, C.c_int, C.c_int64, C.c_int64]),
@@ -414,6 +416,18 @@ class Context:
         records none, an int s every s-th launch from now on."""
         stride = int(on) if not isinstance(on, bool) else (1 if on else 0)
         self._chk(self._L.sod_set_match_timing(self._h, stride))
+
+    def exact_means(self, vbin):
+        """(len(vbin), 2) x / y PoseBin means of those valid bins as the reference computes
+        them (sod_exact_means)."""
+        vb = np.ascontiguousarray(vbin, np.int32)
+        out = np.zeros((len(vb), 2), np.float64)
+        self._chk(self._L.sod_exact_means(self._h, len(vb), ptr(vb, C.c_int32), ptr(out, C.c_double)))
+        return out
+
+    def set_post_exact(self, on):
+        """postprocess() on the survivors' x / y means redone with glibc (default True)."""
+        self._chk(self._L.sod_set_post_exact(self._h, 1 if on else 0))
 
     def set_matcher_streams(self, n):
         """1 (default) or 2 matcher streams (sod_set_matcher_streams)."""

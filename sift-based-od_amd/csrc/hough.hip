@@ -72,16 +72,26 @@ __device__ __forceinline__ void bin_index(double x, double y, double a, int k, i
 
 // estimate_object_pose (HTHF:4-37) + calculate_bin_index (HTHF:39-72); t = the translation
 // (tx, ty) the rotation acts on, for the boundary guard below
+// the pose's terms before the rotation (HTHF:20-30): scale exponent k, s = 2^k, the
+// translation (tx, ty) the rotation acts on, the angle a in [0, 2 pi)
+__device__ __forceinline__ void pose_terms(float mx, float my, float ma, int mo, float qa, int qo,
+                                           double cx, double cy, int& k, double& s, double& tx,
+                                           double& ty, double& a) {
+  k = unpack_octave(qo) - unpack_octave(mo);  // m_scale / q_scale = 2^(oQ-oM), exact
+  s = ldexp(1.0, k);
+  tx = (cx - (double)mx) * s;
+  ty = (cy - (double)my) * s;
+  a = ((double)qa - (double)ma) * kDeg2Rad;
+  a = fmod(a + kTwoPi, kTwoPi);   // argument > 0, so Python % == C fmod
+}
+
 __device__ __forceinline__ void pose_bins(float mx, float my, float ma, int mo, float qx, float qy,
                                           float qa, int qo, double cx, double cy, int H, int W,
                                           Bins b, const int* __restrict__ lut, double pose[4],
                                           int idx[4], double t[2]) {
-  const int k = unpack_octave(qo) - unpack_octave(mo);  // m_scale / q_scale = 2^(oQ-oM), exact
-  const double s = ldexp(1.0, k);
-  const double tx = (cx - (double)mx) * s;
-  const double ty = (cy - (double)my) * s;
-  double a = ((double)qa - (double)ma) * kDeg2Rad;
-  a = fmod(a + kTwoPi, kTwoPi);   // argument > 0, so Python % == C fmod
+  int k;
+  double s, tx, ty, a;
+  pose_terms(mx, my, ma, mo, qa, qo, cx, cy, k, s, tx, ty, a);
   const double ca = cos(a), sa = sin(a);
   const double x = (ca * tx - sa * ty) + (double)qx;
   const double y = (sa * tx + ca * ty) + (double)qy;
@@ -1382,6 +1392,29 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
 #undef FU_STAMP
 }
 
+// (tx, ty, alpha, qx, qy) of the listed queries' poses, for the host's glibc redo of the
+// PoseBin x / y means (sod_exact_xy_means)
+__global__ void pose_rec_kernel(int n, const int32_t* __restrict__ qlist,
+                                const int* __restrict__ idx1, const float* __restrict__ qx,
+                                const float* __restrict__ qy, const float* __restrict__ qa,
+                                const int* __restrict__ qo, const float* __restrict__ mx,
+                                const float* __restrict__ my, const float* __restrict__ ma,
+                                const int* __restrict__ mo, const int* __restrict__ mimg,
+                                const double* __restrict__ cent, double* __restrict__ rec) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int q = qlist[i], m = idx1[q], im = mimg[m];
+  int k;
+  double s, tx, ty, a;
+  pose_terms(mx[m], my[m], ma[m], mo[m], qa[q], qo[q], cent[2 * im], cent[2 * im + 1], k, s, tx, ty,
+             a);
+  rec[5 * i + 0] = tx;
+  rec[5 * i + 1] = ty;
+  rec[5 * i + 2] = a;
+  rec[5 * i + 3] = (double)qx[q];
+  rec[5 * i + 4] = (double)qy[q];
+}
+
 // PoseBin running means in vote order (PoseBin.py:19-43).  The recurrence
 //   v' = (v*n + new) / (n+1)
 // rounds at every step, so each bin's chain is inherently sequential; but the six
@@ -1947,6 +1980,75 @@ void sod_guard_host_pose(const double r[8], const int32_t bins[4], double* x, do
   const int H = (int)r[6], W = (int)r[7];
   *ix = xy_index((*x * bins[0]) / W, bins[0]);
   *iy = xy_index((*y * bins[1]) / H, bins[1]);
+}
+
+// The x / y PoseBin means of valid bins vbin[0..nb) redone on the host: each member's pose
+// x, y with glibc cos / sin (the calls main.py's math.cos / math.sin make, HTHF:31-32) in the
+// reference's expression order, then the running mean of PoseBin.py:45-51 -- so they are the
+// reference's values bit for bit, where the device's cos / sin may differ by an ulp.  Written
+// to means6[6 i + 0 / 1] (the other four means never involve a transcendental: exact already).
+int sod_exact_xy_means(sod_ctx* ctx, const int32_t* vbin, int nb, double* means6) {
+  if (nb <= 0) return SOD_OK;
+  int64_t V, M;
+  SOD_TRY(sod_valid_counts(ctx, &V, &M));
+  std::vector<int64_t> off((size_t)V + 1);
+  std::vector<int32_t> mem((size_t)M);
+  SOD_HIP(ctx, hipMemcpyAsync(off.data(), ctx->voff.p, off.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (M) SOD_HIP(ctx, hipMemcpyAsync(mem.data(), ctx->members.p, mem.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
+  std::vector<int32_t> qlist;
+  for (int i = 0; i < nb; ++i) {
+    const int64_t v = vbin[i];
+    if (v < 0 || v >= V) return sod_fail(ctx, SOD_EINVAL, "valid-bin index out of range");
+    qlist.insert(qlist.end(), mem.begin() + off[(size_t)v], mem.begin() + off[(size_t)v + 1]);
+  }
+  const int n = (int)qlist.size();
+  if (!n) return SOD_OK;
+  const int64_t q0 = sod_win0(ctx);
+  DevBuf<int32_t> dq;
+  DevBuf<double> drec;
+  std::vector<double> rec((size_t)n * 5);
+  int rc = sod_reserve(ctx, dq, (size_t)n);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, drec, (size_t)n * 5);
+  if (rc == SOD_OK && hipMemcpyAsync(dq.p, qlist.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "exact means: upload");
+  if (rc == SOD_OK) {
+    hipLaunchKernelGGL(pose_rec_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, ctx->stream, n,
+                       dq.p, ctx->idx1.p + q0, ctx->qx.p + q0, ctx->qy.p + q0, ctx->qang.p + q0,
+                       ctx->qoct.p + q0, ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p,
+                       ctx->mimg.p, ctx->cent.p, drec.p);
+    if (hipGetLastError() != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, "pose_rec_kernel launch");
+  }
+  if (rc == SOD_OK && hipMemcpyAsync(rec.data(), drec.p, rec.size() * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "exact means: download");
+  if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "exact means: sync");
+  (void)sod_stream_sync(ctx->stream);
+  sod_release(dq);
+  sod_release(drec);
+  if (rc != SOD_OK) return rc;
+  size_t j = 0;
+  for (int i = 0; i < nb; ++i) {
+    const int64_t v = vbin[i], cnt = off[(size_t)v + 1] - off[(size_t)v];
+    double mxv = 0.0, myv = 0.0;
+    for (int64_t t = 0; t < cnt; ++t, ++j) {
+      const double* r = rec.data() + 5 * j;
+      const double ca = std::cos(r[2]), sa = std::sin(r[2]);
+      const double x = (ca * r[0] - sa * r[1]) + r[3];   // HTHF:31, :34
+      const double y = (sa * r[0] + ca * r[1]) + r[4];   // HTHF:32, :35
+      if (t == 0) {
+        mxv = x;
+        myv = y;
+      } else {                                         // PoseBin.py:45-51, n = votes so far
+        const double nn = (double)t;
+        mxv = (mxv * nn + x) / (nn + 1.0);
+        myv = (myv * nn + y) / (nn + 1.0);
+      }
+    }
+    means6[6 * i + 0] = mxv;
+    means6[6 * i + 1] = myv;
+  }
+  return SOD_OK;
 }
 
 int sod_guard_resolve(sod_ctx* ctx) {

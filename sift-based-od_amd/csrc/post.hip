@@ -237,6 +237,25 @@ int sod_post_batch(sod_ctx* ctx, int32_t n, const double* means, int32_t* n_pos,
                     final_orientation, final_pose);
 }
 
+int sod_exact_means(sod_ctx* ctx, int32_t nb, const int32_t* vbin, double* xy) {
+  if (!ctx) return SOD_EINVAL;
+  if (nb < 0 || (nb > 0 && (!vbin || !xy))) return sod_fail(ctx, SOD_EINVAL, "bad exact-means input");
+  std::vector<double> m6((size_t)nb * 6, 0.0);
+  SOD_TRY(sod_exact_xy_means(ctx, vbin, nb, m6.data()));
+  for (int32_t i = 0; i < nb; ++i) {
+    xy[2 * i] = m6[6 * (size_t)i];
+    xy[2 * i + 1] = m6[6 * (size_t)i + 1];
+  }
+  return SOD_OK;
+}
+
+int sod_set_post_exact(sod_ctx* ctx, int on) {
+  if (!ctx) return SOD_EINVAL;
+  if (on != 0 && on != 1) return sod_fail(ctx, SOD_EINVAL, "post exact must be 0 or 1");
+  ctx->post_exact = on != 0;
+  return SOD_OK;
+}
+
 int sod_postprocess(sod_ctx* ctx, int32_t* n_bins, int32_t* bin_index, int32_t* n_pos,
                     int32_t* pos_off, int32_t* pos_members, int32_t* n_ori,
                     int32_t* ori_pos_off, int32_t* ori_off, int32_t* ori_members,
@@ -271,6 +290,10 @@ int sod_postprocess(sod_ctx* ctx, int32_t* n_bins, int32_t* bin_index, int32_t* 
   const int32_t n = (int32_t)idx.size();
   if (n_bins) *n_bins = n;
   if (bin_index && n) std::memcpy(bin_index, idx.data(), (size_t)n * sizeof(int32_t));
+  // the survivors' x / y means as the reference computes them (glibc cos / sin per member,
+  // sod_exact_xy_means): the position relation's <= thresholds (PostProcessing.py:24-28) and
+  // the final pose then see the reference's values bit for bit
+  if (ctx->post_exact && n) SOD_TRY(sod_exact_xy_means(ctx, idx.data(), n, sel.data()));
   PostOut o;
   SOD_TRY(run_post(ctx, n, sel.data(), img.empty() ? nullptr : img.data(), o));
   return write_post(o, n_pos, pos_off, pos_members, n_ori, ori_pos_off, ori_off, ori_members,

@@ -217,6 +217,7 @@ struct sod_ctx {
   hipEvent_t ev_done[2] = {nullptr, nullptr};   // each slot's last matcher-stream completion
   hipStream_t mstream_of(int slot) const { return mtwo && slot ? mstream2 : mstream; }
   bool stage_timing = true;   // sod_set_stage_timing: ev[2..5] around the tail stages
+  bool post_exact = true;     // sod_set_post_exact: survivors' x / y means redone with glibc
   bool overlap = false;
   bool mk_main = true;        // the last matcher launch went on the context stream (idle, no split)
   bool merge_norec[2] = {false, false};   // a slot's last merge released it without an event
@@ -404,4 +405,5 @@ int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
 void sod_guard_host_pose(const double rec[8], const int32_t bins[4], double* x, double* y,
                          int32_t* ix, int32_t* iy);
 int sod_build_sigma_lut(sod_ctx* ctx, int32_t bins_sigma);
+int sod_exact_xy_means(sod_ctx* ctx, const int32_t* vbin, int nb, double* means6);
 void sod_sift_free(sod_ctx* ctx);

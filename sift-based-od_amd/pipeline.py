@@ -277,6 +277,13 @@ class Main:
             finally:
                 if gc_was_on:
                     gc.enable()
+            if out:
+                # the survivors' centroids as the reference computes them (glibc cos / sin per
+                # member, sod_exact_means): post_process's <= thresholds and final pose then see
+                # main.py's values bit for bit (the device means differ in the last ulps)
+                sidx = [i for i, k in enumerate(survived) if k]
+                for b, (x, y) in zip(out, self.ctx.exact_means(sidx).tolist()):
+                    b.centroid = (x, y)
             self.valid_bins = out
             self._valid_sel = None
             self.affine_path = "device-resident"

@@ -108,6 +108,10 @@ def test_main_stages_match_golden():
     for b, mu in zip(m.valid_bins, g["valid_means"]):
         np.testing.assert_allclose([b.centroid[0], b.centroid[1], b.angle, b.scale,
                                     b.img_size[0], b.img_size[1]], mu, rtol=1e-12, atol=1e-9)
+    # the x / y means as the reference computes them (glibc per member): bit for bit
+    xy = m.ctx.exact_means(np.arange(len(m.valid_bins)))
+    ref_xy = np.ascontiguousarray(np.asarray(g["valid_means"], np.float64)[:, :2])
+    assert np.array_equal(xy.view(np.uint64), ref_xy.view(np.uint64))
     m.apply_affine_parameters(4)
     assert m.affine_path == "device-resident"
     assert [b.pose for b in m.valid_bins] == [tuple(k) for k in g["surv_keys"]]
@@ -117,7 +121,9 @@ def test_main_stages_match_golden():
     assert len(m.keypoint_pairs) == int(g["surv_votes"].sum())
     m.post_process()                                   # main.py:186
     got = np.array([[p[0][0], p[0][1], p[1], p[2], p[3][0], p[3][1]] for p in m.final_pose])
-    np.testing.assert_allclose(got.reshape(-1, 6), g["final_pose"], rtol=1e-12, atol=1e-9)
+    # survivors' centroids redone with glibc (sod_exact_means): main.py's final pose exactly
+    assert np.array_equal(got.reshape(-1, 6).view(np.uint64),
+                          np.asarray(g["final_pose"], np.float64).reshape(-1, 6).view(np.uint64))
 
 
 def _kf_rows(kps):

@@ -133,6 +133,13 @@ def test_pipeline_postprocess_golden(ctx, name):
     ctx.pipeline(tuple(int(v) for v in g["shape"]), int(g["bins"]))
     r = ctx.postprocess()
     assert np.array_equal(r["bin_index"], g["surv_index"])
+    # the survivors' x / y means redone with glibc (sod_set_post_exact, default): main.py's
+    # final pose bit for bit
+    assert np.array_equal(r["final_pose"].view(np.uint64),
+                          np.asarray(g["final_pose"], np.float64).view(np.uint64))
+    ctx.set_post_exact(False)   # the device means (device cos / sin): within 1e-12
+    r = ctx.postprocess()
+    ctx.set_post_exact(True)
     np.testing.assert_allclose(r["final_pose"], g["final_pose"], rtol=1e-12, atol=1e-9)
 
 
@@ -156,4 +163,5 @@ def test_stage_api_postprocess_golden(ctx, name):
     r.select(5)
     r.affine((shape[1], shape[0]), 128.0, 128.0, 4)
     res = r.postprocess()
-    np.testing.assert_allclose(res["final_pose"], g["final_pose"], rtol=1e-12, atol=1e-9)
+    assert np.array_equal(res["final_pose"].view(np.uint64),
+                          np.asarray(g["final_pose"], np.float64).view(np.uint64))
