@@ -2027,7 +2027,7 @@ int sod_exact_xy_means(sod_ctx* ctx, const int32_t* vbin, int nb, double* means6
   sod_release(dq);
   sod_release(drec);
   if (rc != SOD_OK) return rc;
-  // bins are independent: host threads over bin ranges of about equal member counts (the
+  // bins are independent: up to 16 host threads over bin ranges of about equal member counts (the
   // two libm calls per member dominate: ~2 ms for C3's survivors on one thread)
   std::vector<size_t> j0((size_t)nb + 1, 0);
   for (int i = 0; i < nb; ++i)
@@ -2055,7 +2055,7 @@ int sod_exact_xy_means(sod_ctx* ctx, const int32_t* vbin, int nb, double* means6
     }
   };
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int nt = (int)std::min<size_t>({(size_t)8, (size_t)hw, (size_t)nb, (size_t)n / 2048 + 1});
+  const int nt = (int)std::min<size_t>({(size_t)16, (size_t)hw, (size_t)nb, (size_t)n / 2048 + 1});
   if (nt <= 1) {
     run(0, nb);
     return SOD_OK;
