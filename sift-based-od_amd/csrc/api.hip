@@ -379,6 +379,9 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->pose); sod_release(ctx->selstat); sod_release(ctx->selticket); sod_release(ctx->scal); sod_release(ctx->vbin);
   sod_release(ctx->voff); sod_release(ctx->members); sod_release(ctx->means);
   sod_release(ctx->vidx); sod_release(ctx->cursor); sod_release(ctx->vfirst_s);
+  sod_release(ctx->xr_idx); sod_release(ctx->xr_rec);
+  if (ctx->xr_host) (void)hipHostFree(ctx->xr_host);
+  ctx->xr_host = nullptr;
   sod_release(ctx->rtab); sod_release(ctx->msize);
   sod_release(ctx->pose_b); sod_release(ctx->msize_b); sod_release(ctx->scal_b);
   sod_release(ctx->voff_b); sod_release(ctx->members_b); sod_release(ctx->means_b);

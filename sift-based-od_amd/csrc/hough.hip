@@ -1415,6 +1415,36 @@ __global__ void pose_rec_kernel(int n, const int32_t* __restrict__ qlist,
   rec[5 * i + 4] = (double)qy[q];
 }
 
+// the same for the members of listed valid bins, one work-group per bin: record roff[b] + t
+// is member t of valid bin vb[b] (vote order)
+__global__ void pose_rec_bins_kernel(int nb, const int32_t* __restrict__ vb,
+                                     const int64_t* __restrict__ roff,
+                                     const int64_t* __restrict__ voff,
+                                     const int32_t* __restrict__ members,
+                                     const int* __restrict__ idx1, const float* __restrict__ qx,
+                                     const float* __restrict__ qy, const float* __restrict__ qa,
+                                     const int* __restrict__ qo, const float* __restrict__ mx,
+                                     const float* __restrict__ my, const float* __restrict__ ma,
+                                     const int* __restrict__ mo, const int* __restrict__ mimg,
+                                     const double* __restrict__ cent, double* __restrict__ rec) {
+  const int b = blockIdx.x;
+  if (b >= nb) return;
+  const int64_t a = voff[vb[b]], cnt = voff[vb[b] + 1] - a, r0 = roff[b];
+  for (int64_t t = threadIdx.x; t < cnt; t += blockDim.x) {
+    const int q = members[a + t], m = idx1[q], im = mimg[m];
+    int k;
+    double s, tx, ty, al;
+    pose_terms(mx[m], my[m], ma[m], mo[m], qa[q], qo[q], cent[2 * im], cent[2 * im + 1], k, s, tx,
+               ty, al);
+    double* r = rec + 5 * (r0 + t);
+    r[0] = tx;
+    r[1] = ty;
+    r[2] = al;
+    r[3] = (double)qx[q];
+    r[4] = (double)qy[q];
+  }
+}
+
 // PoseBin running means in vote order (PoseBin.py:19-43).  The recurrence
 //   v' = (v*n + new) / (n+1)
 // rounds at every step, so each bin's chain is inherently sequential; but the six
@@ -1992,51 +2022,52 @@ int sod_exact_xy_means(sod_ctx* ctx, const int32_t* vbin, int nb, double* means6
   int64_t V, M;
   SOD_TRY(sod_valid_counts(ctx, &V, &M));
   std::vector<int64_t> off((size_t)V + 1);
-  std::vector<int32_t> mem((size_t)M);
   SOD_HIP(ctx, hipMemcpyAsync(off.data(), ctx->voff.p, off.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-  if (M) SOD_HIP(ctx, hipMemcpyAsync(mem.data(), ctx->members.p, mem.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
   SOD_HIP(ctx, sod_stream_sync(ctx->stream));
-  std::vector<int32_t> qlist;
+  // bin list and record offsets up (one upload), records gathered on the device, down into a
+  // pinned buffer; the buffers stay with the context (a hipFree per call synchronises the
+  // device and cost as much as the rest)
+  std::vector<int64_t> up((size_t)nb * 2 + 1);   // [roff 0..nb] [vb as int64 0..nb-1]
+  up[0] = 0;
   for (int i = 0; i < nb; ++i) {
     const int64_t v = vbin[i];
     if (v < 0 || v >= V) return sod_fail(ctx, SOD_EINVAL, "valid-bin index out of range");
-    qlist.insert(qlist.end(), mem.begin() + off[(size_t)v], mem.begin() + off[(size_t)v + 1]);
+    up[(size_t)i + 1] = up[(size_t)i] + (off[(size_t)v + 1] - off[(size_t)v]);
   }
-  const int n = (int)qlist.size();
+  const int64_t n = up[(size_t)nb];
   if (!n) return SOD_OK;
-  const int64_t q0 = sod_win0(ctx);
-  DevBuf<int32_t> dq;
-  DevBuf<double> drec;
-  std::vector<double> rec((size_t)n * 5);
-  int rc = sod_reserve(ctx, dq, (size_t)n);
-  if (rc == SOD_OK) rc = sod_reserve(ctx, drec, (size_t)n * 5);
-  if (rc == SOD_OK && hipMemcpyAsync(dq.p, qlist.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
-    rc = sod_fail(ctx, SOD_EHIP, "exact means: upload");
-  if (rc == SOD_OK) {
-    hipLaunchKernelGGL(pose_rec_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, ctx->stream, n,
-                       dq.p, ctx->idx1.p + q0, ctx->qx.p + q0, ctx->qy.p + q0, ctx->qang.p + q0,
-                       ctx->qoct.p + q0, ctx->mx.p, ctx->my.p, ctx->mang.p, ctx->moct.p,
-                       ctx->mimg.p, ctx->cent.p, drec.p);
-    if (hipGetLastError() != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, "pose_rec_kernel launch");
+  SOD_TRY(sod_reserve(ctx, ctx->xr_idx, (size_t)nb * 3 + 2));   // roff (nb+1 int64) + vb (nb int32)
+  SOD_TRY(sod_reserve(ctx, ctx->xr_rec, (size_t)n * 5));
+  if (ctx->xr_host_n < (size_t)n * 5) {
+    if (ctx->xr_host) (void)hipHostFree(ctx->xr_host);
+    ctx->xr_host = nullptr;
+    ctx->xr_host_n = 0;
+    SOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->xr_host), (size_t)n * 5 * 8, hipHostMallocDefault));
+    ctx->xr_host_n = (size_t)n * 5;
   }
-  if (rc == SOD_OK && hipMemcpyAsync(rec.data(), drec.p, rec.size() * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
-    rc = sod_fail(ctx, SOD_EHIP, "exact means: download");
-  if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
-    rc = sod_fail(ctx, SOD_EHIP, "exact means: sync");
-  (void)sod_stream_sync(ctx->stream);
-  sod_release(dq);
-  sod_release(drec);
-  if (rc != SOD_OK) return rc;
+  int64_t* droff = reinterpret_cast<int64_t*>(ctx->xr_idx.p);
+  int32_t* dvb = reinterpret_cast<int32_t*>(droff + nb + 1);
+  std::vector<int32_t> vb32(vbin, vbin + nb);
+  SOD_HIP(ctx, hipMemcpyAsync(droff, up.data(), ((size_t)nb + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  SOD_HIP(ctx, hipMemcpyAsync(dvb, vb32.data(), (size_t)nb * 4, hipMemcpyHostToDevice, ctx->stream));
+  const int64_t q0 = sod_win0(ctx);
+  hipLaunchKernelGGL(pose_rec_bins_kernel, dim3((unsigned)nb), dim3(256), 0, ctx->stream, nb, dvb,
+                     droff, ctx->voff.p, ctx->members.p, ctx->idx1.p + q0, ctx->qx.p + q0,
+                     ctx->qy.p + q0, ctx->qang.p + q0, ctx->qoct.p + q0, ctx->mx.p, ctx->my.p,
+                     ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p, ctx->xr_rec.p);
+  SOD_HIP(ctx, hipGetLastError());
+  SOD_HIP(ctx, hipMemcpyAsync(ctx->xr_host, ctx->xr_rec.p, (size_t)n * 5 * 8, hipMemcpyDeviceToHost, ctx->stream));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
+  const double* rec = ctx->xr_host;
+  std::vector<size_t> j0((size_t)nb + 1, 0);
+  for (int i = 0; i <= nb; ++i) j0[(size_t)i] = (size_t)up[(size_t)i];
   // bins are independent: up to 16 host threads over bin ranges of about equal member counts (the
   // two libm calls per member dominate: ~2 ms for C3's survivors on one thread)
-  std::vector<size_t> j0((size_t)nb + 1, 0);
-  for (int i = 0; i < nb; ++i)
-    j0[(size_t)i + 1] = j0[(size_t)i] + (size_t)(off[(size_t)vbin[i] + 1] - off[(size_t)vbin[i]]);
   auto run = [&](int b0, int b1) {
     for (int i = b0; i < b1; ++i) {
       double mxv = 0.0, myv = 0.0;
       for (size_t j = j0[(size_t)i]; j < j0[(size_t)i + 1]; ++j) {
-        const double* r = rec.data() + 5 * j;
+        const double* r = rec + 5 * j;
         const double ca = std::cos(r[2]), sa = std::sin(r[2]);
         const double x = (ca * r[0] - sa * r[1]) + r[3];   // HTHF:31, :34
         const double y = (sa * r[0] + ca * r[1]) + r[4];   // HTHF:32, :35

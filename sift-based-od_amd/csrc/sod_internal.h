@@ -218,6 +218,11 @@ struct sod_ctx {
   hipStream_t mstream_of(int slot) const { return mtwo && slot ? mstream2 : mstream; }
   bool stage_timing = true;   // sod_set_stage_timing: ev[2..5] around the tail stages
   bool post_exact = true;     // sod_set_post_exact: survivors' x / y means redone with glibc
+  // sod_exact_xy_means: bin list + record offsets, the pose records, their pinned host copy
+  DevBuf<int32_t> xr_idx;
+  DevBuf<double> xr_rec;
+  double* xr_host = nullptr;
+  size_t xr_host_n = 0;
   bool overlap = false;
   bool mk_main = true;        // the last matcher launch went on the context stream (idle, no split)
   bool merge_norec[2] = {false, false};   // a slot's last merge released it without an event
