@@ -1392,31 +1392,9 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
 #undef FU_STAMP
 }
 
-// (tx, ty, alpha, qx, qy) of the listed queries' poses, for the host's glibc redo of the
-// PoseBin x / y means (sod_exact_xy_means)
-__global__ void pose_rec_kernel(int n, const int32_t* __restrict__ qlist,
-                                const int* __restrict__ idx1, const float* __restrict__ qx,
-                                const float* __restrict__ qy, const float* __restrict__ qa,
-                                const int* __restrict__ qo, const float* __restrict__ mx,
-                                const float* __restrict__ my, const float* __restrict__ ma,
-                                const int* __restrict__ mo, const int* __restrict__ mimg,
-                                const double* __restrict__ cent, double* __restrict__ rec) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int q = qlist[i], m = idx1[q], im = mimg[m];
-  int k;
-  double s, tx, ty, a;
-  pose_terms(mx[m], my[m], ma[m], mo[m], qa[q], qo[q], cent[2 * im], cent[2 * im + 1], k, s, tx, ty,
-             a);
-  rec[5 * i + 0] = tx;
-  rec[5 * i + 1] = ty;
-  rec[5 * i + 2] = a;
-  rec[5 * i + 3] = (double)qx[q];
-  rec[5 * i + 4] = (double)qy[q];
-}
-
-// the same for the members of listed valid bins, one work-group per bin: record roff[b] + t
-// is member t of valid bin vb[b] (vote order)
+// (tx, ty, alpha, qx, qy) of the poses of the members of listed valid bins, for the host's
+// glibc redo of the PoseBin x / y means (sod_exact_xy_means); one work-group per bin:
+// record roff[b] + t is member t of valid bin vb[b] (vote order)
 __global__ void pose_rec_bins_kernel(int nb, const int32_t* __restrict__ vb,
                                      const int64_t* __restrict__ roff,
                                      const int64_t* __restrict__ voff,
