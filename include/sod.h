@@ -139,6 +139,12 @@ int sod_match_enqueue(sod_ctx* ctx);
  * bf16 MFMA rate.  All are bit-exact; call before the descriptor uploads (the packed
  * layouts differ; switching drops uploaded descriptors). */
 int sod_match_set_impl(sod_ctx* ctx, int impl);
+/* Kernel shape of the int8 16x16x64 matcher (impl 1): 0 = by query count (default),
+ * 1 = LDS-ring kernel (queries stationary, 2-8 tiles per wave, DB through LDS; large query
+ * sets), 2 = register-streamed kernel (a 512-query group resident per wave, each wave
+ * streaming its own DB rows from HBM; one query image .. ~10k queries).  Same results bit for
+ * bit; replaces cv2.BFMatcher().knnMatch's single loop (main.py:70-71). */
+int sod_match_set_kernel(sod_ctx* ctx, int kernel);
 /* Matcher on a stream of its own (1) or on the context stream (0, default).  With 1 the
  * matcher kernel of the next sod_match_enqueue / sod_pipeline_enqueue only waits for the
  * previous merge of its partial results (and for the last descriptor upload), so it overlaps

@@ -68,6 +68,7 @@ SIGNATURES = {
     "sod_valid_images_get": (C.c_int, [c_ctx, c_i32p]),
     "sod_match_enqueue": (C.c_int, [c_ctx]),
     "sod_match_set_impl": (C.c_int, [c_ctx, C.c_int]),
+    "sod_match_set_kernel": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_set_overlap": (C.c_int, [c_ctx, C.c_int]),
     "sod_set_cu_reserve": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
@@ -267,6 +268,15 @@ class Context:
         32x32x32); call before uploads."""
         self._chk(self._L.sod_match_set_impl(self._h, self.IMPLS[impl] if isinstance(impl, str)
                                              else int(impl)))
+
+    KERNELS = {"auto": 0, "ring": 1, "streamed": 2}
+
+    def set_match_kernel(self, kernel):
+        """Kernel shape of the int8 matcher: "auto" (by query count, default), "ring" (LDS
+        ring, large query sets) or "streamed" (a 512-query group per wave, small sets);
+        results are identical."""
+        self._chk(self._L.sod_match_set_kernel(self._h, self.KERNELS[kernel] if isinstance(kernel, str)
+                                               else int(kernel)))
 
     def set_overlap(self, on=True):
         """Matcher kernel on a stream of its own: the next query's matcher overlaps this

@@ -899,6 +899,14 @@ int sod_match_set_impl(sod_ctx* ctx, int impl) {
   return SOD_OK;
 }
 
+int sod_match_set_kernel(sod_ctx* ctx, int kernel) {
+  if (!ctx) return SOD_EINVAL;
+  if (kernel < 0 || kernel > 2)
+    return sod_fail(ctx, SOD_EINVAL, "kernel must be 0 (by query count), 1 (LDS ring) or 2 (streamed)");
+  ctx->mkernel = kernel;
+  return SOD_OK;
+}
+
 int sod_match_allgather_enqueue(sod_ctx* ctx) {
   SOD_TRY(set_dev(ctx, false));   // writes no buffer a pending PoseBin means reads
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "sod_match_enqueue first");

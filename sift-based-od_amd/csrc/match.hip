@@ -395,7 +395,7 @@ constexpr int kMergeW = 16;
 __global__ __launch_bounds__(64 * kMergeW) void merge_kernel(
     const float* __restrict__ d1, const int* __restrict__ idx, const float* __restrict__ d2,
     int nparts, int64_t stride, int64_t nq, float* __restrict__ od1, int* __restrict__ oidx,
-    float* __restrict__ od2, int* __restrict__ reset, double ratio, int64_t nq_real,
+    float* __restrict__ od2, int* __restrict__ reset, int reset_words, double ratio, int64_t nq_real,
     float* __restrict__ rd1, float* __restrict__ rd2, int* __restrict__ ridx,
     uint8_t* __restrict__ rgood) {
   __shared__ float s1[kMergeW][64], s2[kMergeW][64];
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(64 * kMergeW) void merge_kernel(
   // the matcher's shared thresholds of this partial-result slot: "nothing known" again for
   // the next launch that takes the slot (it waits for this merge)
   if (reset)
-    for (int r = 0; r < kThrWords; ++r) reset[(int64_t)r * nq + q] = (int)0x80808080;
+    for (int r = 0; r < reset_words; ++r) reset[(int64_t)r * nq + q] = (int)0x80808080;
   od1[q] = v1;
   oidx[q] = i1;
   od2[q] = v2;
@@ -572,7 +572,8 @@ int launch_merge(sod_ctx* ctx, const float* d1, const int32_t* idx, const float*
   const int wv = std::max(1, std::min(kMergeW, nparts));
   hipLaunchKernelGGL(merge_kernel, dim3((unsigned)ceil_div(nq_pad, 64)), dim3(64 * wv), 0,
                      ctx->stream, d1, idx, d2, nparts, stride, nq_pad, ctx->cd1.p, ctx->cidx.p,
-                     ctx->cd2.p, reset, fuse ? ctx->fuse_ratio : -1.0, (int64_t)ctx->nq, ctx->d1.p,
+                     ctx->cd2.p, reset, (int)sod_thr_words(ctx), fuse ? ctx->fuse_ratio : -1.0,
+                     (int64_t)ctx->nq, ctx->d1.p,
                      ctx->d2.p, ctx->idx1.p, ctx->good.p);
   ctx->ratio_fused_valid = fuse;
   if (fuse) ctx->ratio_fused = ctx->fuse_ratio;

@@ -1302,6 +1302,10 @@ int launch_match_i8(sod_ctx* ctx) {
   const int64_t max_st = ((int64_t)1 << 30) / (wide ? w::kStageBytes : kStageBytes);
   if (st_per_split > max_st) st_per_split = max_st;
   split = cdiv(nstages, st_per_split);
+  // small query sets: the register-streamed kernel (match_s.hip); st_per_split then counts
+  // subtiles of a DB range
+  const bool use_s = !wide && sod_match_use_s(ctx);
+  if (use_s) sod_match_s_geometry(ctx, &split, &st_per_split);
   ctx->split = (int)split;
   SOD_TRY(sod_reserve(ctx, ctx->cd1, (size_t)nq_pad));
   SOD_TRY(sod_reserve(ctx, ctx->cd2, (size_t)nq_pad));
@@ -1318,7 +1322,7 @@ int launch_match_i8(sod_ctx* ctx) {
   // uninitialised thresholds
   int32_t* gthr = nullptr;
   if (!wide) {
-    const int64_t gslot = kThrWords * nq_pad;   // words of one slot
+    const int64_t gslot = sod_thr_words(ctx) * nq_pad;   // words of one slot
     if (ctx->gthr.n < (size_t)(2 * gslot) || ctx->gthr_n != nq_pad) {
       if (ctx->gthr.n < (size_t)(2 * gslot)) {
         SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
@@ -1337,7 +1341,9 @@ int launch_match_i8(sod_ctx* ctx) {
   const int seedload = split <= 64 ? 1 : 0;   // see match_unit (SOD_I8_SEEDLOAD)
   hipEvent_t eb, ee;
   SOD_TRY(sod_match_events(ctx, &eb, &ee));
-  if (wide)
+  if (use_s)
+    SOD_TRY(launch_match_s_kernel(ctx, ks, eb, ee, pd1, pidx, pd2, gthr, split, st_per_split));
+  else if (wide)
     hipExtLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0,
                           ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
                           ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),

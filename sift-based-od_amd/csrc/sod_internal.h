@@ -49,6 +49,8 @@ struct sod_ctx {
   int match_cus() const { return num_cus - reserved_cus; }
   int tail_cus() const { return reserved_cus ? reserved_cus : num_cus; }
   int impl = 1;                 // matcher: 1 = int8 MFMA 16x16x64 (default), 2 = int8 32x32x32 (match_i8.hip), 0 = bf16 (match.hip)
+  int mkernel = 0;              // impl 1's kernel shape (sod_match_set_kernel): 0 = by query count,
+                                // 1 = LDS ring (match_i8.hip), 2 = register-streamed (match_s.hip)
 
   // ---- database (keypoints replicated, descriptors = shard) ----
   int64_t n_total = 0;          // keypoints in the whole DB
@@ -362,6 +364,14 @@ int launch_find_rows_i8(sod_ctx* ctx, const float* flo, const float* fhi, const 
                         int32_t* found);
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db);
 int launch_match_i8(sod_ctx* ctx);
+// small query sets (match_s.hip): the register-streamed kernel, its launch geometry, and the
+// shared-threshold words per query of one partial-result slot (both int8 kernels' layouts fit)
+bool sod_match_use_s(const sod_ctx* ctx);
+void sod_match_s_geometry(const sod_ctx* ctx, int64_t* split, int64_t* sub_per_split);
+int launch_match_s_kernel(sod_ctx* ctx, hipStream_t ks, hipEvent_t eb, hipEvent_t ee, float* pd1,
+                          int32_t* pidx, float* pd2, int32_t* gthr, int64_t split,
+                          int64_t sub_per_split);
+int64_t sod_thr_words(const sod_ctx* ctx);
 // matcher-input writers call these around their writes; the match launchers around the
 // kernel (see sod_ctx::mstream)
 int sod_inputs_begin(sod_ctx* ctx);

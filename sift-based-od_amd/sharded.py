@@ -93,7 +93,15 @@ class FileStore:
     ``SOD_STORE_DIR``).  Every rank registers at construction and waits up to
     ``join_timeout`` seconds for the others, so ranks that landed in different directories
     fail at once with the path they used, not after ``timeout``.  ``close()`` removes the
-    directory once every rank is done with it."""
+    directory once every rank is done with it.
+
+    Generations: a run that crashed leaves its files behind, and a later run in the same
+    directory must not read them (an old RCCL unique id or all-gather payload).  Rank 0 clears
+    the directory, then publishes a fresh random generation id in ``gen``; every key of the
+    run is prefixed by it.  A rank > 0 joins the generation it reads with a random nonce of its
+    own and proceeds only when rank 0's ``<gen>_ready`` echoes that nonce -- which a file left
+    by an earlier run cannot -- re-joining whenever ``gen`` changes (it may have read a stale
+    one before rank 0 cleared it)."""
 
     def __init__(self, world, rank, path=None, timeout=600.0, join_timeout=60.0):
         import os
@@ -109,30 +117,92 @@ class FileStore:
         self.path = path
         os.makedirs(path, exist_ok=True)
         self._seq = 0
+        self.gen = ""
         if world > 1:
-            self.set("join_%d" % rank, b"")
-            t, self.timeout = self.timeout, join_timeout
             try:
-                for r in range(world):
-                    self.get("join_%d" % r)
-            except TimeoutError:
+                self._join(join_timeout)
+            except TimeoutError as e:
                 raise TimeoutError(
-                    "FileStore: rank %d of %d found no rank %d in %s within %.0f s -- ranks not "
-                    "started by one launcher must share a directory: set SOD_STORE_DIR"
-                    % (rank, world, r, path, join_timeout)) from None
-            finally:
-                self.timeout = t
+                    "FileStore: rank %d of %d: %s in %s within %.0f s -- ranks not started by "
+                    "one launcher must share a directory: set SOD_STORE_DIR"
+                    % (rank, world, e, path, join_timeout)) from None
+
+    def _join(self, join_timeout):
+        import json
+        import os
+        import time
+        import uuid
+        t0 = time.perf_counter()
+        if self.rank == 0:
+            for name in os.listdir(self.path):   # an earlier run's leftovers
+                try:
+                    os.remove(os.path.join(self.path, name))
+                except OSError:
+                    pass
+            self.gen = uuid.uuid4().hex
+            self._put("gen", self.gen.encode())
+            nonces = {}
+            for r in range(1, self.world):
+                nonces[r] = self._wait("%s_join_%d" % (self.gen, r), t0, join_timeout,
+                                       "found no rank %d" % r).decode()
+            self._put("%s_ready" % self.gen, json.dumps(nonces).encode())
+            return
+        mine = uuid.uuid4().hex
+        gen = None
+        spin = 0
+        while True:
+            if time.perf_counter() - t0 > join_timeout:
+                raise TimeoutError("found no rank 0 (generation %s)" % gen)
+            g = self._read("gen")
+            if g is not None and g.decode() != gen:
+                gen = g.decode()
+                self._put("%s_join_%d" % (gen, self.rank), mine.encode())
+            if gen is not None:
+                ready = self._read("%s_ready" % gen)
+                if ready is not None and json.loads(ready.decode()).get(str(self.rank)) == mine:
+                    self.gen = gen
+                    return
+            spin += 1
+            if spin > 200:
+                time.sleep(1e-4)
+
+    def _put(self, name, data):
+        import os
+        tmp = os.path.join(self.path, ".%s.%d.tmp" % (name, self.rank))
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, os.path.join(self.path, name))
+
+    def _read(self, name):
+        try:
+            with open(self._file_raw(name), "rb") as fh:
+                return fh.read()
+        except OSError:
+            return None
+
+    def _wait(self, name, t0, limit, what):
+        import time
+        spin = 0
+        while True:
+            d = self._read(name)
+            if d is not None:
+                return d
+            if time.perf_counter() - t0 > limit:
+                raise TimeoutError(what)
+            spin += 1
+            if spin > 200:
+                time.sleep(1e-4)
+
+    def _file_raw(self, name):
+        import os
+        return os.path.join(self.path, name)
 
     def _file(self, key):
         import os
-        return os.path.join(self.path, key)
+        return os.path.join(self.path, "%s_%s" % (self.gen, key))
 
     def set(self, key, data):
-        import os
-        tmp = self._file(".%s.%d.tmp" % (key, self.rank))
-        with open(tmp, "wb") as f:
-            f.write(data)
-        os.replace(tmp, self._file(key))
+        self._put("%s_%s" % (self.gen, key), data)
 
     def get(self, key):
         import os

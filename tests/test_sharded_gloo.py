@@ -191,3 +191,47 @@ def test_file_store_fails_fast_without_shared_dir(tmp_path, monkeypatch):
     assert st.path.endswith("sod_store_job42_%d" % os.getpid())
     st.close()
     assert not os.path.exists(st.path)
+
+
+def _store_rank(path, world, rank, q):
+    sys.path.insert(0, os.path.dirname(HERE))
+    import sod_pkg
+    sod_pkg.load()
+    from sift_based_od_amd.sharded import FileStore
+    st = FileStore(world, rank, path=path, timeout=60, join_timeout=30)
+    got = st.broadcast_bytes(b"fresh-%d" % os.getpid() if rank == 0 else b"")
+    parts = st.allgather_bytes(b"r%d" % rank)
+    q.put((rank, got, parts))
+    st.close()
+
+
+def test_file_store_ignores_an_unclosed_runs_files(tmp_path):
+    """a crashed run's files (its join marks, an RCCL-id broadcast, all-gather
+    payloads, an old generation and ready mark) stay in the directory; a new run there must
+    neither join on them nor read their payloads."""
+    import json
+    import multiprocessing as mp
+    path = tmp_path / "store"
+    path.mkdir()
+    old = "deadbeef"
+    (path / "gen").write_bytes(old.encode())
+    (path / ("%s_ready" % old)).write_bytes(json.dumps({"1": "x"}).encode())
+    for name, data in [("join_0", b""), ("join_1", b""), ("b0", b"stale"), ("g1_0", b"stale"),
+                       ("g1_1", b"stale"), ("%s_b0" % old, b"stale"), ("%s_g1_0" % old, b"stale"),
+                       ("%s_g1_1" % old, b"stale"), ("%s_join_1" % old, b"x")]:
+        (path / name).write_bytes(data)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    # rank 1 first: it reads the stale generation before rank 0 clears it
+    procs = [ctx.Process(target=_store_rank, args=(str(path), 2, r, q)) for r in (1, 0)]
+    procs[0].start()
+    import time
+    time.sleep(1.0)
+    procs[1].start()
+    out = dict((r, (g, p)) for r, g, p in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert out[0][0].startswith(b"fresh-") and out[1][0] == out[0][0]
+    assert out[0][1] == out[1][1] == [b"r0", b"r1"]
+    assert not path.exists()   # close() removed the directory
