@@ -528,10 +528,11 @@ extern "C" int sod_debug_scounts(unsigned long long* out, int reset) {
 
 // the streamed kernel for one query image up to ~10k queries (measured: match_s vs match_i8
 // per query count); sod_match_set_kernel forces either
+constexpr bool kStreamedAuto = false;   // not yet faster than the ring kernel anywhere
 bool sod_match_use_s(const sod_ctx* ctx) {
   if (ctx->impl != 1) return false;
   if (ctx->mkernel) return ctx->mkernel == 2;
-  return ctx->nqt >= 24 && ctx->nqt <= 640;
+  return kStreamedAuto && ctx->nqt >= 24 && ctx->nqt <= 640;
 }
 
 // words per query of one shared-threshold slot: match_i8's kThrWords, or the streamed
