@@ -145,6 +145,14 @@ int sod_match_set_impl(sod_ctx* ctx, int impl);
  * streaming its own DB rows from HBM; one query image .. ~10k queries).  Same results bit for
  * bit; replaces cv2.BFMatcher().knnMatch's single loop (main.py:70-71). */
 int sod_match_set_kernel(sod_ctx* ctx, int kernel);
+/* 1 when the device's cos / sin (a restatement of glibc 2.35's x86_64 FMA-variant sin / cos,
+ * glibc_trig.h) equal this host's libm bit for bit -- the math.cos / math.sin that
+ * estimate_object_pose calls (HoughTransformHelperFunctions.py:31-32): poses, bin indices and
+ * PoseBin means (PoseBin.py:20-28) are then the reference's with no host redo.  0: another
+ * libm; the boundary guard and the exact-means redo then re-do the affected values with it. */
+int sod_trig_exact(sod_ctx* ctx);
+/* the device's glibc sin / cos of n angles (host arrays; |x| < 105414350): a test hook */
+int sod_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double* c);
 /* Matcher on a stream of its own (1) or on the context stream (0, default).  With 1 the
  * matcher kernel of the next sod_match_enqueue / sod_pipeline_enqueue only waits for the
  * previous merge of its partial results (and for the last descriptor upload), so it overlaps

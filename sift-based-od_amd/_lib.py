@@ -69,6 +69,8 @@ SIGNATURES = {
     "sod_match_enqueue": (C.c_int, [c_ctx]),
     "sod_match_set_impl": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_set_kernel": (C.c_int, [c_ctx, C.c_int]),
+    "sod_trig_exact": (C.c_int, [c_ctx]),
+    "sod_glibc_sincos": (C.c_int, [c_ctx, C.c_int64, c_vp, c_vp, c_vp]),
     "sod_match_set_overlap": (C.c_int, [c_ctx, C.c_int]),
     "sod_set_cu_reserve": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
@@ -268,6 +270,19 @@ class Context:
         32x32x32); call before uploads."""
         self._chk(self._L.sod_match_set_impl(self._h, self.IMPLS[impl] if isinstance(impl, str)
                                              else int(impl)))
+
+    def trig_exact(self):
+        """True when the device's cos / sin are this host's libm bit for bit (then poses,
+        bins and PoseBin means equal the reference's without any host redo)."""
+        return self._L.sod_trig_exact(self._h) == 1
+
+    def glibc_sincos(self, x):
+        """The device's glibc sin / cos of the angles x (test hook)."""
+        x = np.ascontiguousarray(x, np.float64)
+        s, c = np.empty_like(x), np.empty_like(x)
+        self._chk(self._L.sod_glibc_sincos(self._h, len(x), x.ctypes.data_as(C.c_void_p),
+                                           s.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p)))
+        return s, c
 
     KERNELS = {"auto": 0, "ring": 1, "streamed": 2}
 

@@ -315,6 +315,7 @@ int sod_create(int device, sod_ctx** out) {
     if (e == hipSuccess) {
       ctx->num_cus = prop.multiProcessorCount;
       ctx->gfx950 = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+      ctx->trig_exact = sod_host_trig_matches_device();
       int nx = 0;
       if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, device) == hipSuccess && nx > 0)
         ctx->num_xcds = nx;
@@ -812,6 +813,42 @@ static hipError_t make_stream(hipStream_t* s, const std::vector<uint32_t>& mask)
   return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
 }
 
+// Every event of the context recorded once more, on stream s (empty markers, complete at
+// once).  An event keeps a reference to the command it was last recorded with, and through it
+// to that command's stream; sod_set_cu_reserve destroys the old (CU-masked) streams, and
+// hipStreamDestroy of a stream whose commands are still referenced by events -- the slot
+// release / completion events (ev_merged, ev_matched*, recorded by the merge's and the
+// matcher's own dispatches), the fork / join and read events of the PoseBin means, the timing
+// rings -- hung in round 4 about one suite run in three (r04e / r04f: after "streams idle",
+// never "old streams destroyed"; sod_destroy, which destroys the events before the streams,
+// never hung).  Re-recorded on the new context stream, no event references an old stream.
+static hipError_t rebind_events(sod_ctx* ctx, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  auto rec = [&](hipEvent_t ev) {
+    if (ev && e == hipSuccess) e = hipEventRecord(ev, s);
+  };
+  for (auto& ev : ctx->ev) rec(ev);
+  for (auto& pr : ctx->mev)
+    for (auto& ev : pr) rec(ev);
+  for (auto& pr : ctx->seg_ev)
+    for (auto& ev : pr) rec(ev);
+  rec(ctx->ev_fork);
+  rec(ctx->ev_join);
+  rec(ctx->ev_inputs);
+  rec(ctx->ev_matched);
+  rec(ctx->ev_matched1);
+  for (int i = 0; i < 2; ++i) {
+    rec(ctx->ev_merged[i]);
+    rec(ctx->ev_hread[i]);
+    rec(ctx->ev_sread[i]);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  ctx->nmatch = 0;    // the timing rings hold no launch now
+  ctx->nseg = 0;
+  ctx->seg_open = false;
+  return e;
+}
+
 int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
   SOD_TRY(set_dev(ctx));
   const int nx = ctx->num_xcds;
@@ -869,6 +906,15 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
     return sod_fail(ctx, SOD_EHIP, std::string("cu reserve: ") + hipGetErrorString(e));
   }
   if (dbg) std::fprintf(stderr, "sod: cu_reserve new streams %p %p %p\n", (void*)s, (void*)sd, (void*)ms);
+  e = rebind_events(ctx, s);
+  if (e != hipSuccess) {
+    (void)hipStreamDestroy(s);
+    (void)hipStreamDestroy(sd);
+    (void)hipStreamDestroy(ms);
+    (void)hipStreamDestroy(ms2);
+    return sod_fail(ctx, SOD_EHIP, std::string("cu reserve: events: ") + hipGetErrorString(e));
+  }
+  if (dbg) std::fprintf(stderr, "sod: cu_reserve events re-recorded on the new stream\n");
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->mstream);
@@ -897,6 +943,28 @@ int sod_match_set_impl(sod_ctx* ctx, int impl) {
     ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
   }
   return SOD_OK;
+}
+
+int sod_trig_exact(sod_ctx* ctx) { return ctx ? (ctx->trig_exact ? 1 : 0) : SOD_EINVAL; }
+
+int sod_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double* c) {
+  SOD_TRY(set_dev(ctx, false));
+  if (n < 0 || (n > 0 && (!x || !s || !c))) return sod_fail(ctx, SOD_EINVAL, "bad arguments");
+  if (n == 0) return SOD_OK;
+  DevBuf<double> dx, ds, dc;
+  int rc = upload(ctx, dx, x, (size_t)n);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, ds, (size_t)n);
+  if (rc == SOD_OK) rc = sod_reserve(ctx, dc, (size_t)n);
+  if (rc == SOD_OK) rc = launch_glibc_sincos(ctx, n, dx.p, ds.p, dc.p);
+  if (rc == SOD_OK) rc = download(ctx, s, ds.p, (size_t)n);
+  if (rc == SOD_OK) rc = download(ctx, c, dc.p, (size_t)n);
+  if (rc == SOD_OK && sod_stream_sync(ctx->stream) != hipSuccess)
+    rc = sod_fail(ctx, SOD_EHIP, "glibc sincos failed");
+  (void)sod_stream_sync(ctx->stream);
+  sod_release(dx);
+  sod_release(ds);
+  sod_release(dc);
+  return rc;
 }
 
 int sod_match_set_kernel(sod_ctx* ctx, int kernel) {

@@ -31,6 +31,7 @@
 
 #include <hip/hip_ext.h>
 
+#include "glibc_trig.h"
 #include "sod_internal.h"
 
 namespace {
@@ -92,7 +93,8 @@ __device__ __forceinline__ void pose_bins(float mx, float my, float ma, int mo, 
   int k;
   double s, tx, ty, a;
   pose_terms(mx, my, ma, mo, qa, qo, cx, cy, k, s, tx, ty, a);
-  const double ca = cos(a), sa = sin(a);
+  // glibc's cos / sin bit for bit (glibc_trig.h): math.cos / math.sin of HTHF:31-32
+  const double ca = gtrig::cos(a), sa = gtrig::sin(a);
   const double x = (ca * tx - sa * ty) + (double)qx;
   const double y = (sa * tx + ca * ty) + (double)qy;
   pose[0] = x;
@@ -105,8 +107,12 @@ __device__ __forceinline__ void pose_bins(float mx, float my, float ma, int mo, 
 }
 
 // ---- boundary guard (SURVEY 7 "Hough parity") -------------------------------------------
+// Round 5: the device's cos / sin are glibc's x86_64 FMA variant bit for bit (glibc_trig.h),
+// so every pose is the reference's and the guard is armed only when the host's libm is a
+// different variant (sod_trig_exact() == 0: a CPU without FMA / AVX2), whose last bits the
+// reference there follows; the launchers then pass the record buffer, else nullptr.
 // Every step of the pose is one correctly rounded IEEE operation, the same on both sides,
-// except cos/sin: the device's (ocml) and glibc's (math.cos / math.sin of the reference,
+// except cos/sin: the device's and glibc's (math.cos / math.sin of the reference,
 // HTHF:31-32) may round differently by an ulp or two.  The x / y bin indices are then still
 // exact unless v = (x*b)/W lies within that error of an integer where int(v)-1 clamped to
 // [0, b-1] (HTHF:49-58) steps -- 2..b.  Such matches are listed (guard records) and done
@@ -211,7 +217,7 @@ __global__ void pose_kernel(int64_t nq, const uint8_t* __restrict__ good,
   const float fqx = qx[q], fqy = qy[q];
   pose_bins(mx[m], my[m], ma[m], mo[m], fqx, fqy, qa[q], qo[q], cent[2 * im], cent[2 * im + 1],
             H, W, b, lut, p, ix, t);
-  if (guard_flag(p, t, fqx, fqy, H, W, b)) guard_push(grec, gstat, q, p, t, fqx, fqy, H, W);
+  if (grec && guard_flag(p, t, fqx, fqy, H, W, b)) guard_push(grec, gstat, q, p, t, fqx, fqy, H, W);
   pose[4 * q + 0] = p[0];
   pose[4 * q + 1] = p[1];
   pose[4 * q + 2] = p[2];
@@ -264,7 +270,7 @@ __global__ void pose_batch_kernel(int64_t n, const float* __restrict__ mx,
   int ix[4];
   pose_bins(mx[i], my[i], ma[i], mo[i], qx[i], qy[i], qa[i], qo[i], cx[i], cy[i], H, W, b, lut, p,
             ix, t);
-  if (guard_flag(p, t, qx[i], qy[i], H, W, b)) guard_push(grec, gstat, i, p, t, qx[i], qy[i], H, W);
+  if (grec && guard_flag(p, t, qx[i], qy[i], H, W, b)) guard_push(grec, gstat, i, p, t, qx[i], qy[i], H, W);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     pose[4 * i + j] = p[j];
@@ -1180,7 +1186,7 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
       fmy = my[m];
       pose_bins(fmx, fmy, ma[m], mo[m], fqx, fqy, qa[q], qo[q], cent[2 * im], cent[2 * im + 1],
                 H, W, b, lut, p, ix, t);
-      if (guard_flag(p, t, fqx, fqy, H, W, b)) guard_push(grec, gstat, q, p, t, fqx, fqy, H, W);
+      if (grec && guard_flag(p, t, fqx, fqy, H, W, b)) guard_push(grec, gstat, q, p, t, fqx, fqy, H, W);
       pose[4 * q + 0] = p[0];
       pose[4 * q + 1] = p[1];
       pose[4 * q + 2] = p[2];
@@ -1868,7 +1874,50 @@ int launch_pose_batch(sod_ctx* ctx, int64_t n, const float* mx, const float* my,
   const int bs = 256;
   hipLaunchKernelGGL(pose_batch_kernel, dim3((unsigned)cdiv(n, bs)), dim3(bs), 0, ctx->stream, n,
                      mx, my, ma, mo, qx, qy, qa, qo, cx, cy, ctx->qh, ctx->qw, ctx_bins(ctx),
-                     ctx->sig_lut.p, pose, idx, grec, gstat);
+                     ctx->sig_lut.p, pose, idx, ctx->trig_exact ? nullptr : grec, gstat);
+  SOD_HIP(ctx, hipGetLastError());
+  return SOD_OK;
+}
+
+// Does the host's libm compute sin / cos as glibc_trig.h does (x86_64 glibc, FMA variant)?
+// 20 000 angles in [0, 2 pi) plus branch edges, called through volatile pointers (a compiler
+// may fold sin(x), cos(x) into sincos(), whose last bits differ).  The non-FMA variants
+// differ from the FMA one in ~0.07 % of angles, so a different libm shows ~14 differences.
+bool sod_host_trig_matches_device() {
+  static int cached = -1;
+  if (cached >= 0) return cached == 1;
+  double (*volatile hs)(double) = ::sin;
+  double (*volatile hc)(double) = ::cos;
+  uint64_t st = 0x9E3779B97F4A7C15ull;
+  bool ok = true;
+  for (int i = 0; i < 20000 && ok; ++i) {
+    st ^= st << 13;
+    st ^= st >> 7;
+    st ^= st << 17;
+    double x = (double)(st >> 11) * 0x1p-53 * 6.283185307179586;
+    if (i < 8) x = (const double[]){0.126, 0.855468749, 0.85546875, 2.4262652397, 2.42626524,
+                                    3.141592653589793, 1.5707963267948966, 6.28318530717958}[i];
+    ok = gtrig::ubits(hs(x)) == gtrig::ubits(gtrig::sin(x)) &&
+         gtrig::ubits(hc(x)) == gtrig::ubits(gtrig::cos(x));
+  }
+  cached = ok ? 1 : 0;
+  return ok;
+}
+
+// the device's glibc sin / cos of n angles (test hook: sod_glibc_sincos)
+namespace {
+__global__ void glibc_sincos_kernel(int64_t n, const double* __restrict__ x, double* __restrict__ s,
+                                    double* __restrict__ c) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  s[i] = gtrig::sin(x[i]);
+  c[i] = gtrig::cos(x[i]);
+}
+}  // namespace
+
+int launch_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double* c) {
+  hipLaunchKernelGGL(glibc_sincos_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, ctx->stream,
+                     n, x, s, c);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
@@ -1968,11 +2017,11 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
                      ctx->qh, ctx->qw, qimg_p(ctx), ctx->n_qimg ? ctx->qshape.p : nullptr,
                      ctx_bins(ctx), ctx->sig_lut.p, own_lo, own_hi, ctx->pose.p,
                      ctx->basekey.p, ctx->vmask.p, ctx->nbins, ctx->counts.p, ctx->first.p,
-                     ctx->isize.p, reinterpret_cast<int2*>(ctx->msize.p), ctx->grec.p,
-                     ctx->gstat.p);
+                     ctx->isize.p, reinterpret_cast<int2*>(ctx->msize.p),
+                     ctx->trig_exact ? nullptr : ctx->grec.p, ctx->gstat.p);
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(launch_hist(ctx));
-  ctx->guard_done = false;
+  ctx->guard_done = ctx->trig_exact;   // nothing listed: no read-back before the results
   ctx->hist_dense = true;
   return SOD_OK;
 }
@@ -2376,11 +2425,12 @@ int launch_hough_small(sod_ctx* ctx, int32_t thr) {
                         ctx->mang.p, ctx->moct.p, ctx->mimg.p, ctx->cent.p, ctx->isize.p, ctx->qh,
                         ctx->qw, ctx_bins(ctx), ctx->sig_lut.p, (uint32_t)thr, ctx->pose.p,
                         ctx->basekey.p, ctx->vmask.p, reinterpret_cast<int2*>(ctx->msize.p),
-                        ctx->grec.p, ctx->gstat.p, ctx->vbin.p, ctx->cursor.p, ctx->vfirst_s.p,
+                        ctx->trig_exact ? nullptr : ctx->grec.p, ctx->gstat.p, ctx->vbin.p,
+                        ctx->cursor.p, ctx->vfirst_s.p,
                         ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->amx.p, ctx->amy.p,
                         ctx->aqx.p, ctx->aqy.p, ctx->aisig.p);
   SOD_HIP(ctx, hipGetLastError());
-  ctx->guard_done = false;
+  ctx->guard_done = ctx->trig_exact;
   ctx->hist_dense = false;
   ctx->gathered = true;
   // the PoseBin means wait for the affine enqueue, which runs them in the same launch

@@ -70,10 +70,10 @@ constexpr int kLag = SOD_S_LAG;
 #define SOD_S_XCHG 1              // thresholds shared between the waves of a query group
 #endif
 constexpr bool kXchg = SOD_S_XCHG;
-#ifndef SOD_S_EARLYB
-#define SOD_S_EARLYB 1            // bodies that exchange thresholds after every window
+#ifndef SOD_S_FIRSTX
+#define SOD_S_FIRSTX 1            // first window whose end applies the global words
 #endif
-constexpr int kEarlyB = SOD_S_EARLYB;
+constexpr int kFirstX = SOD_S_FIRSTX;
 #ifndef SOD_S_SEEDPUB
 #define SOD_S_SEEDPUB 1           // the seeds' best rows go out at once
 #endif
@@ -402,7 +402,13 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
 
   const int rowl = row_offset + (int)(s_lo * kSubRows) + g * 4;
   const int nbody = (nloc + kSD - 1) / kSD;
-  for (int b = 0; b < nbody; ++b) {
+  // one loop body = kSW windows; the first body is peeled (Early): it exchanges after every
+  // window from window kFirstX on and only loads before (the leaders' seeds must land first:
+  // a load issued with the seeds in flight reads nothing, and then every work-group would
+  // publish every query's best -- the storm the leaders avoid), so that the steady-state
+  // loop's single exchange reads words loaded a whole body (kSD subtiles of loads) earlier
+  auto body = [&](auto Early, int b) {
+    constexpr bool early = Early;
 #ifdef SOD_S_STAMP
     if (b > 0 && b <= 10) SSTAMP(14 + b);
 #endif
@@ -461,7 +467,9 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
       for (int j = 0; j < kSN; ++j) load_sub(ring[w * kSN + j], (b + 1) * kSD + w * kSN + j);
       // exchange (the words loaded one exchange ago; then the next loads): after every window
       // of the first kEarlyB bodies, while the bounds still move fast, then once per body
-      if (b < kEarlyB || w == kSW - 1) {
+      if constexpr (early && w < kFirstX) {
+        exch_load();
+      } else if constexpr (early || w == kSW - 1) {
         exch_apply();
         exch_load();
         pull();
@@ -470,7 +478,9 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
       if (b == 0) SSTAMP(9 + 2 * w);
 #endif
     });
-  }
+  };
+  if (nbody > 0) body(std::true_type{}, 0);
+  for (int b = 1; b < nbody; ++b) body(std::false_type{}, b);
   SSTAMP(25);
 #ifdef SOD_S_STAMP
   if (lane == 0 && blockIdx.x * 4 + wave < 4096)

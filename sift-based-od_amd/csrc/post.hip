@@ -293,7 +293,9 @@ int sod_postprocess(sod_ctx* ctx, int32_t* n_bins, int32_t* bin_index, int32_t* 
   // the survivors' x / y means as the reference computes them (glibc cos / sin per member,
   // sod_exact_xy_means): the position relation's <= thresholds (PostProcessing.py:24-28) and
   // the final pose then see the reference's values bit for bit
-  if (ctx->post_exact && n) SOD_TRY(sod_exact_xy_means(ctx, idx.data(), n, sel.data()));
+  // (with the device's glibc cos / sin the device means are those values already)
+  if (ctx->post_exact && !ctx->trig_exact && n)
+    SOD_TRY(sod_exact_xy_means(ctx, idx.data(), n, sel.data()));
   PostOut o;
   SOD_TRY(run_post(ctx, n, sel.data(), img.empty() ? nullptr : img.data(), o));
   return write_post(o, n_pos, pos_off, pos_members, n_ori, ori_pos_off, ori_off, ori_members,

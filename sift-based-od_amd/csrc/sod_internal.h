@@ -220,6 +220,11 @@ struct sod_ctx {
   hipStream_t mstream_of(int slot) const { return mtwo && slot ? mstream2 : mstream; }
   bool stage_timing = true;   // sod_set_stage_timing: ev[2..5] around the tail stages
   bool post_exact = true;     // sod_set_post_exact: survivors' x / y means redone with glibc
+                              // (only while !trig_exact)
+  // the device's cos / sin (glibc_trig.h) equal the host's libm bit for bit (checked once per
+  // process, sod_host_trig_matches_device): poses, bins and PoseBin means are the reference's
+  // without the boundary guard's host redo or the exact-means redo, which stay armed otherwise
+  bool trig_exact = false;
   // sod_exact_xy_means: bin list + record offsets, the pose records, their pinned host copy
   DevBuf<int32_t> xr_idx;
   DevBuf<double> xr_rec;
@@ -421,4 +426,6 @@ void sod_guard_host_pose(const double rec[8], const int32_t bins[4], double* x, 
                          int32_t* ix, int32_t* iy);
 int sod_build_sigma_lut(sod_ctx* ctx, int32_t bins_sigma);
 int sod_exact_xy_means(sod_ctx* ctx, const int32_t* vbin, int nb, double* means6);
+bool sod_host_trig_matches_device();
+int launch_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double* c);
 void sod_sift_free(sod_ctx* ctx);

@@ -277,10 +277,11 @@ class Main:
             finally:
                 if gc_was_on:
                     gc.enable()
-            if out:
-                # the survivors' centroids as the reference computes them (glibc cos / sin per
-                # member, sod_exact_means): post_process's <= thresholds and final pose then see
-                # main.py's values bit for bit (the device means differ in the last ulps)
+            if out and not self.ctx.trig_exact():
+                # the device's cos / sin are not this host's libm (sod_trig_exact): the
+                # survivors' centroids as the reference computes them here (the host's cos /
+                # sin per member, sod_exact_means), so post_process's <= thresholds and the
+                # final pose see main.py's values bit for bit
                 sidx = [i for i, k in enumerate(survived) if k]
                 for b, (x, y) in zip(out, self.ctx.exact_means(sidx).tolist()):
                     b.centroid = (x, y)

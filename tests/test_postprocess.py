@@ -124,7 +124,8 @@ def test_device_post_batch_vs_oracle(ctx, n, seed):
 @pytest.mark.parametrize("name", ["c1_b15", "planted_b15", "planted_b12"])
 def test_pipeline_postprocess_golden(ctx, name):
     """Full device pipeline then post-processing over the survivors == main.py's final
-    pose (PoseBin means carry device cos/sin: 1e-12 relative)."""
+    pose bit for bit (with the device's glibc cos / sin even without the host's redo of the
+    survivors' x / y means, sod_set_post_exact(0))."""
     from helpers import kp
     g = golden(name)
     ctx.set_keypoints(kp(g, "db_"), g["db_img"], g["centroid"], g["size"])
@@ -137,9 +138,12 @@ def test_pipeline_postprocess_golden(ctx, name):
     # final pose bit for bit
     assert np.array_equal(r["final_pose"].view(np.uint64),
                           np.asarray(g["final_pose"], np.float64).view(np.uint64))
-    ctx.set_post_exact(False)   # the device means (device cos / sin): within 1e-12
+    ctx.set_post_exact(False)   # the device means alone
     r = ctx.postprocess()
     ctx.set_post_exact(True)
+    if ctx.trig_exact():   # device glibc cos / sin: already main.py's bit for bit
+        assert np.array_equal(r["final_pose"].view(np.uint64),
+                              np.asarray(g["final_pose"], np.float64).view(np.uint64))
     np.testing.assert_allclose(r["final_pose"], g["final_pose"], rtol=1e-12, atol=1e-9)
 
 
