@@ -153,6 +153,16 @@ int sod_match_set_kernel(sod_ctx* ctx, int kernel);
 int sod_trig_exact(sod_ctx* ctx);
 /* the device's glibc sin / cos of n angles (host arrays; |x| < 105414350): a test hook */
 int sod_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double* c);
+/* Tuning / test switches of this context, by name (integers; read at the next enqueue).
+ * sod_create seeds each from the environment variable SOD_<NAME> once.  Names: match_qt,
+ * match_pf (LDS-ring matcher tiles per wave / prefetch), hough_fused (0: never the
+ * one-work-group Hough kernel), select_multi (1: multi-kernel selection for small windows),
+ * sift_stream_mask, sift_sort_max, sift_desc_range_max, sift_layer_split, sift_side_mask,
+ * sift_fork2, sift_early_desc, sift_direct, sift_eager_rank (SIFT scheduling A/B and the
+ * rank / ranged-enumeration test paths), debug_sync (stderr trace of long stream waits).
+ * None changes results.  SOD_EINVAL for an unknown name. */
+int sod_set_option(sod_ctx* ctx, const char* name, int64_t value);
+int sod_get_option(sod_ctx* ctx, const char* name, int64_t* value);
 /* Matcher on a stream of its own (1) or on the context stream (0, default).  With 1 the
  * matcher kernel of the next sod_match_enqueue / sod_pipeline_enqueue only waits for the
  * previous merge of its partial results (and for the last descriptor upload), so it overlaps

@@ -71,6 +71,8 @@ SIGNATURES = {
     "sod_match_set_kernel": (C.c_int, [c_ctx, C.c_int]),
     "sod_trig_exact": (C.c_int, [c_ctx]),
     "sod_glibc_sincos": (C.c_int, [c_ctx, C.c_int64, c_vp, c_vp, c_vp]),
+    "sod_set_option": (C.c_int, [c_ctx, C.c_char_p, C.c_int64]),
+    "sod_get_option": (C.c_int, [c_ctx, C.c_char_p, C.POINTER(C.c_int64)]),
     "sod_match_set_overlap": (C.c_int, [c_ctx, C.c_int]),
     "sod_set_cu_reserve": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_allgather_enqueue": (C.c_int, [c_ctx]),
@@ -285,6 +287,22 @@ class Context:
         return s, c
 
     KERNELS = {"auto": 0, "ring": 1, "streamed": 2}
+
+    OPTIONS = ("match_qt", "match_pf", "hough_fused", "select_multi", "sift_stream_mask",
+               "sift_sort_max", "sift_desc_range_max", "sift_layer_split", "sift_side_mask",
+               "sift_fork2", "sift_early_desc", "sift_direct", "sift_eager_rank", "debug_sync")
+
+    def set_option(self, name, value):
+        """A tuning / test switch of this context by name (sod.h sod_set_option); returns the
+        previous value.  None of them changes results."""
+        old = self.get_option(name)
+        self._chk(self._L.sod_set_option(self._h, name.encode(), int(value)))
+        return old
+
+    def get_option(self, name):
+        v = C.c_int64()
+        self._chk(self._L.sod_get_option(self._h, name.encode(), C.byref(v)))
+        return v.value
 
     def set_match_kernel(self, kernel):
         """Kernel shape of the int8 matcher: "auto" (by query count, default), "ring" (LDS

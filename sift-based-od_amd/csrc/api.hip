@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 #include <vector>
 
@@ -302,11 +303,66 @@ int sod_device_count(int* n) {
   return SOD_OK;
 }
 
+namespace {
+struct OptEntry {
+  const char* name;
+  int sod_opts::*field;
+};
+const OptEntry kOpts[] = {
+    {"match_qt", &sod_opts::match_qt},
+    {"match_pf", &sod_opts::match_pf},
+    {"hough_fused", &sod_opts::hough_fused},
+    {"select_multi", &sod_opts::select_multi},
+    {"sift_stream_mask", &sod_opts::sift_stream_mask},
+    {"sift_sort_max", &sod_opts::sift_sort_max},
+    {"sift_desc_range_max", &sod_opts::sift_desc_range_max},
+    {"sift_layer_split", &sod_opts::sift_layer_split},
+    {"sift_side_mask", &sod_opts::sift_side_mask},
+    {"sift_fork2", &sod_opts::sift_fork2},
+    {"sift_early_desc", &sod_opts::sift_early_desc},
+    {"sift_direct", &sod_opts::sift_direct},
+    {"sift_eager_rank", &sod_opts::sift_eager_rank},
+    {"debug_sync", &sod_opts::debug_sync},
+};
+const OptEntry* find_opt(const char* name) {
+  for (const OptEntry& o : kOpts)
+    if (name && std::strcmp(o.name, name) == 0) return &o;
+  return nullptr;
+}
+// SOD_<NAME> of the environment, read once at sod_create
+void opts_from_env(sod_opts& op) {
+  for (const OptEntry& o : kOpts) {
+    std::string env = "SOD_";
+    for (const char* c = o.name; *c; ++c) env += (char)std::toupper((unsigned char)*c);
+    if (const char* e = std::getenv(env.c_str())) op.*(o.field) = std::atoi(e);
+  }
+  if (op.debug_sync) sod_debug_sync = 1;
+}
+}  // namespace
+
+int sod_set_option(sod_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx) return SOD_EINVAL;
+  const OptEntry* o = find_opt(name);
+  if (!o) return sod_fail(ctx, SOD_EINVAL, std::string("unknown option ") + (name ? name : "(null)"));
+  ctx->opt.*(o->field) = (int)value;
+  sod_debug_sync = ctx->opt.debug_sync != 0;
+  return SOD_OK;
+}
+
+int sod_get_option(sod_ctx* ctx, const char* name, int64_t* value) {
+  if (!ctx || !value) return SOD_EINVAL;
+  const OptEntry* o = find_opt(name);
+  if (!o) return sod_fail(ctx, SOD_EINVAL, std::string("unknown option ") + (name ? name : "(null)"));
+  *value = ctx->opt.*(o->field);
+  return SOD_OK;
+}
+
 int sod_create(int device, sod_ctx** out) {
   if (!out) return SOD_EINVAL;
   *out = nullptr;
   sod_ctx* ctx = new sod_ctx();
   ctx->device = device;
+  opts_from_env(ctx->opt);
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) {
@@ -876,7 +932,7 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
                           std::to_string(per_xcd * nx) +
                           " CUs: call sod_set_cu_reserve before sod_comm_init");
   }
-  if (std::getenv("SOD_DEBUG_SYNC"))
+  if (ctx->opt.debug_sync)
     std::fprintf(stderr, "sod: cu_reserve %d -> %d: stream %p side %p mstream %p\n", ctx->cu_reserve,
                  per_xcd, (void*)ctx->stream, (void*)ctx->side, (void*)ctx->mstream);
   SOD_HIP(ctx, sod_stream_drain(ctx->side));
@@ -885,7 +941,7 @@ int sod_set_cu_reserve(sod_ctx* ctx, int per_xcd) {
   SOD_HIP(ctx, sod_stream_drain(ctx->stream));
   ctx->side_pending = false;
   ctx->ev_done[0] = ctx->ev_done[1] = nullptr;
-  const bool dbg = std::getenv("SOD_DEBUG_SYNC") != nullptr;
+  const bool dbg = ctx->opt.debug_sync != 0;
   if (dbg) std::fprintf(stderr, "sod: cu_reserve streams idle\n");
   const int n = ctx->num_cus, words = (n + 31) / 32, r = per_xcd * nx;
   std::vector<uint32_t> tail, match;

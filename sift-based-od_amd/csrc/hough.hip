@@ -2255,11 +2255,8 @@ static int run_compaction(sod_ctx* ctx, uint32_t thr, uint32_t* out, uint32_t* t
 
 static int launch_members_multi(sod_ctx* ctx, uint32_t thr, int64_t nq);
 static int launch_means(sod_ctx* ctx, bool on_main = false);
-// SOD_SELECT_MULTI=1: small windows take the multi-kernel path too (parity tests of both)
-static bool select_multi_forced() {
-  const char* e = std::getenv("SOD_SELECT_MULTI");
-  return e && e[0] == '1';
-}
+// option select_multi = 1: small windows take the multi-kernel path too (parity tests of both)
+static bool select_multi_forced(const sod_ctx* ctx) { return ctx->opt.select_multi == 1; }
 
 int launch_select(sod_ctx* ctx, int32_t thr, bool may_defer_means) {
   const int64_t nq = sod_win_n(ctx);
@@ -2282,7 +2279,7 @@ int launch_select(sod_ctx* ctx, int32_t thr, bool may_defer_means) {
     SOD_TRY(sod_reserve(ctx, ctx->vidx, (size_t)ctx->nbins));
     SOD_HIP(ctx, hipMemsetAsync(ctx->vidx.p, 0xFF, ctx->vidx.n * 4, ctx->stream));
   }
-  if (nq <= kSmallQ && !select_multi_forced()) {   // one work-group, one launch
+  if (nq <= kSmallQ && !select_multi_forced(ctx)) {   // one work-group, one launch
     hipLaunchKernelGGL(select_small_kernel, dim3(1), dim3(kSmallT), 0, ctx->stream, nq,
                        ctx->basekey.p, ctx->vmask.p, ctx->counts.p, ctx->first.p, ctx_bins(ctx),
                        qimg_p(ctx), ctx->nbins1, (uint32_t)thr, ctx->vbin.p, ctx->scal.p,
@@ -2381,8 +2378,7 @@ static int launch_means(sod_ctx* ctx, bool on_main) {
 // launch_affine_gather do for a window of <= kFusedQ queries of one image on one rank, in one
 // launch; the dense histogram is built only if something reads it (sod_hist_dense).
 bool sod_hough_small_ok(const sod_ctx* ctx) {
-  if (const char* e = std::getenv("SOD_HOUGH_FUSED"))
-    if (e[0] == '0') return false;
+  if (ctx->opt.hough_fused == 0) return false;
   return ctx->nranks <= 1 && !ctx->comm && ctx->n_qimg == 0 && sod_win_n(ctx) <= kFusedQ &&
          sod_win_n(ctx) >= 1;
 }

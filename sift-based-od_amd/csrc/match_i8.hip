@@ -1259,10 +1259,10 @@ extern "C" int sod_debug_stamps(unsigned long long* out, int n) {
 // Query tiles per wave for the 16x16x64 kernel.  A work-group holds 8*QT tiles; the chip is
 // filled by splitting the DB into chunks, and every chunk restarts its queries' top-2 (the
 // dense early phase), so fewer queries per work-group buy longer chunks and no padding tiles
-// for small query sets, at more LDS reads per MFMA.  SOD_MATCH_QT overrides (experiments).
-static int pick_qt(int32_t nqt) {
-  if (const char* e = std::getenv("SOD_MATCH_QT")) {
-    const int v = std::atoi(e);
+// for small query sets, at more LDS reads per MFMA.  Option match_qt overrides (experiments).
+static int pick_qt(const sod_ctx* ctx, int32_t nqt) {
+  {
+    const int v = ctx->opt.match_qt;
     if (v == 2 || v == 4 || v == 8) return v;
   }
   // measured (C3-sized DB, one MI355X): 8 from ~16 work-groups of 1024 queries up (20k
@@ -1273,10 +1273,10 @@ static int pick_qt(int32_t nqt) {
   return 2;
 }
 
-// LDS prefetch distance (subtiles) per query tiles per wave; SOD_MATCH_PF overrides
-static int pick_pf(int qt) {
-  if (const char* e = std::getenv("SOD_MATCH_PF")) {
-    const int v = std::atoi(e);
+// LDS prefetch distance (subtiles) per query tiles per wave; option match_pf overrides
+static int pick_pf(const sod_ctx* ctx, int qt) {
+  {
+    const int v = ctx->opt.match_pf;
     if (v == 1 || v == 2) return v;
   }
   return 1;
@@ -1286,7 +1286,7 @@ int launch_match_i8(sod_ctx* ctx) {
   const bool wide = ctx->impl == 2;
   const int rows = wide ? 32 : kSubRows;
   const int sps = wide ? w::SPS : SPS;
-  const int qt = wide ? w::QT : pick_qt(ctx->nqt);
+  const int qt = wide ? w::QT : pick_qt(ctx, ctx->nqt);
   const int qt_per_wg = wide ? w::NW * w::QT : NW16 * qt;
   const int64_t nq_pad = (int64_t)ctx->nqt * rows;
   const int64_t qblocks = cdiv(ctx->nqt, qt_per_wg);
@@ -1356,7 +1356,7 @@ int launch_match_i8(sod_ctx* ctx) {
                         ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),       \
                         ctx->nqt, nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, \
                         pd1, pidx, pd2, (int)qblocks, gthr, seedload)
-    const int pf = pick_pf(qt);
+    const int pf = pick_pf(ctx, qt);
     if (qt == 8) {
       if (pf == 2) SOD_LAUNCH_I8(8, 2); else SOD_LAUNCH_I8(8, 1);
     } else if (qt == 4) {

@@ -206,24 +206,37 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
     d.c = ok ? c : i32x4{kMaskC, kMaskC, kMaskC, kMaskC};
   };
 
-  // the query group, resident as MFMA B operands (the accumulator file: an MFMA reads its B
-  // operand from there directly; the VGPRs keep the DB ring, the thresholds, the accumulators)
-  i32x4 bq[QT][2];
-  sfor<QT>([&](auto T) {
-    constexpr int t = T;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)   // (padding tiles of the group's last wave read tile 0)
-      bq[t][k] = *reinterpret_cast<const i32x4*>(
-          qpack + ((int64_t)(t < ntile ? qt0 + t : qt0) * 2 + k) * 1024 + lane * 16);
-  });
-  // all loads in flight first, then pinned (a pin right after each load waited for each)
-#pragma unroll
-  for (int t = 0; t < QT; ++t)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) asm volatile("" : "+a"(bq[t][k]));
-
+  // the DB stream starts first (its HBM latency overlaps the query fragments' load)
   Sub ring[kSD];
   sfor<kSD>([&](auto J) { load_sub(ring[J], J); });
+
+  // the query group, resident as MFMA B operands (the accumulator file: an MFMA reads its B
+  // operand from there directly; the VGPRs keep the DB ring, the thresholds, the accumulators).
+  // The 64 KiB of fragments are loaded once per work-group (each wave a quarter, through the
+  // LDS the top-2 slots take later), not once per wave: 4x less L2 traffic at the start
+  // (1 024 waves reading the same 64 KiB took ~8 k cycles)
+  i32x4 bq[QT][2];
+  {
+    i32x4* stage = reinterpret_cast<i32x4*>(top2);   // [tile t][k][lane] = 64 KiB
+    static_assert(sizeof(top2) >= QT * 2 * 64 * 16, "fragment staging fits the top-2 slots");
+#pragma unroll
+    for (int i = 0; i < 2 * QT / kSNW; ++i) {
+      const int f = wave * (2 * QT / kSNW) + i;      // fragment (t, k) = (f / 2, f % 2)
+      const int t = f >> 1;
+      stage[f * 64 + lane] = *reinterpret_cast<const i32x4*>(
+          qpack + ((int64_t)(t < ntile ? qt0 + t : qt0) * 2 + (f & 1)) * 1024 + lane * 16);
+    }
+    __syncthreads();
+    sfor<QT>([&](auto T) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) bq[T][k] = stage[(2 * T + k) * 64 + lane];
+    });
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) asm volatile("" : "+a"(bq[t][k]));
+    __syncthreads();   // the staging area becomes the top-2 slots
+  }
   SSTAMP(1);
 
   int* const slot = top2 + wave * (QT * 3 * 64) + lane;   // + (t * 3 + f) * 64

@@ -1520,8 +1520,8 @@ int get_slot(sod_ctx* ctx, SiftWork& W, int i, SiftSlot** out) {
     // (round 3's layout: the lone image and the batches shared slot 0) and 7.3-7.5 ms with all
     // masked (SOD_SIFT_STREAM_MASK=0: none masked, 2: all)
     int masked = (int)W.slots.size() == kSlots + 1 ? 1 : 0;
-    if (const char* e = std::getenv("SOD_SIFT_STREAM_MASK"))
-      masked = std::atoi(e) == 2 ? 1 : std::atoi(e) == 0 ? 0 : masked;
+    if (ctx->opt.sift_stream_mask == 2 || ctx->opt.sift_stream_mask == 0)
+      masked = ctx->opt.sift_stream_mask == 2 ? 1 : 0;
     if (masked && ctx->num_cus > 2) {
       std::vector<uint32_t> mask((size_t)(ctx->num_cus + 31) / 32, 0u);
       for (int i = 1; i < ctx->num_cus; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
@@ -1672,10 +1672,10 @@ void plan_pyramid(int L, int w, int h, Pyr& P, int64_t& go, int64_t& dof, int& o
     }
 }
 
-// SOD_SIFT_SORT_MAX (tests): a lower one-work-group limit, so the rank path runs too
-int sort_max() {
+// option sift_sort_max (tests): a lower one-work-group limit, so the rank path runs too
+int sort_max(const sod_ctx* ctx) {
   int smax = kSortMax;
-  if (const char* e = std::getenv("SOD_SIFT_SORT_MAX")) smax = std::max(-1, std::min(kSortMax, std::atoi(e)));
+  if (ctx->opt.sift_sort_max != -2) smax = std::max(-1, std::min(kSortMax, ctx->opt.sift_sort_max));
   return smax;
 }
 
@@ -1698,10 +1698,9 @@ int enqueue_rank(sod_ctx* ctx, SiftSlot& S, int smax) {
 // descriptors of the final list, then the counts to the host
 int enqueue_describe(sod_ctx* ctx, SiftSlot& S, int lane_order) {
   hipStream_t st = S.stream;
-  // SOD_SIFT_DESC_RANGE_MAX (tests): a lower window-row limit of the ranged enumeration
+  // option sift_desc_range_max (tests): a lower window-row limit of the ranged enumeration
   int rmax = kDescSide;
-  if (const char* e = std::getenv("SOD_SIFT_DESC_RANGE_MAX"))
-    rmax = std::max(0, std::min(kDescSide, std::atoi(e)));
+  if (ctx->opt.sift_desc_range_max >= 0) rmax = std::min(kDescSide, ctx->opt.sift_desc_range_max);
   if (S.early_desc)
     hipLaunchKernelGGL(gather_desc_kernel, dim3(1024), dim3(256), 0, st,
                        reinterpret_cast<const float4*>(S.rdesc.p), S.src.p, S.cnt.p + 2,
@@ -1756,14 +1755,13 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
   const bool split = lone && tot > 0 && o_small < nOct;
   bool lsplit = split && pyramid && W.radius[L + 1] >= 1 && W.radius[L + 1] <= kMaxR &&
                 W.radius[L + 2] >= 1 && W.radius[L + 2] <= kMaxR;
-  int nsplit = kMaxOct;   // SOD_SIFT_LAYER_SPLIT=n (A/B): only the first n octaves split
-  if (const char* e = std::getenv("SOD_SIFT_LAYER_SPLIT")) nsplit = std::max(0, std::atoi(e));
+  int nsplit = kMaxOct;   // option sift_layer_split = n (A/B): only the first n octaves split
+  if (ctx->opt.sift_layer_split >= 0) nsplit = ctx->opt.sift_layer_split;
   if (split && !S.side) {
-    // the side stream leaves one CU out of its mask (SOD_SIFT_SIDE_MASK=0: all CUs): the
+    // the side stream leaves one CU out of its mask (option sift_side_mask 0: all CUs): the
     // small-octave chain (one 1 024-thread work-group, ~146 KB of LDS) then always finds a
     // free CU instead of waiting for the extrema launch's work-groups to drain
-    int keep_free = 1;
-    if (const char* e = std::getenv("SOD_SIFT_SIDE_MASK")) keep_free = std::atoi(e) != 0;
+    const int keep_free = ctx->opt.sift_side_mask != 0;
     if (keep_free && ctx->num_cus > 1) {
       std::vector<uint32_t> mask((size_t)(ctx->num_cus + 31) / 32, 0u);
       for (int i = 0; i < ctx->num_cus - 1; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
@@ -1805,7 +1803,7 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
     if (split) {   // the side stream holds the top layers (lsplit) and waits for the rest
       // (when the last big octave split, the side stream already waits for every layer the
       // image's stream blurs: no second event right before the small-octave chain)
-      if (!(lsplit && o_small - 1 < nsplit) || std::getenv("SOD_SIFT_FORK2")) {
+      if (!(lsplit && o_small - 1 < nsplit) || ctx->opt.sift_fork2) {
         SOD_HIP(ctx, hipEventRecord(S.fork, st));
         SOD_HIP(ctx, hipStreamWaitEvent(S.side, S.fork, 0));
       }
@@ -1827,30 +1825,27 @@ int slot_enqueue(sod_ctx* ctx, const SiftWork& W, SiftSlot& S, int w, int h, boo
                      S.cnt.p + 3, cap, S.kps.p, S.cnt.p + 1, cap, W.lane_order);
   // lone image: descriptors of the raw list on the side stream, beside the keypoint sort
   // (a descriptor depends on its keypoint only; the few duplicates the sort drops cost their
-  // work-groups); SOD_SIFT_EARLY_DESC=0: after the sort, of the final list
-  S.early_desc = split;
-  if (const char* e = std::getenv("SOD_SIFT_EARLY_DESC")) S.early_desc = split && std::atoi(e) != 0;
+  // work-groups); option sift_early_desc 0: after the sort, of the final list
+  S.early_desc = split && ctx->opt.sift_early_desc != 0;
   if (S.early_desc) {
     SOD_TRY(sod_reserve(ctx, S.rdesc, (size_t)cap * 128));
     SOD_TRY(sod_reserve(ctx, S.src, (size_t)cap));
     int rmax = kDescSide;
-    if (const char* e = std::getenv("SOD_SIFT_DESC_RANGE_MAX"))
-      rmax = std::max(0, std::min(kDescSide, std::atoi(e)));
+    if (ctx->opt.sift_desc_range_max >= 0) rmax = std::min(kDescSide, ctx->opt.sift_desc_range_max);
     SOD_HIP(ctx, hipEventRecord(S.fork, st));
     SOD_HIP(ctx, hipStreamWaitEvent(S.side, S.fork, 0));
     hipLaunchKernelGGL(descriptor_kernel, dim3(kDescGrid), dim3(kDT), 0, S.side, S.gauss.p, P, S.kps.p,
                        S.cnt.p + 1, S.rdesc.p, W.lane_order, rmax, cap);
     SOD_HIP(ctx, hipEventRecord(S.join, S.side));
   }
-  const int smax = sort_max();
+  const int smax = sort_max(ctx);
   hipLaunchKernelGGL(sort_dedup_kernel, dim3(1), dim3(1024), 0, st, S.kps.p, S.cnt.p + 1, cap,
                      S.final_kp(), S.cnt.p + 2, smax, S.early_desc ? S.src.p : nullptr);
   // lists longer than smax take the rank path; an image small enough that its list most
   // likely fits leaves those launches (two memsets, three kernels that would exit at once:
   // ~25 us of a ~660 us image) to a second enqueue after the host sees the count
   S.rank_deferred = (int64_t)w * h <= kEagerRankPixels;
-  if (const char* e = std::getenv("SOD_SIFT_EAGER_RANK"))   // A/B and tests: 1 = always eager
-    S.rank_deferred = S.rank_deferred && std::atoi(e) == 0;
+  S.rank_deferred = S.rank_deferred && ctx->opt.sift_eager_rank == 0;   // option: 1 = always eager
   if (!S.rank_deferred) SOD_TRY(enqueue_rank(ctx, S, smax));
   if (S.early_desc) SOD_HIP(ctx, hipStreamWaitEvent(st, S.join, 0));
   return enqueue_describe(ctx, S, W.lane_order);
@@ -1920,8 +1915,8 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
   W.off.assign(1, 0);
   W.shapes.clear();
   const int K = std::min(n, kSlots);
-  bool direct = true;   // SOD_SIFT_DIRECT=0 (A/B): a lone image's results copied after the sync too
-  if (const char* e = std::getenv("SOD_SIFT_DIRECT")) direct = std::atoi(e) != 0;
+  // option sift_direct 0 (A/B): a lone image's results copied after the sync too
+  const bool direct = ctx->opt.sift_direct != 0;
   for (int i0 = 0; i0 < n; i0 += K) {
     const int m = std::min(K, n - i0);
     // a lone image (a round of one) on its own CU-masked slot, batches on the unmasked ones
@@ -1947,8 +1942,8 @@ int run_batch(sod_ctx* ctx, int n, const uint8_t* const* imgs, const int32_t* ws
         SOD_TRY(set_direct(ctx, W, *S, S->out_kp != nullptr));   // room for the grown list
         SOD_TRY(slot_enqueue(ctx, W, *S, ws[i], hs[i], false, m == 1));
       }
-      if (S->rank_deferred && (int64_t)S->hcnt[1] > sort_max()) {   // the list did not fit one work-group
-        SOD_TRY(enqueue_rank(ctx, *S, sort_max()));
+      if (S->rank_deferred && (int64_t)S->hcnt[1] > sort_max(ctx)) {   // the list did not fit one work-group
+        SOD_TRY(enqueue_rank(ctx, *S, sort_max(ctx)));
         SOD_TRY(enqueue_describe(ctx, *S, W.lane_order));
         SOD_HIP(ctx, sod_stream_sync(S->stream));
       }

@@ -38,6 +38,26 @@ struct DevBuf {
 
 struct SiftWork;   // sift.hip: SIFT detect + describe workspace
 
+// Development / test switches of one context (sod_set_option; each also read once from the
+// environment variable SOD_<NAME> at sod_create).  The defaults are the measured best; the
+// tests flip them to cover both sides of a choice.
+struct sod_opts {
+  int match_qt = 0;            // int8 ring kernel query tiles per wave: 0 by query count; 2, 4, 8
+  int match_pf = 0;            // its LDS prefetch distance: 0 default (1); 1, 2
+  int hough_fused = 1;         // 0: never the one-work-group Hough kernel (parity tests)
+  int select_multi = 0;        // 1: small windows take the multi-kernel selection too
+  int sift_stream_mask = -1;   // -1: only the lone image's slot CU-masked; 0 none; 2 all
+  int sift_sort_max = -2;      // -2: kSortMax; lower: the rank path for shorter lists (tests)
+  int sift_desc_range_max = -1;   // -1: kDescSide; lower limits the ranged enumeration (tests)
+  int sift_layer_split = -1;   // -1: every big octave splits its top layers onto the side stream
+  int sift_side_mask = 1;      // 0: the side stream on all CUs
+  int sift_fork2 = 0;          // 1: the second fork event before the small-octave chain
+  int sift_early_desc = 1;     // 0: descriptors after the sort, of the final list
+  int sift_direct = 1;         // 0: a lone image's results copied after the sync
+  int sift_eager_rank = 0;     // 1: the rank-path launches always enqueued with the sort
+  int debug_sync = 0;          // 1: stderr trace of long stream waits and stream re-creation
+};
+
 struct sod_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -49,6 +69,7 @@ struct sod_ctx {
   int match_cus() const { return num_cus - reserved_cus; }
   int tail_cus() const { return reserved_cus ? reserved_cus : num_cus; }
   int impl = 1;                 // matcher: 1 = int8 MFMA 16x16x64 (default), 2 = int8 32x32x32 (match_i8.hip), 0 = bf16 (match.hip)
+  sod_opts opt;                 // sod_set_option
   int mkernel = 0;              // impl 1's kernel shape (sod_match_set_kernel): 0 = by query count,
                                 // 1 = LDS ring (match_i8.hip), 2 = register-streamed (match_s.hip)
 
@@ -269,6 +290,7 @@ struct sod_ctx {
 // polling returns within a query's cost of the end.  Longer waits (C3's 3.7 ms matcher)
 // fall back to the blocking call after the spin.
 constexpr int kSpinUs = 400;
+inline int sod_debug_sync = 0;   // any context's "debug_sync" option (diagnostics only)
 inline hipError_t sod_stream_sync(hipStream_t s) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
@@ -278,7 +300,7 @@ inline hipError_t sod_stream_sync(hipStream_t s) {
     (void)hipGetLastError();   // hipErrorNotReady is an answer, not an error
     if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) break;
   }
-  if (std::getenv("SOD_DEBUG_SYNC")) {   // diagnostics: say which stream a long wait is on
+  if (sod_debug_sync) {   // diagnostics (sod_set_option "debug_sync"): which stream a long wait is on
     for (int k = 0; k < 50000; ++k) {
       const hipError_t q = hipStreamQuery(s);
       if (q == hipSuccess) return hipSuccess;

@@ -688,9 +688,9 @@ def test_pipeline_empty_and_ragged(ctx, case):
 
 
 @pytest.mark.parametrize("bins", [15, (32, 32, 8, 12)])
-def test_select_one_workgroup_equals_multi_kernel(bins, monkeypatch):
+def test_select_one_workgroup_equals_multi_kernel(bins):
     """Windows of <= 2048 queries take select + member lists in one work-group
-    (select_small_kernel); SOD_SELECT_MULTI=1 forces the multi-kernel path.  Both equal the
+    (select_small_kernel); option select_multi 1 forces the multi-kernel path.  Both equal the
     oracle and each other bit for bit (valid bins, votes, offsets, members, means, affine),
     for a plain query window and for a fused batch of two images (image-major bin keys)."""
     db = synthetic.make_database(12, 500, seed=91)
@@ -705,7 +705,7 @@ def test_select_one_workgroup_equals_multi_kernel(bins, monkeypatch):
         c.set_keypoints(db.kp, db.img, db.centroid, db.size)
         c.upload_db(db.des)
         for multi in ("0", "1"):
-            monkeypatch.setenv("SOD_SELECT_MULTI", multi)
+            c.set_option("select_multi", int(multi))
             des, kp_, shape = imgs[0]
             c.upload_queries(des, kp_)
             c.pipeline(shape, bins)

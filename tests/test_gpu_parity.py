@@ -74,13 +74,13 @@ def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
 
 
 @pytest.mark.parametrize("qt", ["2", "4", "8"])
-def test_matcher_query_tiles_shared_thresholds(ctx, monkeypatch, qt):
-    """int8 matcher with each query-tile count per wave (SOD_MATCH_QT) over a DB split into
+def test_matcher_query_tiles_shared_thresholds(ctx, qt):
+    """int8 matcher with each query-tile count per wave (option match_qt) over a DB split into
     many chunks, so the chunks exchange prefilter thresholds mid-run: DB rows duplicated far
     apart (other chunks) make exact distance ties ACROSS chunks -- a shared threshold must
     keep them (lowest trainIdx wins), and queries equal to a DB row (d1 = 0) or near one,
     including runs of equal rows inside a chunk's seed stage."""
-    monkeypatch.setenv("SOD_MATCH_QT", qt)
+    ctx.set_option("match_qt", int(qt))
     rng = np.random.default_rng(31)
     ndb, nq = 150000, 2000
     db = synthetic.sift_like_descriptors(rng, ndb)
@@ -414,8 +414,8 @@ def test_member_order_at_scale(ctx, nq):
     ctx.set_impl("bf16")
 
 
-def _hough_state(c, shape, bins, thr, fused, monkeypatch, affine=True):
-    monkeypatch.setenv("SOD_HOUGH_FUSED", "1" if fused else "0")
+def _hough_state(c, shape, bins, thr, fused, affine=True):
+    c.set_option("hough_fused", int(fused))
     c.hough_select(shape, bins, thr)
     if affine:
         c.affine((shape[1], shape[0]), 128.0, 128.0, 4)
@@ -442,7 +442,7 @@ def _same_hough(a, b):
 
 @pytest.mark.parametrize("name,ngroups", [("near_edge_b15", 78), ("near_edge_b32", 78),
                                           ("edge_b15", 0), ("edge_b6", 0)])
-def test_fused_hough_select_equals_dense(ctx, monkeypatch, name, ngroups):
+def test_fused_hough_select_equals_dense(ctx, name, ngroups):
     """The fused one-image launch (hough_small_kernel: pose, votes from a base-key hash, valid
     bins, members, affine inputs) equals the dense path (pose_kernel + hist_kernel +
     select_small_kernel + affine_gather_kernel) bit for bit -- bin table, valid bins, members,
@@ -465,7 +465,7 @@ def test_fused_hough_select_equals_dense(ctx, monkeypatch, name, ngroups):
         good = np.zeros(nq, bool)
         good[q] = True
         ctx.set_matches(idx1, good)
-        outs.append(_hough_state(ctx, shape, int(g["bins"]), 5, fused, monkeypatch))
+        outs.append(_hough_state(ctx, shape, int(g["bins"]), 5, fused))
     _same_hough(*outs)
     if name.startswith("near_edge"):
         assert outs[0]["guard"][0] == (0 if ctx.trig_exact() else len(q))
@@ -474,7 +474,7 @@ def test_fused_hough_select_equals_dense(ctx, monkeypatch, name, ngroups):
 @pytest.mark.parametrize("nq,thr,n_objects,decoy", [(500, 5, 4, 0.05), (1024, 5, 2, 0.05),
                                                     (1024, 1, 4, 0.6), (700, 2, 0, 0.05),
                                                     (1, 1, 1, 0.0)])
-def test_fused_pipeline_equals_dense(ctx, monkeypatch, nq, thr, n_objects, decoy):
+def test_fused_pipeline_equals_dense(ctx, nq, thr, n_objects, decoy):
     """One query image through the whole pipeline, fused vs dense Hough / select, against
     the 1M-row-shaped DB of 200 images: identical bins, members, means, affine results and
     a second threshold.  thr 1 with many decoys (good matches at random poses) makes
@@ -489,7 +489,7 @@ def test_fused_pipeline_equals_dense(ctx, monkeypatch, nq, thr, n_objects, decoy
     ctx.upload_db(db.des)
     outs = []
     for fused in (True, False):
-        monkeypatch.setenv("SOD_HOUGH_FUSED", "1" if fused else "0")
+        ctx.set_option("hough_fused", int(fused))
         ctx.upload_queries(qs.des, qs.kp)
         ctx.pipeline(qs.shape, (32, 32, 8, 12), ratio=0.75, vote_threshold=thr, affine_threshold=4)
         o = {"valid": ctx.valid_result(), "bins": ctx.all_bins(), "guard": ctx.guard_stats()[:2],

@@ -140,22 +140,22 @@ def test_sift_parity_images(ctx):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sort_max", ["0", "64"])
-def test_sift_rank_path(ctx, monkeypatch, sort_max):
-    """Keypoint order + dedup: lists above SOD_SIFT_SORT_MAX (default 3072) take the O(n^2)
+def test_sift_rank_path(ctx, sort_max):
+    """Keypoint order + dedup: lists above option sift_sort_max (default 3072) take the O(n^2)
     rank passes instead of the one-work-group sort; forcing that path (and a mixed limit)
     gives the same bit-exact results against the C oracle."""
-    monkeypatch.setenv("SOD_SIFT_SORT_MAX", sort_max)
+    ctx.set_option("sift_sort_max", int(sort_max))
     for name, img in _images().items():
         _assert_same(ctx.sift_detect(img), osift.detect_and_compute(img), name + "/rank" + sort_max)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("range_max", ["0", "41"])
-def test_sift_descriptor_full_window_path(ctx, monkeypatch, range_max):
-    """Descriptor windows above SOD_SIFT_DESC_RANGE_MAX rows (default 256) enumerate every
+def test_sift_descriptor_full_window_path(ctx, range_max):
+    """Descriptor windows above option sift_desc_range_max rows (default 256) enumerate every
     window position instead of the per-row j ranges; forcing that path (and a limit that
     splits the keypoints between the two) gives the same bit-exact results."""
-    monkeypatch.setenv("SOD_SIFT_DESC_RANGE_MAX", range_max)
+    ctx.set_option("sift_desc_range_max", int(range_max))
     for name, img in _images().items():
         _assert_same(ctx.sift_detect(img), osift.detect_and_compute(img), name + "/range" + range_max)
 
