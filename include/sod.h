@@ -52,7 +52,7 @@ void sod_destroy(sod_ctx* ctx);
 const char* sod_last_error(const sod_ctx* ctx);
 int sod_synchronize(sod_ctx* ctx);
 /* Kernel timing of the last enqueued matcher launch (ms), measured with HIP events on
- * the ctx stream; and the launch geometry used. */
+ * the ctx stream; SOD_ESTATE when that launch was not timed (sod_set_match_timing). */
 int sod_last_match_ms(sod_ctx* ctx, float* ms);
 /* Kernel times (ms) of the last n matcher launches, oldest first (n <= 64 and <= launches
  * so far), from begin/end HIP events recorded on the matcher's stream around each launch:
@@ -63,7 +63,8 @@ int sod_match_times(sod_ctx* ctx, int n, float* ms);
  * launches -- host work and waits between two calls (a host-staged exchange, other ranks)
  * are not counted: [0 matcher kernel, 1 merge + ratio kernels, 2 Hough pose + vote,
  * 3 select + members (+ PoseBin means fork), 4 affine, 5 all-reduce of the bin counts (or
- * the host exchange's upload), 6 all-gather of the candidates (or its upload)]. */
+ * the host exchange's upload), 6 all-gather of the candidates (or its upload)].  The matcher
+ * entry is 0 when the step's launch was not timed (sod_set_match_timing stride > 1). */
 int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n);
 /* Stage events (the bounds sod_last_stage_ms reads) on (1, the default) or off (0): each is
  * a marker packet on the tail's critical path, so a timed loop turns them off.  With them
@@ -226,7 +227,7 @@ int sod_hough_allreduce_enqueue(sod_ctx* ctx);
  * (centroid x,y, angle, scale, img_size w,h) in vote order. */
 int sod_select_enqueue(sod_ctx* ctx, int32_t vote_threshold);
 /* main.py:89-132 as one call: sod_hough_enqueue over this rank's shard (all rows on one
- * rank), the all-reduce, sod_select_enqueue.  One image of <= 2048 queries on one rank runs
+ * rank), the all-reduce, sod_select_enqueue.  One image of <= 1024 queries (kFusedQ) on one rank runs
  * as ONE kernel (pose, votes, valid bins, members, the affine inputs) without the dense bin
  * histogram, which readers that need it (sod_bins_*, another threshold, the host exchange)
  * build on demand; results identical either way.  sod_pipeline_enqueue uses it. */
@@ -299,6 +300,54 @@ typedef struct sod_pipeline_args {
   int32_t run_affine;
 } sod_pipeline_args;
 int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* args);
+
+/* Results of the enqueued pipeline in ONE device -> host transfer (main.py's per-image
+ * reads, main.py:182-186, without a copy and a wait per array): one kernel writes the
+ * requested parts -- SOD_RES_MATCH the match arrays, SOD_RES_VALID the valid bins (keys
+ * decoded on the host, votes, offsets, members, PoseBin means), SOD_RES_AFFINE the affine
+ * results, SOD_RES_POST (implies VALID) the survivors' post-processing relations -- into
+ * page-locked host memory the context owns; one wait; the post-processing walk
+ * (sod_postprocess's outputs) then runs on the host.  Pointers stay valid until the next
+ * sod_results_fetch or sod_destroy.  Needs sod_ratio_enqueue (+ select for the bins, + affine
+ * for its arrays); parts not requested or not enqueued come back with count 0 / NULL.  The
+ * same values as sod_match_get, sod_valid_get, sod_affine_get and sod_postprocess, bit for
+ * bit. */
+#define SOD_RES_MATCH 1
+#define SOD_RES_VALID 2
+#define SOD_RES_AFFINE 4
+#define SOD_RES_POST 8
+#define SOD_RES_ALL 15
+typedef struct sod_results {
+  int64_t nq;                       /* queries (0 without SOD_RES_MATCH) */
+  const int32_t* idx1;              /* [nq] */
+  const float* d1;                  /* [nq] */
+  const float* d2;                  /* [nq] */
+  const uint8_t* good;              /* [nq] */
+  int32_t selected;                 /* 1: the valid-bin arrays below are set */
+  int64_t n_valid, n_members;
+  const int32_t* keys;              /* [n_valid*4] */
+  const int32_t* votes;             /* [n_valid] */
+  const int64_t* offsets;           /* [n_valid+1] */
+  const int32_t* members;           /* [n_members] */
+  const double* means;              /* [n_valid*6] */
+  int32_t affined;                  /* 1: the affine arrays below are set */
+  const uint8_t* survived;          /* [n_valid] */
+  const int32_t* affine_votes;      /* [n_valid] */
+  const double* params;             /* [n_valid*6] */
+  const uint8_t* alive;             /* [n_members] */
+  int32_t post;                     /* 1: the post-processing outputs below are set */
+  int32_t n_bins;                   /* post-processed bins (survivors, or valid bins) */
+  const int32_t* bin_index;         /* [n_bins] valid-bin index of each */
+  int32_t n_pos, n_ori;
+  const int32_t* pos_off;           /* [n_pos+1] */
+  const int32_t* pos_members;       /* [n_bins] */
+  const int32_t* ori_pos_off;       /* [n_pos+1] */
+  const int32_t* ori_off;           /* [n_ori+1] */
+  const int32_t* ori_members;       /* [n_bins] */
+  const double* final_orientation;  /* [n_pos] */
+  const double* final_pose;         /* [n_pos*6] */
+} sod_results;
+int sod_results_fetch(sod_ctx* ctx, int parts, sod_results* out);
 
 /* ---- stateless batch forms of the per-item reference functions -------------------- */
 /* estimate_object_pose + calculate_bin_index for n (model kp, query kp, centroid)

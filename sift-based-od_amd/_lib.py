@@ -38,6 +38,51 @@ class PipelineArgs(C.Structure):
                 ("y_factor", C.c_double), ("run_affine", C.c_int32)]
 
 
+class Results(C.Structure):
+    """sod_results (sod.h): pointers into the context's page-locked staging buffer."""
+    _fields_ = [("nq", C.c_int64), ("idx1", C.POINTER(C.c_int32)), ("d1", C.POINTER(C.c_float)),
+                ("d2", C.POINTER(C.c_float)), ("good", C.POINTER(C.c_uint8)),
+                ("selected", C.c_int32), ("n_valid", C.c_int64), ("n_members", C.c_int64),
+                ("keys", C.POINTER(C.c_int32)), ("votes", C.POINTER(C.c_int32)),
+                ("offsets", C.POINTER(C.c_int64)), ("members", C.POINTER(C.c_int32)),
+                ("means", C.POINTER(C.c_double)), ("affined", C.c_int32),
+                ("survived", C.POINTER(C.c_uint8)), ("affine_votes", C.POINTER(C.c_int32)),
+                ("params", C.POINTER(C.c_double)), ("alive", C.POINTER(C.c_uint8)),
+                ("post", C.c_int32), ("n_bins", C.c_int32),
+                ("bin_index", C.POINTER(C.c_int32)), ("n_pos", C.c_int32), ("n_ori", C.c_int32),
+                ("pos_off", C.POINTER(C.c_int32)), ("pos_members", C.POINTER(C.c_int32)),
+                ("ori_pos_off", C.POINTER(C.c_int32)), ("ori_off", C.POINTER(C.c_int32)),
+                ("ori_members", C.POINTER(C.c_int32)),
+                ("final_orientation", C.POINTER(C.c_double)),
+                ("final_pose", C.POINTER(C.c_double))]
+
+
+class _Mem:
+    """An __array_interface__ over host memory at an address (np.array(...) copies it)."""
+    __slots__ = ("__array_interface__",)
+
+    def __init__(self, addr, shape, typestr):
+        self.__array_interface__ = {"data": (addr, True), "shape": shape, "typestr": typestr,
+                                    "version": 3}
+
+
+def _arr(addr, n, typestr, width=0):
+    """A numpy copy of n elements (rows of `width`) at a host address (staging memory is
+    reused by the next fetch)."""
+    shape = (n, width) if width else (n,)
+    if n <= 0 or not addr:
+        return np.zeros(shape, np.dtype(typestr))
+    return np.array(_Mem(addr, shape, typestr))
+
+
+# sod_results read in one go: every field as a plain number (pointers as addresses)
+_RES_DTYPE = np.dtype({"names": [f for f, _ in Results._fields_],
+                       "formats": ["<u8" if issubclass(t, C._Pointer) else
+                                   ("<i8" if t is C.c_int64 else "<i4") for _, t in Results._fields_],
+                       "offsets": [getattr(Results, f).offset for f, _ in Results._fields_],
+                       "itemsize": C.sizeof(Results)})
+
+
 # name -> (restype, argtypes); must mirror include/sod.h exactly (tests check the symbols)
 SIGNATURES = {
     "sod_abi_version": (C.c_int, []),
@@ -71,6 +116,7 @@ SIGNATURES = {
     "sod_match_set_kernel": (C.c_int, [c_ctx, C.c_int]),
     "sod_trig_exact": (C.c_int, [c_ctx]),
     "sod_glibc_sincos": (C.c_int, [c_ctx, C.c_int64, c_vp, c_vp, c_vp]),
+    "sod_results_fetch": (C.c_int, [c_ctx, C.c_int, C.POINTER(Results)]),
     "sod_set_option": (C.c_int, [c_ctx, C.c_char_p, C.c_int64]),
     "sod_get_option": (C.c_int, [c_ctx, C.c_char_p, C.POINTER(C.c_int64)]),
     "sod_match_set_overlap": (C.c_int, [c_ctx, C.c_int]),
@@ -185,6 +231,7 @@ class Context:
         self.nq = 0
         self.n_total = 0
         self.bins = None
+        self.db_gen = 0      # counts DB uploads / shares / impl switches (residency checks)
 
     # -- plumbing --
     def _chk(self, rc):
@@ -237,6 +284,7 @@ class Context:
         d, dt = self._des(des)
         self._chk(self._L.sod_db_upload_descriptors(self._h, d.ctypes.data_as(c_vp), dt,
                                                      d.shape[0], int(row_offset)))
+        self.db_gen += 1
         self.n_shard = d.shape[0]
         self.row_offset = int(row_offset)
 
@@ -272,6 +320,7 @@ class Context:
         32x32x32); call before uploads."""
         self._chk(self._L.sod_match_set_impl(self._h, self.IMPLS[impl] if isinstance(impl, str)
                                              else int(impl)))
+        self.db_gen += 1
 
     def trig_exact(self):
         """True when the device's cos / sin are this host's libm bit for bit (then poses,
@@ -375,7 +424,7 @@ class Context:
 
     def hough_select(self, query_shape, bins, vote_threshold=5):
         """Hough + select in one call (sod_hough_select_enqueue): one fused launch for one image
-        of <= 2048 queries on one rank, else hough() + select()."""
+        of <= 1024 queries (kFusedQ) on one rank, else hough() + select()."""
         b = np.ascontiguousarray(bins4(bins), np.int32)
         self._chk(self._L.sod_hough_select_enqueue(self._h, int(query_shape[0]),
                                                    int(query_shape[1]), ptr(b, C.c_int32),
@@ -428,6 +477,51 @@ class Context:
                                          ptr(params, C.c_double), ptr(alive, C.c_uint8)))
         return {"survived": surv.astype(bool), "votes": votes, "params": params,
                 "alive": alive.astype(bool)}
+
+    RES = {"match": 1, "valid": 2, "affine": 4, "post": 8}
+
+    def results(self, post=True, parts=None):
+        """Results of the last pipeline in one device -> host transfer (sod_results_fetch):
+        {"match": (idx1, d1, d2, good), "valid": valid_result()'s dict, "affine":
+        affine_result()'s dict, "post": postprocess()'s dict} -- of ``parts`` (names; default
+        all, without "post" when post is False) that were enqueued; the same values as those
+        getters."""
+        if parts is None:
+            parts = ("match", "valid", "affine") + (("post",) if post else ())
+        mask = 0
+        for p in parts:
+            mask |= self.RES[p]
+        rs = Results()
+        self._chk(self._L.sod_results_fetch(self._h, mask, C.byref(rs)))
+        r = np.frombuffer(rs, _RES_DTYPE)[0].tolist()   # (values in field order)
+        r = dict(zip(_RES_DTYPE.names, r))
+        out = {}
+        if mask & 1:
+            n = r["nq"]
+            out["match"] = (_arr(r["idx1"], n, "<i4"), _arr(r["d1"], n, "<f4"),
+                            _arr(r["d2"], n, "<f4"), _arr(r["good"], n, "|b1"))
+        V, M = r["n_valid"], r["n_members"]
+        if r["selected"]:
+            out["valid"] = {"keys": _arr(r["keys"], V, "<i4", 4), "votes": _arr(r["votes"], V, "<i4"),
+                            "offsets": _arr(r["offsets"], V + 1, "<i8"),
+                            "members": _arr(r["members"], M, "<i4"),
+                            "means": _arr(r["means"], V, "<f8", 6)}
+        if r["affined"]:
+            out["affine"] = {"survived": _arr(r["survived"], V, "|b1"),
+                             "votes": _arr(r["affine_votes"], V, "<i4"),
+                             "params": _arr(r["params"], V, "<f8", 6),
+                             "alive": _arr(r["alive"], M, "|b1")}
+        if r["post"]:
+            nb, npos, nori = r["n_bins"], r["n_pos"], r["n_ori"]
+            out["post"] = {"bin_index": _arr(r["bin_index"], nb, "<i4"),
+                           "pos_off": _arr(r["pos_off"], npos + 1, "<i4"),
+                           "pos_members": _arr(r["pos_members"], nb, "<i4"),
+                           "ori_pos_off": _arr(r["ori_pos_off"], npos + 1, "<i4"),
+                           "ori_off": _arr(r["ori_off"], nori + 1, "<i4"),
+                           "ori_members": _arr(r["ori_members"], nb, "<i4"),
+                           "final_orientation": _arr(r["final_orientation"], npos, "<f8"),
+                           "final_pose": _arr(r["final_pose"], npos, "<f8", 6)}
+        return out
 
     def pipeline(self, query_shape, bins=15, ratio=0.75, vote_threshold=5, affine_threshold=4,
                  x_factor=128.0, y_factor=128.0, run_affine=True):
@@ -704,6 +798,7 @@ class Context:
     def share_db(self, src):
         """Use ``src``'s resident database (no copy); ``src`` must outlive this context."""
         self._chk(self._L.sod_db_share(self._h, src._h))
+        self.db_gen += 1
         self.n_total = src.n_total
         self._db_src = src
 

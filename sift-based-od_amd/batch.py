@@ -89,11 +89,11 @@ def _fused_sizes(ctx, sizes, shapes, bins, vote_threshold, affine_threshold, pos
     ctx.affine((1, 1), POS_FACTOR * 4.0, POS_FACTOR * 4.0, affine_threshold)
     out = []
     if results:
-        v = ctx.valid_result()
-        a = ctx.affine_result()
+        res = ctx.results(post=post_process)   # one transfer, one wait (sod_results_fetch)
+        v, a = res["valid"], res["affine"]
         img = ctx.valid_images()
-        post = ctx.postprocess() if post_process else None
-        idx1, d1, d2, good = ctx.match_result()
+        post = res.get("post")
+        idx1, d1, d2, good = res["match"]
         for b in range(len(sizes)):
             lo, hi = int(off[b]), int(off[b + 1])
             sel = np.nonzero(img == b)[0]

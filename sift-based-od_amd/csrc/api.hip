@@ -146,7 +146,10 @@ int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end) {
   hipEvent_t& e = ctx->mev[ctx->nmatch % sod_ctx::kMatchRing][end];
   if (!e) SOD_HIP(ctx, hipEventCreate(&e));
   SOD_HIP(ctx, hipEventRecord(e, ks));
-  if (end) ++ctx->nmatch;
+  if (end) {
+    ++ctx->nmatch;
+    ctx->last_timed = true;
+  }
   return SOD_OK;
 }
 // begin / end events of the next matcher launch, recorded by the launch itself
@@ -154,6 +157,7 @@ int sod_match_mark(sod_ctx* ctx, hipStream_t ks, int end) {
 int sod_match_events(sod_ctx* ctx, hipEvent_t* begin, hipEvent_t* end) {
   const bool timed = ctx->match_stride > 0 && ctx->mlaunch % ctx->match_stride == 0;
   ++ctx->mlaunch;
+  ctx->last_timed = timed;
   if (!timed) {
     // untimed launch: no begin event (a dispatch that records one delays the next kernel of
     // its stream); a matcher-stream launch still records its completion, which the context
@@ -439,6 +443,8 @@ void sod_destroy(sod_ctx* ctx) {
   sod_release(ctx->xr_idx); sod_release(ctx->xr_rec);
   if (ctx->xr_host) (void)hipHostFree(ctx->xr_host);
   ctx->xr_host = nullptr;
+  if (ctx->hres) (void)hipHostFree(ctx->hres);
+  ctx->hres = nullptr;
   sod_release(ctx->rtab); sod_release(ctx->msize);
   sod_release(ctx->pose_b); sod_release(ctx->msize_b); sod_release(ctx->scal_b);
   sod_release(ctx->voff_b); sod_release(ctx->members_b); sod_release(ctx->means_b);
@@ -490,6 +496,8 @@ int sod_last_match_ms(sod_ctx* ctx, float* ms) {
   SOD_TRY(set_dev(ctx));
   if (!ms) return sod_fail(ctx, SOD_EINVAL, "null output");
   if (!ctx->matched) return sod_fail(ctx, SOD_ESTATE, "no matcher launch yet");
+  if (!ctx->last_timed)
+    return sod_fail(ctx, SOD_ESTATE, "the last matcher launch was not timed (sod_set_match_timing)");
   return sod_match_times(ctx, 1, ms);
 }
 
@@ -522,7 +530,8 @@ int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n) {
   if (!ms_out || n < 0) return sod_fail(ctx, SOD_EINVAL, "null output");
   SOD_HIP(ctx, sod_stream_sync(ctx->stream));
   float acc[kStages] = {};
-  if (ctx->matched && ctx->nmatch > 0) {   // the last matcher launch's own begin / end events
+  // the last matcher launch's own begin / end events (0 when that launch was not timed)
+  if (ctx->matched && ctx->nmatch > 0 && ctx->last_timed) {
     hipEvent_t* m = ctx->mev[(ctx->nmatch - 1) % sod_ctx::kMatchRing];
     if (hipEventElapsedTime(&acc[kStageMatch], m[0], m[1]) != hipSuccess) {
       acc[kStageMatch] = 0.f;
@@ -1434,6 +1443,113 @@ int sod_affine_get(sod_ctx* ctx, uint8_t* survived, int32_t* votes, double* para
   SOD_TRY(download(ctx, params, ctx->params.p, (size_t)V * 6));
   SOD_TRY(download(ctx, member_alive, ctx->alive.p, (size_t)M));
   SOD_HIP(ctx, sod_stream_sync(ctx->stream));
+  return SOD_OK;
+}
+
+// ---- results staging -----------------------------------------------------------------
+int sod_results_fetch(sod_ctx* ctx, int parts, sod_results* out) {
+  SOD_TRY(set_dev(ctx));   // joins the side stream (PoseBin means)
+  if (!out) return sod_fail(ctx, SOD_EINVAL, "null output");
+  if (parts & ~SOD_RES_ALL) return sod_fail(ctx, SOD_EINVAL, "unknown result part");
+  if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "sod_ratio_enqueue first");
+  if (ctx->selected) SOD_TRY(sod_guard_resolve(ctx));   // (patches the device results)
+  const bool do_post = (parts & SOD_RES_POST) && ctx->selected;
+  const bool do_valid = ((parts & SOD_RES_VALID) || do_post) && ctx->selected;
+  const bool do_aff = (parts & SOD_RES_AFFINE) && ctx->selected && ctx->affined;
+  ResLayout L;
+  L.nq = (parts & SOD_RES_MATCH) ? ctx->nq : 0;
+  L.valid = do_valid;
+  L.affine = do_aff;
+  L.vcap = do_valid || do_aff ? ctx->vmax : 0;
+  L.mcap = do_valid || do_aff ? ctx->mmax : 0;
+  L.ncap = do_post ? std::min<int64_t>(L.vcap, 1024) : 0;
+  L.words = (int)((L.ncap + 63) / 64);
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o += (bytes + 15) & ~(size_t)15;
+    return at;
+  };
+  L.hdr = take(64);
+  L.idx1 = take((size_t)L.nq * 4);
+  L.d1 = take((size_t)L.nq * 4);
+  L.d2 = take((size_t)L.nq * 4);
+  L.good = take((size_t)L.nq);
+  L.vbin = take((size_t)L.vcap * 4);
+  L.voff = take(((size_t)L.vcap + 1) * 8);
+  L.members = take((size_t)L.mcap * 4);
+  L.means = take((size_t)L.vcap * 48);
+  L.surv = take((size_t)L.vcap);
+  L.fvotes = take((size_t)L.vcap * 4);
+  L.params = take((size_t)L.vcap * 48);
+  L.alive = take((size_t)L.mcap);
+  L.sidx = take(do_post ? (size_t)L.vcap * 4 : 0);
+  L.smeans = take(do_post ? (size_t)L.vcap * 48 : 0);
+  L.pos = take((size_t)L.ncap * L.words * 8);
+  L.ori = take((size_t)L.ncap * L.words * 8);
+  L.total = o;
+  if (ctx->hres_n < L.total) {   // (nothing writes into the old buffer: every fetch waits)
+    if (ctx->hres) (void)hipHostFree(ctx->hres);
+    ctx->hres = nullptr;
+    ctx->hres_n = 0;
+    SOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->hres), L.total, hipHostMallocDefault));
+    ctx->hres_n = L.total;
+  }
+  reinterpret_cast<int64_t*>(ctx->hres + L.hdr)[2] = 0;
+  SOD_TRY(launch_results_stage(ctx, L, do_post));
+  SOD_HIP(ctx, sod_stream_sync(ctx->stream));
+  const int64_t* hdr = reinterpret_cast<const int64_t*>(ctx->hres + L.hdr);
+  const int64_t V = L.vcap ? hdr[0] : 0, M = L.vcap ? hdr[1] : 0;
+  ResHost& r = ctx->res;
+  const uint8_t* h = ctx->hres;
+  *out = sod_results{};
+  out->nq = L.nq;
+  if (L.nq) {
+    out->idx1 = reinterpret_cast<const int32_t*>(h + L.idx1);
+    out->d1 = reinterpret_cast<const float*>(h + L.d1);
+    out->d2 = reinterpret_cast<const float*>(h + L.d2);
+    out->good = h + L.good;
+  }
+  if (do_valid) {
+    const uint32_t* vb = reinterpret_cast<const uint32_t*>(h + L.vbin);
+    const int64_t* off = reinterpret_cast<const int64_t*>(h + L.voff);
+    r.keys.resize((size_t)std::max<int64_t>(1, V) * 4);
+    decode_keys(ctx, std::vector<uint32_t>(vb, vb + V), r.keys.data());
+    r.votes.resize((size_t)std::max<int64_t>(1, V));
+    for (int64_t i = 0; i < V; ++i) r.votes[(size_t)i] = (int32_t)(off[i + 1] - off[i]);
+    out->selected = 1;
+    out->n_valid = V;
+    out->n_members = M;
+    out->keys = r.keys.data();
+    out->votes = r.votes.data();
+    out->offsets = off;
+    out->members = reinterpret_cast<const int32_t*>(h + L.members);
+    out->means = reinterpret_cast<const double*>(h + L.means);
+  }
+  if (do_aff) {
+    out->n_valid = V;
+    out->n_members = M;
+    out->affined = 1;
+    out->survived = h + L.surv;
+    out->affine_votes = reinterpret_cast<const int32_t*>(h + L.fvotes);
+    out->params = reinterpret_cast<const double*>(h + L.params);
+    out->alive = h + L.alive;
+  }
+  if (do_post) {
+    SOD_TRY(sod_post_staged(ctx, L, r));
+    out->post = 1;
+    out->n_bins = r.n_bins;
+    out->bin_index = r.bin_index.data();
+    out->n_pos = r.n_pos;
+    out->n_ori = r.n_ori;
+    out->pos_off = r.pos_off.data();
+    out->pos_members = r.pos_members.data();
+    out->ori_pos_off = r.ori_pos_off.data();
+    out->ori_off = r.ori_off.data();
+    out->ori_members = r.ori_members.data();
+    out->final_orientation = r.orient.data();
+    out->final_pose = r.pose.data();
+  }
   return SOD_OK;
 }
 

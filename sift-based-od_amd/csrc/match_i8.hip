@@ -1316,14 +1316,14 @@ int launch_match_i8(sod_ctx* ctx) {
   SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
   // shared thresholds, one array per partial-result slot: "nothing known" is bytes 0x80 (below
   // every reachable t2); the merge that releases a slot resets its array for the next launch,
-  // a new query count (slot layout) resets BOTH slots here (stream_begin waited for both
+  // a new slot layout (query count, kernel shape) resets BOTH slots here (stream_begin waited for both
   // merges) -- also the one an overlap-off context never uses, so switching overlap on later
   // (sod_match_set_overlap / sod_set_cu_reserve, which also clear gthr_n) never reads
   // uninitialised thresholds
   int32_t* gthr = nullptr;
   if (!wide) {
     const int64_t gslot = sod_thr_words(ctx) * nq_pad;   // words of one slot
-    if (ctx->gthr.n < (size_t)(2 * gslot) || ctx->gthr_n != nq_pad) {
+    if (ctx->gthr.n < (size_t)(2 * gslot) || ctx->gthr_n != gslot) {
       if (ctx->gthr.n < (size_t)(2 * gslot)) {
         SOD_HIP(ctx, sod_stream_sync(ctx->mstream));
         SOD_HIP(ctx, sod_stream_sync(ctx->mstream2));
@@ -1334,7 +1334,7 @@ int launch_match_i8(sod_ctx* ctx) {
       // stream, must not write bounds of the old layout into it)
       if (ctx->mtwo && !ctx->mk_main) SOD_HIP(ctx, sod_stream_sync(ctx->mstream_of(ctx->pslot ^ 1)));
       SOD_HIP(ctx, hipMemsetAsync(ctx->gthr.p, 0x80, (size_t)(2 * gslot) * 4, ks));
-      ctx->gthr_n = nq_pad;
+      ctx->gthr_n = gslot;
     }
     gthr = ctx->gthr.p + ctx->pslot * gslot;
   }

@@ -23,12 +23,16 @@
 //
 // Thresholds: a wave first runs kSeedW windows with only the running max (no compare): the
 // second largest of a query's four lane-group maxima comes from two distinct rows, so it is
-// a valid threshold from the first exact window on.  The waves of a query group publish
-// their thresholds to a global array (atomic max, h units; layout [group][lane j][tile t]
-// so a lane reads its 32 values with 8 wide loads) and take the max of what the others
-// published -- a chunk holding t2 has two rows with y >= 2 t2, so no row below it is in
-// the query's global top-2 (match_i8.hip, SOD_I8_XCHUNK).  A stale value is still a valid
-// bound: loads are issued one body ahead of their use and nothing waits for them.
+// a valid threshold from the first exact window on.  The work-groups of a query group (one
+// per DB range) share bounds without atomics: each keeps per query the top-2 (row value, id
+// of the work-group whose row reaches it) of distinct ids it knows of -- its own best row and
+// what it read -- and publishes that list to a slot of its own with plain stores; at
+// exchange r it merges the slot of work-group (sp - 2^(r mod log2 n)) mod n into its list
+// (a dissemination pattern: after log2 n rounds every list has seen every work-group).  The
+// second entry is reached by two distinct rows, so no row below it is in the query's global
+// top-2.  A stale slot is still a valid bound: loads are issued one exchange ahead of their
+// use and nothing waits for them.  (Atomic max on one shared word per query -- round 5's
+// first build -- serialised 256 work-groups' publications at the memory side: ~60 us.)
 //
 // Output: per work-group (4 waves = one DB range) the partial top-2 of every query of its
 // group, merged over the waves and lane groups in LDS, into slot sp of pd1 / pidx / pd2 --
@@ -70,27 +74,41 @@ constexpr int kLag = SOD_S_LAG;
 #define SOD_S_XCHG 1              // thresholds shared between the waves of a query group
 #endif
 constexpr bool kXchg = SOD_S_XCHG;
-#ifndef SOD_S_FIRSTX
-#define SOD_S_FIRSTX 1            // first window whose end applies the global words
+#ifndef SOD_S_EARLYB
+#define SOD_S_EARLYB 2            // loop bodies that exchange after every window
 #endif
-constexpr int kFirstX = SOD_S_FIRSTX;
-#ifndef SOD_S_SEEDPUB
-#define SOD_S_SEEDPUB 1           // the seeds' best rows go out at once
-#endif
-constexpr bool kSeedPub = SOD_S_SEEDPUB;
-#ifndef SOD_S_LEADER
-#define SOD_S_LEADER 16           // every kLeader-th work-group publishes its seeds
-#endif
-constexpr int kLeader = SOD_S_LEADER;
+constexpr int kEarlyB = SOD_S_EARLYB;
 constexpr int kSubB = 2048;       // bytes per 16-row subtile
 constexpr int kRsrc3 = 0x00020000;
 // accumulator init of a subtile beyond the wave's range: h < -2^30 <= every threshold, and
 // no wrap (|q'.d'| <= 2^21)
 constexpr int kMaskC = INT_MIN + (1 << 22);
-// threshold words per query group: lane j's 32 words at j * kGStride (a padded row: the
-// 16 lanes' LDS reads of one tile word hit different banks)
+// LDS boards per query group: lane j's 32 words at j * kGStride (a padded row: the 16 lanes'
+// LDS reads of one tile word hit different banks)
 constexpr int kGStride = kSQT + 4;
 constexpr int kGroupWords = 16 * kGStride;
+// a work-group's published top-2 (packed, below) of its query group: query (t, j) at words
+// j * kLStride + 2t, 2t + 1; the same layout in LDS (the work-group's board) and in its
+// global slot
+constexpr int kLStride = 2 * kSQT + 4;
+constexpr int kSlotWords = 16 * kLStride;
+
+// a bound entry: a row value h (>= -2^22: any reachable h of a real row; kMaskC rows are
+// clamped, they never become a bound) and the id of the work-group whose row reaches it --
+// ordered by h, then id.  Two entries of different ids are reached by two distinct rows.
+__device__ __forceinline__ int bpack(int h, int id) { return (max(h, -(1 << 22)) << 8) | id; }
+// top-2 of distinct ids of two top-2 lists (each of distinct ids, a1 >= a2, b1 >= b2): the
+// first is the larger first; the second the largest entry of another id (copies of one
+// id -- a work-group's value seen at two times -- count once)
+__device__ __forceinline__ void bmerge(int& a1, int& a2, int b1, int b2) {
+  const int f = max(a1, b1), fid = f & 255;
+  int s2 = (a1 & 255) != fid ? a1 : INT_MIN;
+  s2 = max(s2, (a2 & 255) != fid ? a2 : INT_MIN);
+  s2 = max(s2, (b1 & 255) != fid ? b1 : INT_MIN);
+  s2 = max(s2, (b2 & 255) != fid ? b2 : INT_MIN);
+  a1 = f;
+  a2 = s2;
+}
 
 __device__ __forceinline__ int imed3(int a, int b, int c) {
   int r;
@@ -141,9 +159,12 @@ __device__ unsigned long long g_scounts[8];
 #ifdef SOD_S_STAMP
 // diagnostic build only: per wave (block * 4 + wave) s_memtime at [0] start, [1] query
 // fragments loaded, seed: [2] scan, [3] pushes, [4] barrier, [5] apply, [6] load issued, [7]
-// pull; body 0: [8 + 2w] window w scanned, [9 + 2w] its exchange done; [14 + b] body b
-// (1 <= b <= 10) starts; [25] end; s_memrealtime at start / end in [26] / [27]
+// pull; body 0: [8 + 3w] window w scanned, [9 + 3w] its slow path done, [10 + 3w] its
+// exchange done (w < 3); [16 + b] body b (1 <= b <= 8) starts; [25] end; s_memrealtime at
+// start / end in [26] / [27]
 __device__ unsigned long long g_sstamps[4096][28];
+// hit tiles per wave and body: [0..7] bodies 0..7, [8] the later bodies together
+__device__ unsigned g_shits[4096][9];
 #define SSTAMP(i)                                                                 \
   do {                                                                            \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();                   \
@@ -161,11 +182,13 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int64_t sub_per_split, int row_offset, float* __restrict__ pd1, int* __restrict__ pidx,
     float* __restrict__ pd2, int nqb, int* __restrict__ gthr) {
+  // gthr: [query group][DB range][kSlotWords] published top-2 lists
   static_assert(QT == 32, "a lane's 32 threshold words are 8 wide loads; 8 tiles per exchanging wave");
   // exact top-2 per (wave, tile, field, lane): 24 KiB per wave
   __shared__ int top2[kSNW * QT * 3 * 64];
   // threshold boards of the work-group (below)
   __shared__ __attribute__((aligned(16))) int t2b[kGroupWords], bb[kGroupWords];
+  __shared__ __attribute__((aligned(16))) int tb[16 * kLStride];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -297,73 +320,63 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
     return any;
   };
 
-  // ---- thresholds shared between waves ----
+  // ---- thresholds shared between waves and work-groups ----
   // LDS boards of the work-group (its 4 waves hold the same queries), layout [lane j]
-  // [kGStride] like the global words: t2b = the best bound known per query, bb = the best row
-  // value (h) the work-group has seen per query.  Global: gb[parity][group][j][kGStride] = max
-  // over the work-groups of one parity class (sp & 1) of their bb, so min(even, odd) -- with
-  // the own class's word raised by the own bb -- is reached by two distinct rows, one in each
-  // class: a bound close to the second best over ALL rows the work-groups have seen
-  // (match_i8.hip's best-row slots).  Wave w exchanges tiles [8w, 8w+8): applies the global
-  // words it loaded one body ago, publishes its work-group's bb where it beats them (atomic
-  // max; a same-address storm is serialised at the memory side, so only improvements go out),
-  // and loads them again (sc1: past this XCD's L2).  Every wave pulls t2b into its t2 once per
-  // body and pushes its own t2 / best after a slow-path update (LDS atomics).
-  const int par = sp & 1;
-  int* const gown = gthr + ((int64_t)par * nqb + qb) * kGroupWords;
-  int* const goth = gthr + ((int64_t)(1 - par) * nqb + qb) * kGroupWords;
-  const __amdgpu_buffer_rsrc_t rso =
-      __builtin_amdgcn_make_buffer_rsrc((void*)gown, (short)0, kGroupWords * 4, kRsrc3);
-  const __amdgpu_buffer_rsrc_t rsx =
-      __builtin_amdgcn_make_buffer_rsrc((void*)goth, (short)0, kGroupWords * 4, kRsrc3);
-  constexpr int kXT = QT / kSNW;   // tiles a wave exchanges
-  const int xt0 = wave * kXT;
-  i32x4 ge[2], go[2];   // loaded own-class / other-class global words of the wave's 8 tiles
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    ge[i] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
-    go[i] = ge[i];
-  }
+  // [kGStride]: t2b = the best bound known per query (h), bb = the best row value (h) the
+  // work-group has seen per query; tb = the work-group's top-2 list (layout [j][kLStride]).
+  // Wave w exchanges tiles [8w, 8w+8), lane (g, j) the tiles 8w + 2g, 8w + 2g + 1 of query
+  // j: one 16-byte word group of the list per lane
+  const int nsplit = (int)(gridDim.x / nqb);
+  const int nbits = nsplit > 1 ? 32 - __builtin_clz((unsigned)(nsplit - 1)) : 0;
+  int* const gslot = gthr + (int64_t)qb * nsplit * kSlotWords;
+  const uint32_t lo_off = (uint32_t)(j16 * kLStride + 2 * (wave * (QT / kSNW) + 2 * g)) * 4u;
+  const __amdgpu_buffer_rsrc_t rsg = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)gslot, (short)0, nsplit * kSlotWords * 4, kRsrc3);
+  const int xt = wave * (QT / kSNW) + 2 * g;   // the lane's first exchanged tile
+  i32x4 pe = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};   // loaded partner entries
+  int xr = 0;                                              // exchange rounds so far
   for (int i = tid; i < kGroupWords; i += kSNW * 64) {
     t2b[i] = INT_MIN >> 1;
     bb[i] = INT_MIN >> 1;
   }
+  for (int i = tid; i < 16 * kLStride; i += kSNW * 64) tb[i] = INT_MIN;
   __syncthreads();
+  // the partner slot of the next round, loaded (sc1: past this XCD's L2) for the round after
   auto exch_load = [&]() {
     if constexpr (kXchg) {
-      const uint32_t vo = (uint32_t)(j16 * kGStride + xt0) * 4u;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        ge[i] = __builtin_amdgcn_raw_buffer_load_b128(rso, vo + 16u * i, 0, 16 /* sc1 */);
-        go[i] = __builtin_amdgcn_raw_buffer_load_b128(rsx, vo + 16u * i, 0, 16 /* sc1 */);
+      if (nbits) {
+        const int p = (sp - (1 << (xr % nbits)) + nsplit) % nsplit;
+        pe = __builtin_amdgcn_raw_buffer_load_b128(rsg, lo_off, (uint32_t)p * kSlotWords * 4u,
+                                                   16 /* sc1 */);
       }
+      ++xr;
     }
   };
+  // merge the own best rows and the loaded partner list into the work-group's list, publish
+  // it (write-through stores: the other XCDs read it from memory) and raise the bounds
   auto exch_apply = [&]() {
     if constexpr (kXchg) {
-      const int* bw = bb + j16 * kGStride + xt0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const i32x4 w4 = *reinterpret_cast<const i32x4*>(bw + 4 * i);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int t = xt0 + 4 * i + k;
-          const int bound = min(max(ge[i][k], w4[k]), go[i][k]);
-          if (lane < 16) {   // (tiles past the group's last: words nobody reads)
-            __hip_atomic_fetch_max(&t2b[j16 * kGStride + t], bound, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (w4[k] > ge[i][k])
-              __hip_atomic_fetch_max(gown + j16 * kGStride + t, w4[k], __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      }
+      i32x4 l = *reinterpret_cast<const i32x4*>(tb + j16 * kLStride + 2 * xt);
+      const int o0 = bb[j16 * kGStride + xt], o1 = bb[j16 * kGStride + xt + 1];
+      int a1 = l[0], a2 = l[1], c1 = l[2], c2 = l[3];
+      bmerge(a1, a2, bpack(o0, sp), INT_MIN);
+      bmerge(c1, c2, bpack(o1, sp), INT_MIN);
+      bmerge(a1, a2, pe[0], pe[1]);
+      bmerge(c1, c2, pe[2], pe[3]);
+      l = i32x4{a1, a2, c1, c2};
+      *reinterpret_cast<i32x4*>(tb + j16 * kLStride + 2 * xt) = l;
+      __builtin_amdgcn_raw_buffer_store_b128(l, rsg, lo_off, (uint32_t)sp * kSlotWords * 4u,
+                                             17 /* sc0 sc1 */);
+      __hip_atomic_fetch_max(&t2b[j16 * kGStride + xt], a2 >> 8, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_max(&t2b[j16 * kGStride + xt + 1], c2 >> 8, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   };
   auto pull = [&]() {
-    const int* tb = t2b + j16 * kGStride;
+    const int* tb2 = t2b + j16 * kGStride;
     sfor<QT / 4>([&](auto I) {
-      const i32x4 v = *reinterpret_cast<const i32x4*>(tb + 4 * I);
+      const i32x4 v = *reinterpret_cast<const i32x4*>(tb2 + 4 * I);
 #pragma unroll
       for (int k = 0; k < 4; ++k) t2[4 * I + k] = max(t2[4 * I + k], v[k]);
     });
@@ -399,13 +412,9 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
         SSTAMP(3);
         __syncthreads();   // every wave's seeds are on the boards
         SSTAMP(4);
-        // the seeds' best rows go out from every kLeader-th work-group only: nothing is
-        // loaded yet, so every publisher would send every query's word -- same-address
-        // atomics the memory side serialises (a storm of 256 x 512 stalled every wave's
-        // memory pipe for ~20 us at one image); the others publish improvements later
-        if ((kSeedPub && sp % kLeader == 0) || W > 0) exch_apply();
+        exch_apply();   // the seeds' best rows go out at once
         SSTAMP(5);
-        if constexpr (W == 0) exch_load();
+        exch_load();
         SSTAMP(6);
         pull();
         SSTAMP(7);
@@ -415,25 +424,28 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
 
   const int rowl = row_offset + (int)(s_lo * kSubRows) + g * 4;
   const int nbody = (nloc + kSD - 1) / kSD;
-  // one loop body = kSW windows; the first body is peeled (Early): it exchanges after every
-  // window from window kFirstX on and only loads before (the leaders' seeds must land first:
-  // a load issued with the seeds in flight reads nothing, and then every work-group would
-  // publish every query's best -- the storm the leaders avoid), so that the steady-state
-  // loop's single exchange reads words loaded a whole body (kSD subtiles of loads) earlier
+  // one loop body = kSW windows; the first kEarlyB bodies (Early) exchange after every
+  // window, while the bounds still move fast, the later ones once per body
   auto body = [&](auto Early, int b) {
     constexpr bool early = Early;
 #ifdef SOD_S_STAMP
-    if (b > 0 && b <= 10) SSTAMP(14 + b);
+    if (b > 0 && b <= 8) SSTAMP(16 + b);
+#endif
+#ifdef SOD_S_STAMP
+    unsigned hcnt = 0;
 #endif
     sfor<kSW>([&](auto W) {
       constexpr int w = W;
       int m[QT];
       const uint64_t any = scan(W, m);
 #ifdef SOD_S_STAMP
-      if (b == 0) SSTAMP(8 + 2 * w);
+      if (b == 0 && w < 3) SSTAMP(8 + 3 * w);
 #endif
 #ifdef SOD_S_COUNT
       if (lane == 0) atomicAdd(&g_scounts[0], 1ull);
+#endif
+#ifdef SOD_S_NOSLOW
+      if (b < 0)
 #endif
       if (__builtin_expect(any != 0, 0)) {
 #ifdef SOD_S_COUNT
@@ -447,6 +459,9 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
           if (__builtin_amdgcn_ballot_w64(m[t] >= tt) == 0) return;
 #ifdef SOD_S_COUNT
           if (lane == 0) atomicAdd(&g_scounts[2], 1ull);
+#endif
+#ifdef SOD_S_STAMP
+          ++hcnt;
 #endif
           int y1 = slot[(t * 3 + 0) * 64], id = slot[(t * 3 + 1) * 64], y2 = slot[(t * 3 + 2) * 64];
 #pragma unroll
@@ -475,25 +490,29 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
           push(t, t2[t], g1 >> 1);
         });
       }
+#ifdef SOD_S_STAMP
+      if (b == 0 && w < 3) SSTAMP(9 + 3 * w);
+#endif
       // the window's slots take the subtiles kSD ahead
 #pragma unroll
       for (int j = 0; j < kSN; ++j) load_sub(ring[w * kSN + j], (b + 1) * kSD + w * kSN + j);
-      // exchange (the words loaded one exchange ago; then the next loads): after every window
-      // of the first kEarlyB bodies, while the bounds still move fast, then once per body
-      if constexpr (early && w < kFirstX) {
-        exch_load();
-      } else if constexpr (early || w == kSW - 1) {
+      // exchange (the list loaded one exchange ago; then the next load)
+      if constexpr (early || w == kSW - 1) {
         exch_apply();
         exch_load();
         pull();
       }
 #ifdef SOD_S_STAMP
-      if (b == 0) SSTAMP(9 + 2 * w);
+      if (b == 0 && w < 3) SSTAMP(10 + 3 * w);
 #endif
     });
+#ifdef SOD_S_STAMP
+    if (lane == 0 && blockIdx.x * 4 + wave < 4096) g_shits[blockIdx.x * 4 + wave][min(b, 8)] += hcnt;
+#endif
   };
-  if (nbody > 0) body(std::true_type{}, 0);
-  for (int b = 1; b < nbody; ++b) body(std::false_type{}, b);
+  int b = 0;
+  for (; b < min(nbody, kEarlyB); ++b) body(std::true_type{}, b);
+  for (; b < nbody; ++b) body(std::false_type{}, b);
   SSTAMP(25);
 #ifdef SOD_S_STAMP
   if (lane == 0 && blockIdx.x * 4 + wave < 4096)
@@ -537,6 +556,16 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
 extern "C" int sod_debug_sstamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sstamps), sizeof(g_sstamps)) == hipSuccess ? 0 : 1;
 }
+// per-wave hit tiles per body, summed over the launches since the last reset
+extern "C" int sod_debug_shits(unsigned* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_shits), sizeof(g_shits)) != hipSuccess) return 1;
+  if (reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_shits)) != hipSuccess) return 1;
+    if (hipMemset(p, 0, sizeof(g_shits)) != hipSuccess) return 1;
+  }
+  return 0;
+}
 #endif
 #ifdef SOD_S_COUNT
 extern "C" int sod_debug_scounts(unsigned long long* out, int reset) {
@@ -558,11 +587,14 @@ bool sod_match_use_s(const sod_ctx* ctx) {
   return kStreamedAuto && ctx->nqt >= 24 && ctx->nqt <= 640;
 }
 
-// words per query of one shared-threshold slot: match_i8's kThrWords, or the streamed
-// kernel's 512 per query group when that is more
+// words per query of one shared-threshold slot: match_i8's kThrWords, or for the streamed
+// kernel its published lists (kSlotWords per query group and DB range)
 int64_t sod_thr_words(const sod_ctx* ctx) {
+  if (!sod_match_use_s(ctx)) return kThrWords;
+  int64_t split, per;
+  sod_match_s_geometry(ctx, &split, &per);
   const int64_t nq_pad = std::max<int64_t>(1, (int64_t)ctx->nqt * kSubRows);
-  const int64_t sw = 2 * (int64_t)((ctx->nqt + kSQT - 1) / kSQT) * kGroupWords;
+  const int64_t sw = (int64_t)((ctx->nqt + kSQT - 1) / kSQT) * split * kSlotWords;
   return std::max<int64_t>(kThrWords, (sw + nq_pad - 1) / nq_pad);
 }
 
@@ -573,6 +605,8 @@ int launch_match_s_kernel(sod_ctx* ctx, hipStream_t ks, hipEvent_t eb, hipEvent_
                           int64_t sub_per_split) {
   const int64_t nq_pad = (int64_t)ctx->nqt * kSubRows;
   const int64_t nqb = (ctx->nqt + kSQT - 1) / kSQT;
+  if (split > 256)   // list entries carry the DB range in 8 bits (bpack)
+    return sod_fail(ctx, SOD_EINVAL, "streamed matcher: more than 256 DB ranges");
   hipExtLaunchKernelGGL((match_s_kernel<kSQT>), dim3((unsigned)(nqb * split)), dim3(kSNW * 64), 0,
                         ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
                         ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p), ctx->nqt,

@@ -17,6 +17,7 @@
 // reference's exact visit order (it fixes every later sum and tie), so the DFS walks the
 // bitmask rows on the host (set bits = ascending neighbours), O(n^2 / 64) word reads.
 // Compiled with -ffp-contract=off: the comparisons are the reference's Python floats.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -88,6 +89,9 @@ struct PostOut {
   std::vector<double> pose;                          // 6 per cluster
 };
 
+int post_walk(int32_t n, int words, const uint64_t* pos, const uint64_t* ori,
+              const double* means_host, PostOut& out);
+
 int run_post(sod_ctx* ctx, int32_t n, const double* means_host, const int32_t* img_host,
              PostOut& out) {
   if (n <= 0) return SOD_OK;
@@ -121,10 +125,16 @@ int run_post(sod_ctx* ctx, int32_t n, const double* means_host, const int32_t* i
     if (e != hipSuccess) rc = sod_fail(ctx, SOD_EHIP, std::string("post-processing: ") + hipGetErrorString(e));
   }
   if (rc != SOD_OK) return rc;
+  return post_walk(n, words, pos.data(), ori.data(), means_host, out);
+}
 
+// the host walk over the two relation bitmasks (rows of `words` words): position clusters,
+// orientation clusters inside each, their dominant orientation and the final pose
+int post_walk(int32_t n, int words, const uint64_t* pos, const uint64_t* ori,
+              const double* means_host, PostOut& out) {
   // position clusters: neighbours of a node = set bits of its row, ascending
   auto pos_next = [&](int node, int from, const std::vector<char>& seen) -> int {
-    const uint64_t* row = pos.data() + (size_t)node * words;
+    const uint64_t* row = pos + (size_t)node * words;
     for (int w = from >> 6; w < words; ++w) {
       uint64_t bits = row[w];
       if (w == (from >> 6)) bits &= ~0ull << (from & 63);
@@ -142,7 +152,7 @@ int run_post(sod_ctx* ctx, int32_t n, const double* means_host, const int32_t* i
     // orientation clusters in the cluster's own indexing (local k -> global cl[k])
     const int nc = (int)cl.size();
     auto ori_next = [&](int k, int from, const std::vector<char>& seen) -> int {
-      const uint64_t* row = ori.data() + (size_t)cl[k] * words;
+      const uint64_t* row = ori + (size_t)cl[k] * words;
       for (int m = from; m < nc; ++m) {
         if (m == k || seen[m]) continue;
         const int g = cl[m];
@@ -219,7 +229,199 @@ int write_post(const PostOut& o, int32_t* n_pos, int32_t* pos_off, int32_t* pos_
   return SOD_OK;
 }
 
+// ---- results staging (sod_results_fetch) ----------------------------------------------
+struct StageArgs {
+  uint8_t* h;   // page-locked host buffer (device-visible)
+  ResLayout L;
+  const int32_t* idx1;
+  const float *d1, *d2;
+  const uint8_t* good;
+  const uint32_t* vbin;
+  const int64_t* voff;
+  const int32_t* members;
+  const double* means;
+  const uint8_t* surv;
+  const int32_t* fvotes;
+  const double* params;
+  const uint8_t* alive;
+  const uint32_t* scal;   // [0] valid bins, [1] members
+  int selected, affined, n_qimg;
+  int64_t nbins1;
+};
+
+template <typename T>
+__device__ __forceinline__ void stage_copy(uint8_t* h, size_t off, const T* src, int64_t n,
+                                           int64_t gt, int64_t gs) {
+  T* dst = reinterpret_cast<T*>(h + off);
+  for (int64_t i = gt; i < n; i += gs) dst[i] = src[i];
+}
+
+// every array of the last pipeline into the host buffer, at the sizes the device holds
+__global__ __launch_bounds__(256) void results_pack_kernel(StageArgs a) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+  const int64_t V = a.L.vcap ? min<int64_t>(a.scal[0], a.L.vcap) : 0;
+  const int64_t M = a.L.vcap ? min<int64_t>(a.scal[1], a.L.mcap) : 0;
+  if (gt == 0) {
+    int64_t* hdr = reinterpret_cast<int64_t*>(a.h + a.L.hdr);
+    hdr[0] = V;
+    hdr[1] = M;
+  }
+  const int64_t nq = a.L.nq;
+  stage_copy(a.h, a.L.idx1, a.idx1, nq, gt, gs);
+  stage_copy(a.h, a.L.d1, a.d1, nq, gt, gs);
+  stage_copy(a.h, a.L.d2, a.d2, nq, gt, gs);
+  stage_copy(a.h, a.L.good, a.good, nq, gt, gs);
+  if (a.L.valid) {
+    stage_copy(a.h, a.L.vbin, a.vbin, V, gt, gs);
+    stage_copy(a.h, a.L.voff, a.voff, V + 1, gt, gs);
+    stage_copy(a.h, a.L.members, a.members, M, gt, gs);
+    stage_copy(a.h, a.L.means, a.means, 6 * V, gt, gs);
+  }
+  if (!a.L.affine) return;
+  stage_copy(a.h, a.L.surv, a.surv, V, gt, gs);
+  stage_copy(a.h, a.L.fvotes, a.fvotes, V, gt, gs);
+  stage_copy(a.h, a.L.params, a.params, 6 * V, gt, gs);
+  stage_copy(a.h, a.L.alive, a.alive, M, gt, gs);
+}
+
+// post-processing input on the device: the survivors (affine survivors, else every valid
+// bin) in list order -- their valid index and means into the host buffer, hdr[2] = their
+// count -- and, for at most ncap of them, both relation bitmasks (post_adjacency_kernel's,
+// rows of ceil(n/64) words); one work-group
+__global__ __launch_bounds__(1024) void results_post_kernel(StageArgs a, double* __restrict__ sm,
+                                                            int32_t* __restrict__ simg) {
+  __shared__ int wtot[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t V = min<int64_t>(a.scal[0], a.L.vcap);
+  int32_t* sidx = reinterpret_cast<int32_t*>(a.h + a.L.sidx);
+  double* smeans = reinterpret_cast<double*>(a.h + a.L.smeans);
+  int base = 0;
+  for (int64_t c0 = 0; c0 < V; c0 += 1024) {
+    const int64_t v = c0 + tid;
+    const bool keep = v < V && (!a.affined || a.surv[v]);
+    const uint64_t bal = __ballot(keep);
+    const int pre = __popcll(bal & ((1ull << lane) - 1));
+    if (lane == 0) wtot[wv] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wv; ++w) off += wtot[w];
+    int tot = 0;
+    for (int w = 0; w < 16; ++w) tot += wtot[w];
+    if (keep) {
+      const int k = off + pre;
+      sidx[k] = (int32_t)v;
+      for (int f = 0; f < 6; ++f) smeans[6 * (int64_t)k + f] = a.means[6 * v + f];
+      if (k < a.L.ncap) {
+        for (int f = 0; f < 6; ++f) sm[6 * k + f] = a.means[6 * v + f];
+        simg[k] = a.n_qimg ? (int32_t)(a.vbin[v] / a.nbins1) : 0;
+      }
+    }
+    base += tot;
+    __syncthreads();   // wtot reused
+  }
+  const int n = base;
+  if (tid == 0) reinterpret_cast<int64_t*>(a.h + a.L.hdr)[2] = n;
+  __threadfence_block();
+  __syncthreads();
+  if (n > a.L.ncap) return;   // the host runs post_adjacency_kernel on them instead
+  const int words = (n + 63) / 64;
+  uint64_t* pos = reinterpret_cast<uint64_t*>(a.h + a.L.pos);
+  uint64_t* ori = reinterpret_cast<uint64_t*>(a.h + a.L.ori);
+  for (int64_t t = tid; t < (int64_t)n * words; t += 1024) {
+    const int i = (int)(t / words), wd = (int)(t % words);
+    const double xi = sm[6 * i], yi = sm[6 * i + 1], ai = sm[6 * i + 2], si = sm[6 * i + 3];
+    const double txi = sm[6 * i + 4] * si / 4, tyi = sm[6 * i + 5] * si / 4;
+    uint64_t pb = 0, ob = 0;
+    for (int k = 0; k < 64; ++k) {
+      const int j = wd * 64 + k;
+      if (j >= n) break;
+      if (j == i || (a.n_qimg && simg[j] != simg[i])) continue;
+      const double xj = sm[6 * j], yj = sm[6 * j + 1], aj = sm[6 * j + 2], sj = sm[6 * j + 3];
+      const double dx = fabs(xi - xj), dy = fabs(yi - yj);
+      const bool close = dx <= txi && dy <= tyi && dx <= sm[6 * j + 4] * sj / 4 &&
+                         dy <= sm[6 * j + 5] * sj / 4;
+      if (close) pb |= 1ull << k;
+      if (fabs((ai - aj) * kRadToDeg) <= 1) ob |= 1ull << k;
+    }
+    pos[t] = pb;
+    ori[t] = ob;
+  }
+}
+
 }  // namespace
+
+int launch_results_stage(sod_ctx* ctx, const ResLayout& L, bool post) {
+  StageArgs a;
+  a.h = ctx->hres;
+  a.L = L;
+  a.idx1 = ctx->idx1.p;
+  a.d1 = ctx->d1.p;
+  a.d2 = ctx->d2.p;
+  a.good = ctx->good.p;
+  a.vbin = ctx->vbin.p;
+  a.voff = ctx->voff.p;
+  a.members = ctx->members.p;
+  a.means = ctx->means.p;
+  a.surv = ctx->surv.p;
+  a.fvotes = ctx->fvotes.p;
+  a.params = ctx->params.p;
+  a.alive = ctx->alive.p;
+  a.scal = ctx->scal.p;
+  a.selected = ctx->selected ? 1 : 0;
+  a.affined = ctx->affined ? 1 : 0;
+  a.n_qimg = ctx->n_qimg;
+  a.nbins1 = std::max<int64_t>(1, ctx->nbins1);
+  const int64_t work = std::max<int64_t>({L.nq, 6 * L.vcap, L.mcap, 1});
+  const unsigned blocks = (unsigned)std::min<int64_t>(256, (work + 255) / 256);
+  hipLaunchKernelGGL(results_pack_kernel, dim3(blocks), dim3(256), 0, ctx->stream, a);
+  SOD_HIP(ctx, hipGetLastError());
+  if (post && ctx->selected) {
+    SOD_TRY(sod_reserve(ctx, ctx->post_m, (size_t)std::max<int64_t>(1, L.ncap) * 6));
+    SOD_TRY(sod_reserve(ctx, ctx->post_img, (size_t)std::max<int64_t>(1, L.ncap)));
+    hipLaunchKernelGGL(results_post_kernel, dim3(1), dim3(1024), 0, ctx->stream, a,
+                       ctx->post_m.p, ctx->post_img.p);
+    SOD_HIP(ctx, hipGetLastError());
+  }
+  return SOD_OK;
+}
+
+// the post-processing outputs from the staged survivors: the relations the device wrote
+// (or, past ncap survivors or with the host-libm means, post_adjacency_kernel again)
+int sod_post_staged(sod_ctx* ctx, const ResLayout& L, ResHost& r) {
+  const int64_t* hdr = reinterpret_cast<const int64_t*>(ctx->hres + L.hdr);
+  const int32_t n = (int32_t)hdr[2];
+  const int32_t* sidx = reinterpret_cast<const int32_t*>(ctx->hres + L.sidx);
+  const double* smeans = reinterpret_cast<const double*>(ctx->hres + L.smeans);
+  r.n_bins = n;
+  r.bin_index.assign(sidx, sidx + n);
+  PostOut o;
+  const bool exact_redo = ctx->post_exact && !ctx->trig_exact && n;
+  if (exact_redo || n > L.ncap) {
+    std::vector<double> sel(smeans, smeans + 6 * (size_t)n);
+    std::vector<int32_t> img;
+    if (ctx->n_qimg) {
+      const uint32_t* vb = reinterpret_cast<const uint32_t*>(ctx->hres + L.vbin);
+      for (int32_t k = 0; k < n; ++k) img.push_back((int32_t)(vb[sidx[k]] / ctx->nbins1));
+    }
+    if (exact_redo) SOD_TRY(sod_exact_xy_means(ctx, sidx, n, sel.data()));
+    SOD_TRY(run_post(ctx, n, sel.data(), img.empty() ? nullptr : img.data(), o));
+  } else {
+    SOD_TRY(post_walk(n, (n + 63) / 64, reinterpret_cast<const uint64_t*>(ctx->hres + L.pos),
+                      reinterpret_cast<const uint64_t*>(ctx->hres + L.ori), smeans, o));
+  }
+  const size_t n1 = (size_t)n + 1;
+  r.pos_off.assign(n1, 0);
+  r.pos_members.assign(std::max<size_t>(1, n), 0);
+  r.ori_pos_off.assign(n1, 0);
+  r.ori_off.assign(n1, 0);
+  r.ori_members.assign(std::max<size_t>(1, n), 0);
+  r.orient.assign(std::max<size_t>(1, n), 0.0);
+  r.pose.assign(6 * std::max<size_t>(1, n), 0.0);
+  return write_post(o, &r.n_pos, r.pos_off.data(), r.pos_members.data(), &r.n_ori,
+                    r.ori_pos_off.data(), r.ori_off.data(), r.ori_members.data(), r.orient.data(),
+                    r.pose.data());
+}
 
 extern "C" {
 

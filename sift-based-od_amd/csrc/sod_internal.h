@@ -41,6 +41,24 @@ struct SiftWork;   // sift.hip: SIFT detect + describe workspace (SURVEY 8(f) ro
 // Development / test switches of one context (sod_set_option; each also read once from the
 // environment variable SOD_<NAME> at sod_create).  The defaults are the measured best; the
 // tests flip them to cover both sides of a choice.
+// sod_results_fetch: where each array lies in the page-locked staging buffer (byte offsets)
+// and the capacities it was laid out for
+struct ResLayout {
+  int64_t nq = 0, vcap = 0, mcap = 0, ncap = 0;   // queries, valid bins, members, post bins
+  int words = 0;                                  // 64-bit words per relation row (ncap)
+  bool valid = false, affine = false;             // parts staged besides the match arrays
+  size_t hdr = 0, idx1 = 0, d1 = 0, d2 = 0, good = 0, vbin = 0, voff = 0, members = 0,
+         means = 0, surv = 0, fvotes = 0, params = 0, alive = 0, sidx = 0, smeans = 0,
+         pos = 0, ori = 0, total = 0;
+};
+// the host-side outputs of sod_results_fetch (decoded keys, votes, post-processing)
+struct ResHost {
+  std::vector<int32_t> keys, votes, bin_index, pos_off, pos_members, ori_pos_off, ori_off,
+      ori_members;
+  std::vector<double> orient, pose;
+  int32_t n_bins = 0, n_pos = 0, n_ori = 0;
+};
+
 struct sod_opts {
   int match_qt = 0;            // int8 ring kernel query tiles per wave: 0 by query count; 2, 4, 8
   int match_pf = 0;            // its LDS prefetch distance: 0 default (1); 1, 2
@@ -70,6 +88,7 @@ struct sod_ctx {
   int tail_cus() const { return reserved_cus ? reserved_cus : num_cus; }
   int impl = 1;                 // matcher: 1 = int8 MFMA 16x16x64 (default), 2 = int8 32x32x32 (match_i8.hip), 0 = bf16 (match.hip)
   sod_opts opt;                 // sod_set_option
+  bool last_timed = false;      // the last matcher launch recorded begin / end events
   int mkernel = 0;              // impl 1's kernel shape (sod_match_set_kernel): 0 = by query count,
                                 // 1 = LDS ring (match_i8.hip), 2 = register-streamed (match_s.hip)
 
@@ -114,7 +133,7 @@ struct sod_ctx {
   DevBuf<float> cd1, cd2;       // merged (this shard / after allgather: global)  [nq_pad]
   DevBuf<int32_t> cidx;
   DevBuf<int32_t> gthr;         // matcher: prefilter thresholds shared by the DB chunks
-  int64_t gthr_n = 0;           //   [partial-result slot][kThrWords][nq_pad]; reset by the merge
+  int64_t gthr_n = 0;           //   words of one slot ([slot][words][nq_pad]); reset by the merge
   DevBuf<float> gd1, gd2;       // allgather landing [nranks * nq_pad]
   DevBuf<int32_t> gidx;
   DevBuf<float> d1, d2;         // sqrt distances [nq]
@@ -194,6 +213,11 @@ struct sod_ctx {
   DevBuf<double> post_m;        // [n*6] bin means
   DevBuf<uint64_t> post_pos, post_ori;   // [n * ceil(n/64)] relation bitmasks
   DevBuf<int32_t> post_img;     // [n] query image of each bin (image batches)
+
+  // ---- results staging (sod_results_fetch) ----
+  uint8_t* hres = nullptr;      // page-locked host buffer the staging kernel writes into
+  size_t hres_n = 0;
+  ResHost res;                  // host-side outputs (decoded keys, votes, post-processing)
 
   // ---- SIFT on the device (sift.hip) ----
   SiftWork* sift = nullptr;
@@ -448,6 +472,11 @@ void sod_guard_host_pose(const double rec[8], const int32_t bins[4], double* x, 
                          int32_t* ix, int32_t* iy);
 int sod_build_sigma_lut(sod_ctx* ctx, int32_t bins_sigma);
 int sod_exact_xy_means(sod_ctx* ctx, const int32_t* vbin, int nb, double* means6);
+// results staging (post.hip): the kernels that write every result into ctx->hres (layout
+// L; post = the survivors' compaction and relations too), and the host post-processing
+// over the staged survivors
+int launch_results_stage(sod_ctx* ctx, const ResLayout& L, bool post);
+int sod_post_staged(sod_ctx* ctx, const ResLayout& L, ResHost& r);
 bool sod_host_trig_matches_device();
 int launch_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double* c);
 void sod_sift_free(sod_ctx* ctx);

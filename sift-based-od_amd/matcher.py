@@ -80,7 +80,7 @@ class BFMatcher:
         if crossCheck:
             raise NotImplementedError("crossCheck is not used by the reference")
         self._ctx = ctx
-        self._resident = None      # the array object whose rows are on the device
+        self._resident = None      # (array, context, its db_gen) of the rows on the device
         self._collection = []      # add() / train(): OpenCV's train descriptor collection
         self._trained = None
         self.uploads = 0           # descriptor uploads so far (a residency check)
@@ -119,10 +119,16 @@ class BFMatcher:
         self._starts = np.cumsum([0] + [len(d) for d in self._collection])
 
     def _upload(self, d, ctx):
-        if self._resident is d and not d.flags.writeable:
+        # residency is trusted only for an array that cannot change behind our back -- the
+        # trained collection, or a read-only array owning its data (a read-only VIEW of a
+        # writeable base can change through the base) -- and only while the context still
+        # holds the DB this matcher put there (db_gen counts every upload / share / impl switch)
+        fixed = d is self._trained or (not d.flags.writeable and d.flags.owndata)
+        if (fixed and self._resident is not None and self._resident[0] is d
+                and self._resident[1] is ctx and self._resident[2] == ctx.db_gen):
             return
         ctx.upload_db(d)
-        self._resident = d
+        self._resident = (d, ctx, ctx.db_gen)
         self.uploads += 1
 
     def knnMatch(self, queryDescriptors, trainDescriptors=None, k=2):

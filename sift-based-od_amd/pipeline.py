@@ -137,7 +137,7 @@ class Main:
         self.ctx.match()
         self.ctx.ratio(ratio)
         self.ctx.float_order()
-        idx1, d1, d2, good = self.ctx.match_result()
+        idx1, d1, d2, good = self.ctx.results(parts=("match",))["match"]   # one transfer
         self._match = (idx1, good)
         self._matching = None
         self._stage = "matched"
@@ -203,7 +203,7 @@ class Main:
     def _select(self, threshold):
         self.ctx.select(threshold)
         self._sel_token += 1
-        return self.ctx.valid_result()
+        return self.ctx.results(parts=("valid",))["valid"]   # one transfer
 
     def get_valid_bins(self, threshold=5):
         """``main.py:121-132``: bins with votes >= threshold, insertion order.  The bins'
@@ -254,7 +254,7 @@ class Main:
         keypoint pairs."""
         if self._device_resident():
             self.ctx.affine(self.image_query_size, POS_FACTOR * 4, POS_FACTOR * 4, threshold)
-            a = self.ctx.affine_result()
+            a = self.ctx.results(parts=("affine",))["affine"]   # one transfer
             offs = np.asarray(self._valid_sel[1]["offsets"])
             off = offs.tolist()
             alive = a["alive"].astype(bool)
@@ -325,13 +325,16 @@ class Main:
             if run_affine:
                 self.ctx.affine(self.image_query_size, POS_FACTOR * 4.0, POS_FACTOR * 4.0,
                                 affine_threshold)
-        idx1, d1, d2, good = self.ctx.match_result()
-        out = {"idx1": idx1, "d1": d1, "d2": d2, "good": good, "valid": self.ctx.valid_result()}
+        # every result in one device -> host transfer and one wait (sod_results_fetch)
+        r = self.ctx.results(parts=("match", "valid") + (("affine",) if run_affine else ())
+                             + (("post",) if post_process else ()))
+        idx1, d1, d2, good = r["match"]
+        out = {"idx1": idx1, "d1": d1, "d2": d2, "good": good, "valid": r["valid"]}
         if run_affine:
-            out["affine"] = self.ctx.affine_result()
+            out["affine"] = r["affine"]
         if post_process:
             from .postprocessing import final_pose_from_arrays
-            out["post"] = self.ctx.postprocess()
+            out["post"] = r["post"]
             self.final_pose = final_pose_from_arrays(out["post"])
         self._match = (idx1, good)
         self._hough_bins = bins

@@ -35,6 +35,7 @@ def _ctx_session():
 @pytest.fixture
 def ctx(_ctx_session):
     _ctx_session.set_impl("i8")
+    _ctx_session.set_match_kernel("auto")
     opts = {k: _ctx_session.get_option(k) for k in _ctx_session.OPTIONS}
     yield _ctx_session
     for k, v in opts.items():          # a test's set_option stays in that test

@@ -3,6 +3,7 @@ declares; the ctypes signature table mirrors the header.  No compute calls (CPU 
 import ctypes
 import os
 import re
+import shutil
 import subprocess
 
 import pytest
@@ -76,3 +77,20 @@ def test_host_trig_is_glibc_sin_and_cos_not_sincos():
     imported = set(re.findall(r" U (\w+)(?:@\S+)?", out))
     assert {"sin", "cos"} <= imported
     assert not imported & {"sincos", "__sincos", "sincosf"}
+
+
+@pytest.mark.skipif(not shutil.which("gcc"), reason="needs gcc")
+def test_results_struct_layout(tmp_path):
+    """sod_results (sod.h) as the C compiler lays it out == the ctypes mirror (_lib.Results)."""
+    fields = [f[0] for f in _lib.Results._fields_]
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "sod.h"\nint main(void) {\n'
+                   '  printf("%zu\\n", sizeof(sod_results));\n' +
+                   "".join('  printf("%%zu\\n", offsetof(sod_results, %s));\n' % f for f in fields) +
+                   "  return 0;\n}\n")
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert got[0] == ctypes.sizeof(_lib.Results)
+    assert got[1:] == [getattr(_lib.Results, f).offset for f in fields]

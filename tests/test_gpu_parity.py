@@ -54,6 +54,48 @@ def test_matcher_edges(ctx, impl):
     assert np.array_equal(good, g["good"])
 
 
+@pytest.mark.parametrize("nq,ndb,seed", [(1, 2, 0), (17, 1000, 1), (500, 1000, 4), (700, 4099, 2),
+                                         (513, 77777, 5), (3000, 60000, 3), (500, 400000, 6)])
+def test_streamed_matcher_vs_oracle(ctx, nq, ndb, seed):
+    """The register-streamed kernel (match_s.hip: a 512-query group per wave, the DB split
+    into up to 256 ranges that exchange top-2 lists) bit for bit against the oracle: one
+    query, partial groups (17, 513), ranges of a few subtiles (1 000 rows over 256 work-
+    groups), exact duplicates of DB rows (d1 = 0) and DB rows repeated in other ranges
+    (cross-range ties: the lowest trainIdx wins), and the matcher_edges golden."""
+    rng = np.random.default_rng(seed)
+    db = synthetic.sift_like_descriptors(rng, ndb)
+    q = synthetic.sift_like_descriptors(rng, nq)
+    if ndb > 8 and nq > 8:
+        k = min(nq // 3, ndb // 2)
+        q[:k] = db[rng.integers(0, ndb, k)]
+        h = ndb // 2
+        n = min(200, h)
+        db[h:h + n] = db[:n]                       # the same rows in two far ranges
+        q[k:k + min(n, nq - k)] = db[:min(n, nq - k)]
+    ctx.set_impl("i8")
+    ctx.set_match_kernel("streamed")
+    ctx.upload_db(db)
+    ctx.upload_queries(q)
+    for _ in range(2):        # the second launch reuses the reset list slots
+        ctx.match()
+    ctx.ratio(0.75)
+    idx1, d1, d2, good = ctx.match_result()
+    e1, f1, f2 = orc.knn2_match(q, db)
+    assert np.array_equal(idx1, e1)
+    assert np.array_equal(d1, f1) and np.array_equal(d2, f2)
+    assert np.array_equal(good, orc.ratio_test(f1, f2))
+    if seed == 0:
+        g = golden("matcher_edges")
+        ctx.upload_db(g["db_des"])
+        ctx.upload_queries(g["q_des"])
+        ctx.match()
+        ctx.ratio(0.75)
+        idx1, d1, d2, good = ctx.match_result()
+        assert np.array_equal(idx1, g["idx1"])
+        assert np.array_equal(d1, g["d1"]) and np.array_equal(d2, g["d2"])
+        assert np.array_equal(good, g["good"])
+
+
 @pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("nq,ndb,seed", [(1, 2, 0), (17, 1000, 1), (700, 4099, 2), (3000, 60000, 3)])
 def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
@@ -73,14 +115,18 @@ def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
     assert np.array_equal(good, orc.ratio_test(f1, f2))
 
 
-@pytest.mark.parametrize("qt", ["2", "4", "8"])
+@pytest.mark.parametrize("qt", ["2", "4", "8", "streamed"])
 def test_matcher_query_tiles_shared_thresholds(ctx, qt):
-    """int8 matcher with each query-tile count per wave (option match_qt) over a DB split into
+    """int8 matcher with each query-tile count per wave (option match_qt; "streamed": the
+    register-streamed kernel, match_s.hip, whose DB ranges exchange top-2 lists) over a DB split into
     many chunks, so the chunks exchange prefilter thresholds mid-run: DB rows duplicated far
     apart (other chunks) make exact distance ties ACROSS chunks -- a shared threshold must
     keep them (lowest trainIdx wins), and queries equal to a DB row (d1 = 0) or near one,
     including runs of equal rows inside a chunk's seed stage."""
-    ctx.set_option("match_qt", int(qt))
+    if qt == "streamed":
+        ctx.set_match_kernel("streamed")
+    else:
+        ctx.set_option("match_qt", int(qt))
     rng = np.random.default_rng(31)
     ndb, nq = 150000, 2000
     db = synthetic.sift_like_descriptors(rng, ndb)
@@ -216,11 +262,26 @@ def test_knnmatch_resident_train_set():
         assert bf.uploads == 1
         assert [m.trainIdx for m, _ in res] == i1.tolist()
         assert [n.trainIdx for _, n in res] == i2.tolist()
+    # the context's DB replaced by another user between calls: uploaded again
+    bf._context().upload_db(db[:100])
+    res = bf.knnMatch(q, ro, k=2)
+    assert bf.uploads == 2
+    assert [m.trainIdx for m, _ in res] == i1.tolist()
+    # a read-only view of a writeable base is not trusted (it changes through the base)
+    base = db.copy()
+    view = base[:]
+    view.flags.writeable = False
+    bf.knnMatch(q, view, k=2)
+    base[i1[1]] = 255 - base[i1[1]]
+    res = bf.knnMatch(q, view, k=2)
+    assert bf.uploads == 4
+    k1, _, _ = orc.knn2_match(q, base)
+    assert [m.trainIdx for m, _ in res] == k1.tolist()
     wr = db.copy()
     bf.knnMatch(q, wr, k=2)
     wr[i1[0]] = 255 - wr[i1[0]]          # in-place change between calls: must be seen
     res = bf.knnMatch(q, wr, k=2)
-    assert bf.uploads == 3
+    assert bf.uploads == 6
     j1, _, _ = orc.knn2_match(q, wr)
     assert [m.trainIdx for m, _ in res] == j1.tolist()
     # OpenCV's collection: two sets, rows numbered within their set, imgIdx = the set
@@ -501,6 +562,32 @@ def test_fused_pipeline_equals_dense(ctx, nq, thr, n_objects, decoy):
     assert np.array_equal(outs[0]["post"]["final_pose"], outs[1]["post"]["final_pose"])
     if thr == 1 and nq > 1:
         assert len(outs[0]["valid"]["keys"]) > 2048
+    # every result in one transfer (sod_results_fetch) == the per-array getters, with the
+    # affine pass and without it (post-processing then over every valid bin: thousands at
+    # thr 1, past the staging kernel's 1 024 relation rows -> its host-relations path)
+    for run_affine in (True, False):
+        ctx.upload_queries(qs.des, qs.kp)
+        ctx.pipeline(qs.shape, (32, 32, 8, 12), ratio=0.75, vote_threshold=thr, affine_threshold=4,
+                     run_affine=run_affine)
+        _results_equal_getters(ctx, run_affine)
+
+
+def _results_equal_getters(ctx, affined=True):
+    r = ctx.results(post=True)
+    for a, b in zip(r["match"], ctx.match_result()):
+        assert np.array_equal(a, b)
+    v = ctx.valid_result()
+    for k in ("keys", "votes", "offsets", "members", "means"):
+        assert np.array_equal(r["valid"][k], v[k]), k
+    if affined:
+        a = ctx.affine_result()
+        for k in ("survived", "votes", "params", "alive"):
+            assert np.array_equal(r["affine"][k], a[k]), k
+    else:
+        assert "affine" not in r
+    p = ctx.postprocess()
+    for k in p:
+        assert np.array_equal(r["post"][k], p[k]), k
 
 
 def test_knn_indices_refused_after_matches_set(ctx):

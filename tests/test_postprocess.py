@@ -134,6 +134,9 @@ def test_pipeline_postprocess_golden(ctx, name):
     ctx.pipeline(tuple(int(v) for v in g["shape"]), int(g["bins"]))
     r = ctx.postprocess()
     assert np.array_equal(r["bin_index"], g["surv_index"])
+    f = ctx.results(post=True)["post"]          # the one-transfer form: the same outputs
+    for k in r:
+        assert np.array_equal(f[k], r[k]), k
     # the survivors' x / y means redone with glibc (sod_set_post_exact, default): main.py's
     # final pose bit for bit
     assert np.array_equal(r["final_pose"].view(np.uint64),

@@ -235,3 +235,15 @@ def test_file_store_ignores_an_unclosed_runs_files(tmp_path):
     assert out[0][0].startswith(b"fresh-") and out[1][0] == out[0][0]
     assert out[0][1] == out[1][1] == [b"r0", b"r1"]
     assert not path.exists()   # close() removed the directory
+
+
+def test_torch_host_comm_deprecated_shim():
+    """TorchHostComm left the exports in round 4: the old names still resolve, with a
+    DeprecationWarning, to a HostComm over torch.distributed."""
+    import sift_based_od_amd as pkg
+    from sift_based_od_amd import sharded
+    with pytest.warns(DeprecationWarning):
+        cls = sharded.TorchHostComm
+    assert issubclass(cls, sharded.HostComm)
+    with pytest.warns(DeprecationWarning):
+        assert pkg.TorchHostComm is cls

@@ -88,7 +88,15 @@ def main():
                             bad += 1
         if hasattr(ctx._L, "sod_debug_sstamps"):   # diagnostic build: per-wave timeline
             import ctypes as C
+            hits = np.zeros((4096, 9), np.uint32)
+            ctx._L.sod_debug_shits(hits.ctypes.data_as(C.c_void_p), 1)
             run(ctx, "streamed", 8)
+            ctx.synchronize()
+            ctx._L.sod_debug_shits(hits.ctypes.data_as(C.c_void_p), 1)
+            nl = WARM + 8
+            hw = hits[hits.sum(axis=1) > 0].astype(np.float64) / nl
+            print("  %s hit tiles per wave and launch, bodies 0..7 and the rest: %s (total %.1f)" % (
+                name, " ".join("%.2f" % v for v in hw.mean(axis=0)), hw.sum(axis=1).mean()))
             st = np.zeros((4096, 28), np.uint64)
             ctx._L.sod_debug_sstamps(st.ctypes.data_as(C.c_void_p))
             st = st.astype(np.int64)   # (one config per process: rows of other grids stay)
@@ -98,7 +106,8 @@ def main():
             print("  %s stamps over %d waves (cycles after the wave's start: median [p10 p90]); "
                   "clock %.0f MHz" % (name, len(st), np.median(clk)))
             labels = ["start", "frags", "s.scan", "s.push", "s.bar", "s.apply", "s.load", "s.pull",
-                      "w0", "x0", "w1", "x1", "w2", "x2"] + ["body%d" % b for b in range(1, 11)] + ["", "end"]
+                      "w0", "sl0", "x0", "w1", "sl1", "x1", "w2", "sl2", "x2"] + \
+                ["body%d" % b for b in range(1, 9)] + ["end"]
             for i, lab in enumerate(labels):
                 if not lab:
                     continue
