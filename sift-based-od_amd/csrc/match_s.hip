@@ -75,8 +75,12 @@ constexpr int kLag = SOD_S_LAG;
 #endif
 constexpr bool kXchg = SOD_S_XCHG;
 #ifndef SOD_S_EARLYB
-#define SOD_S_EARLYB 2            // loop bodies that exchange after every window
+#define SOD_S_EARLYB 4            // loop bodies that exchange after every window
 #endif
+#ifndef SOD_S_PRELOAD
+#define SOD_S_PRELOAD 1           // a hit window's subtiles copied, its refill issued first
+#endif
+constexpr bool kPreload = SOD_S_PRELOAD;
 constexpr int kEarlyB = SOD_S_EARLYB;
 constexpr int kSubB = 2048;       // bytes per 16-row subtile
 constexpr int kRsrc3 = 0x00020000;
@@ -444,10 +448,20 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
 #ifdef SOD_S_COUNT
       if (lane == 0) atomicAdd(&g_scounts[0], 1ull);
 #endif
+      // a window with a hit keeps a copy of its subtiles for the exact update and issues the
+      // refill of its ring slots first: the update (~0.5-2 k cycles) then runs under the
+      // loads' latency instead of delaying them (the ring's lead is only kSD subtiles)
+      Sub keep[kSN];
+      const bool hit = any != 0;
+      if constexpr (kPreload) {
+        if (__builtin_expect(hit, 0)) sfor<kSN>([&](auto J) { keep[J] = ring[w * kSN + J]; });
+#pragma unroll
+        for (int j = 0; j < kSN; ++j) load_sub(ring[w * kSN + j], (b + 1) * kSD + w * kSN + j);
+      }
 #ifdef SOD_S_NOSLOW
       if (b < 0)
 #endif
-      if (__builtin_expect(any != 0, 0)) {
+      if (__builtin_expect(hit, 0)) {
 #ifdef SOD_S_COUNT
         if (lane == 0) atomicAdd(&g_scounts[1], 1ull);
 #endif
@@ -467,7 +481,7 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
 #pragma unroll
           for (int j = 0; j < kSN; ++j) {
             if (i0 + j >= nloc) break;   // wave-uniform: beyond the range
-            const Sub& d = ring[w * kSN + j];
+            const Sub& d = kPreload ? keep[j] : ring[w * kSN + j];
             i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(d.a0, bq[t][0], d.c, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(d.a1, bq[t][1], acc, 0, 0, 0);
             const int rowb = rowl + (wave + kSNW * (i0 + j)) * kSubRows;
@@ -494,8 +508,10 @@ __global__ __launch_bounds__(kSNW * 64, 1) void match_s_kernel(
       if (b == 0 && w < 3) SSTAMP(9 + 3 * w);
 #endif
       // the window's slots take the subtiles kSD ahead
+      if constexpr (!kPreload) {
 #pragma unroll
-      for (int j = 0; j < kSN; ++j) load_sub(ring[w * kSN + j], (b + 1) * kSD + w * kSN + j);
+        for (int j = 0; j < kSN; ++j) load_sub(ring[w * kSN + j], (b + 1) * kSD + w * kSN + j);
+      }
       // exchange (the list loaded one exchange ago; then the next load)
       if constexpr (early || w == kSW - 1) {
         exch_apply();

@@ -28,12 +28,12 @@ namespace {
 
 constexpr double kRadToDeg = 180.0 / 3.141592653589793;   // CPython math.degrees factor
 
-// one thread per (row i, 64-column word): bits of the position / orientation relations
-__global__ void post_adjacency_kernel(int n, int words, const double* __restrict__ m,
-                                      const int32_t* __restrict__ img,
-                                      uint64_t* __restrict__ pos, uint64_t* __restrict__ ori) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)n * words) return;
+// word t = (row i, 64-column word) of the position / orientation relations over n bins'
+// means m[n*6]; the same code (and, -ffp-contract=off, the same bits) on the host and the
+// device
+__host__ __device__ inline void post_word(int n, int words, const double* m,
+                                          const int32_t* img, int64_t t, uint64_t* pos,
+                                          uint64_t* ori) {
   const int i = (int)(t / words), wd = (int)(t % words);
   const double xi = m[6 * i], yi = m[6 * i + 1], ai = m[6 * i + 2], si = m[6 * i + 3];
   const double txi = m[6 * i + 4] * si / 4, tyi = m[6 * i + 5] * si / 4;
@@ -52,6 +52,19 @@ __global__ void post_adjacency_kernel(int n, int words, const double* __restrict
   pos[t] = pb;
   ori[t] = ob;
 }
+
+// one thread per (row i, 64-column word): bits of the position / orientation relations
+__global__ void post_adjacency_kernel(int n, int words, const double* __restrict__ m,
+                                      const int32_t* __restrict__ img,
+                                      uint64_t* __restrict__ pos, uint64_t* __restrict__ ori) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n * words) return;
+  post_word(n, words, m, img, t, pos, ori);
+}
+
+// up to this many bins the relations are computed on the host: n^2 / 2 pair tests take
+// less than a device round trip (H2D means, launch, D2H bitmasks, wait: ~40-50 us)
+constexpr int kHostPostMax = 64;
 
 // Components over indices 0..n-1 in the order of the reference's recursive dfs started
 // from every unseen index in order; adj_next(node, from, seen) returns the node's next
@@ -96,6 +109,12 @@ int run_post(sod_ctx* ctx, int32_t n, const double* means_host, const int32_t* i
              PostOut& out) {
   if (n <= 0) return SOD_OK;
   const int words = (n + 63) / 64;
+  if (n <= kHostPostMax) {   // small: the relations on the host
+    std::vector<uint64_t> pos((size_t)n * words), ori((size_t)n * words);
+    for (int64_t t = 0; t < (int64_t)n * words; ++t)
+      post_word(n, words, means_host, img_host, t, pos.data(), ori.data());
+    return post_walk(n, words, pos.data(), ori.data(), means_host, out);
+  }
   DevBuf<double>& dm = ctx->post_m;
   DevBuf<uint64_t>& dpos = ctx->post_pos;
   DevBuf<uint64_t>& dori = ctx->post_ori;
@@ -328,25 +347,8 @@ __global__ __launch_bounds__(1024) void results_post_kernel(StageArgs a, double*
   const int words = (n + 63) / 64;
   uint64_t* pos = reinterpret_cast<uint64_t*>(a.h + a.L.pos);
   uint64_t* ori = reinterpret_cast<uint64_t*>(a.h + a.L.ori);
-  for (int64_t t = tid; t < (int64_t)n * words; t += 1024) {
-    const int i = (int)(t / words), wd = (int)(t % words);
-    const double xi = sm[6 * i], yi = sm[6 * i + 1], ai = sm[6 * i + 2], si = sm[6 * i + 3];
-    const double txi = sm[6 * i + 4] * si / 4, tyi = sm[6 * i + 5] * si / 4;
-    uint64_t pb = 0, ob = 0;
-    for (int k = 0; k < 64; ++k) {
-      const int j = wd * 64 + k;
-      if (j >= n) break;
-      if (j == i || (a.n_qimg && simg[j] != simg[i])) continue;
-      const double xj = sm[6 * j], yj = sm[6 * j + 1], aj = sm[6 * j + 2], sj = sm[6 * j + 3];
-      const double dx = fabs(xi - xj), dy = fabs(yi - yj);
-      const bool close = dx <= txi && dy <= tyi && dx <= sm[6 * j + 4] * sj / 4 &&
-                         dy <= sm[6 * j + 5] * sj / 4;
-      if (close) pb |= 1ull << k;
-      if (fabs((ai - aj) * kRadToDeg) <= 1) ob |= 1ull << k;
-    }
-    pos[t] = pb;
-    ori[t] = ob;
-  }
+  for (int64_t t = tid; t < (int64_t)n * words; t += 1024)
+    post_word(n, words, sm, a.n_qimg ? simg : nullptr, t, pos, ori);
 }
 
 }  // namespace

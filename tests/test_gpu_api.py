@@ -522,6 +522,36 @@ def test_matcher_overlap_equals_serial(use_comm, reserve, affine):
             assert np.array_equal(a0["params"], a1["params"])
 
 
+def test_cu_reserve_toggle_stress():
+    """The round-4 hang (sod_set_cu_reserve 1 -> 0 never returning from hipStreamDestroy of
+    the old CU-masked streams, about one suite run in three): the split switched on and off
+    24 times, each time with pipelines in flight (overlapped matcher, PoseBin means on the
+    side stream, timed launches -- every kind of event recorded on the streams being
+    destroyed); results stay equal to the first round's.  The test's own timeout catches a
+    hang."""
+    db = synthetic.make_database(8, 1000, seed=71)
+    qs = synthetic.make_queries(3000, seed=72, db_seed=71, kp_per_image=1000)
+    bins = (32, 32, 8, 12)
+    with _lib.Context(0) as c:
+        c.set_keypoints(db.kp, db.img, db.centroid, db.size)
+        c.upload_db(db.des)
+        c.upload_queries(qs.des, qs.kp)
+        first = None
+        for k in range(24):
+            c.set_cu_reserve(1 if k % 2 == 0 else 0)
+            if k % 2:
+                c.set_overlap(k % 4 == 1)
+            for thr in (3, 5):
+                c.pipeline(qs.shape, bins, vote_threshold=thr)
+            v = c.valid_result()
+            if first is None:
+                first = v
+            for key in ("keys", "votes", "offsets", "members"):
+                assert np.array_equal(v[key], first[key]), (k, key)
+        c.set_cu_reserve(0)
+        c.set_overlap(False)
+
+
 @pytest.mark.parametrize("nq,streams", [(600, 1), (3000, 1), (600, 2), (3000, 2)])
 def test_untimed_split_launches_equal_serial(nq, streams):
     """Under the CU split a matcher launch without timing events signals the context stream

@@ -102,7 +102,7 @@ def test_device_post_batch_golden(ctx, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,seed", [(0, 0), (1, 1), (65, 2), (1500, 3)])
+@pytest.mark.parametrize("n,seed", [(0, 0), (1, 1), (40, 4), (64, 5), (65, 2), (1500, 3)])
 def test_device_post_batch_vs_oracle(ctx, n, seed):
     rng = np.random.default_rng(seed)
     c = rng.integers(0, max(1, n // 20), n)
