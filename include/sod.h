@@ -305,11 +305,12 @@ int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* args);
  * reads, main.py:182-186, without a copy and a wait per array): one kernel writes the
  * requested parts -- SOD_RES_MATCH the match arrays, SOD_RES_VALID the valid bins (keys
  * decoded on the host, votes, offsets, members, PoseBin means), SOD_RES_AFFINE the affine
- * results, SOD_RES_POST (implies VALID) the survivors' post-processing relations -- into
+ * results, SOD_RES_POST the survivors' post-processing (relations on the device) -- into
  * page-locked host memory the context owns; one wait; the post-processing walk
  * (sod_postprocess's outputs) then runs on the host.  Pointers stay valid until the next
- * sod_results_fetch or sod_destroy.  Needs sod_ratio_enqueue (+ select for the bins, + affine
- * for its arrays); parts not requested or not enqueued come back with count 0 / NULL.  The
+ * sod_results_fetch or sod_destroy.  SOD_ESTATE without sod_ratio_enqueue (MATCH) or
+ * sod_select_enqueue (the other parts); AFFINE before sod_affine_enqueue and parts not
+ * requested come back with count 0 / NULL.  The
  * same values as sod_match_get, sod_valid_get, sod_affine_get and sod_postprocess, bit for
  * bit. */
 #define SOD_RES_MATCH 1

@@ -778,7 +778,12 @@ class Context:
 
     def postprocess(self):
         """main.py:159-168 on the pipeline's surviving (or valid) bins; ``bin_index`` maps
-        the post-processed list to valid-bin indices."""
+        the post-processed list to valid-bin indices.  One device -> host transfer
+        (sod_results_fetch, SOD_RES_POST); ``postprocess_getter`` is the sod_postprocess
+        form (the same outputs)."""
+        return self.results(parts=("post",))["post"]
+
+    def postprocess_getter(self):
         V, _ = self.valid_counts()
         a = self._post_arrays(V)
         nb = C.c_int32(0)

@@ -1451,17 +1451,21 @@ int sod_results_fetch(sod_ctx* ctx, int parts, sod_results* out) {
   SOD_TRY(set_dev(ctx));   // joins the side stream (PoseBin means)
   if (!out) return sod_fail(ctx, SOD_EINVAL, "null output");
   if (parts & ~SOD_RES_ALL) return sod_fail(ctx, SOD_EINVAL, "unknown result part");
-  if (!ctx->ratio_done) return sod_fail(ctx, SOD_ESTATE, "sod_ratio_enqueue first");
+  if ((parts & SOD_RES_MATCH) && !ctx->ratio_done)
+    return sod_fail(ctx, SOD_ESTATE, "sod_ratio_enqueue first");
+  if ((parts & ~SOD_RES_MATCH) && !ctx->selected)
+    return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
   if (ctx->selected) SOD_TRY(sod_guard_resolve(ctx));   // (patches the device results)
   const bool do_post = (parts & SOD_RES_POST) && ctx->selected;
-  const bool do_valid = ((parts & SOD_RES_VALID) || do_post) && ctx->selected;
+  const bool do_valid = (parts & SOD_RES_VALID) && ctx->selected;
   const bool do_aff = (parts & SOD_RES_AFFINE) && ctx->selected && ctx->affined;
   ResLayout L;
   L.nq = (parts & SOD_RES_MATCH) ? ctx->nq : 0;
   L.valid = do_valid;
   L.affine = do_aff;
-  L.vcap = do_valid || do_aff ? ctx->vmax : 0;
-  L.mcap = do_valid || do_aff ? ctx->mmax : 0;
+  L.keys_only = do_post;   // (image batches: the host relations path needs each bin's image)
+  L.vcap = do_valid || do_aff || do_post ? ctx->vmax : 0;
+  L.mcap = do_valid || do_aff || do_post ? ctx->mmax : 0;
   L.ncap = do_post ? std::min<int64_t>(L.vcap, 1024) : 0;
   L.words = (int)((L.ncap + 63) / 64);
   size_t o = 0;

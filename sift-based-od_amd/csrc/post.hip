@@ -265,6 +265,7 @@ struct StageArgs {
   const uint8_t* alive;
   const uint32_t* scal;   // [0] valid bins, [1] members
   int selected, affined, n_qimg;
+  int alone;   // results_post_kernel without a pack launch before it
   int64_t nbins1;
 };
 
@@ -291,8 +292,8 @@ __global__ __launch_bounds__(256) void results_pack_kernel(StageArgs a) {
   stage_copy(a.h, a.L.d1, a.d1, nq, gt, gs);
   stage_copy(a.h, a.L.d2, a.d2, nq, gt, gs);
   stage_copy(a.h, a.L.good, a.good, nq, gt, gs);
+  if (a.L.valid || a.L.keys_only) stage_copy(a.h, a.L.vbin, a.vbin, V, gt, gs);
   if (a.L.valid) {
-    stage_copy(a.h, a.L.vbin, a.vbin, V, gt, gs);
     stage_copy(a.h, a.L.voff, a.voff, V + 1, gt, gs);
     stage_copy(a.h, a.L.members, a.members, M, gt, gs);
     stage_copy(a.h, a.L.means, a.means, 6 * V, gt, gs);
@@ -315,6 +316,13 @@ __global__ __launch_bounds__(1024) void results_post_kernel(StageArgs a, double*
   const int64_t V = min<int64_t>(a.scal[0], a.L.vcap);
   int32_t* sidx = reinterpret_cast<int32_t*>(a.h + a.L.sidx);
   double* smeans = reinterpret_cast<double*>(a.h + a.L.smeans);
+  if (a.alone) {   // no pack launch: the header and the bins' keys (batch images) from here
+    if (tid == 0) {
+      reinterpret_cast<int64_t*>(a.h + a.L.hdr)[0] = V;
+      reinterpret_cast<int64_t*>(a.h + a.L.hdr)[1] = min<int64_t>(a.scal[1], a.L.mcap);
+    }
+    stage_copy(a.h, a.L.vbin, a.vbin, V, tid, 1024);
+  }
   int base = 0;
   for (int64_t c0 = 0; c0 < V; c0 += 1024) {
     const int64_t v = c0 + tid;
@@ -374,10 +382,14 @@ int launch_results_stage(sod_ctx* ctx, const ResLayout& L, bool post) {
   a.affined = ctx->affined ? 1 : 0;
   a.n_qimg = ctx->n_qimg;
   a.nbins1 = std::max<int64_t>(1, ctx->nbins1);
-  const int64_t work = std::max<int64_t>({L.nq, 6 * L.vcap, L.mcap, 1});
-  const unsigned blocks = (unsigned)std::min<int64_t>(256, (work + 255) / 256);
-  hipLaunchKernelGGL(results_pack_kernel, dim3(blocks), dim3(256), 0, ctx->stream, a);
-  SOD_HIP(ctx, hipGetLastError());
+  // post-processing alone (Context.postprocess): one launch
+  a.alone = post && ctx->selected && !L.nq && !L.valid && !L.affine;
+  if (!a.alone) {
+    const int64_t work = std::max<int64_t>({L.nq, 6 * L.vcap, L.mcap, 1});
+    const unsigned blocks = (unsigned)std::min<int64_t>(256, (work + 255) / 256);
+    hipLaunchKernelGGL(results_pack_kernel, dim3(blocks), dim3(256), 0, ctx->stream, a);
+    SOD_HIP(ctx, hipGetLastError());
+  }
   if (post && ctx->selected) {
     SOD_TRY(sod_reserve(ctx, ctx->post_m, (size_t)std::max<int64_t>(1, L.ncap) * 6));
     SOD_TRY(sod_reserve(ctx, ctx->post_img, (size_t)std::max<int64_t>(1, L.ncap)));

@@ -47,6 +47,7 @@ struct ResLayout {
   int64_t nq = 0, vcap = 0, mcap = 0, ncap = 0;   // queries, valid bins, members, post bins
   int words = 0;                                  // 64-bit words per relation row (ncap)
   bool valid = false, affine = false;             // parts staged besides the match arrays
+  bool keys_only = false;                         // the valid bins' keys alone (post only)
   size_t hdr = 0, idx1 = 0, d1 = 0, d2 = 0, good = 0, vbin = 0, voff = 0, members = 0,
          means = 0, surv = 0, fvotes = 0, params = 0, alive = 0, sidx = 0, smeans = 0,
          pos = 0, ori = 0, total = 0;

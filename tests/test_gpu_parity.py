@@ -40,6 +40,22 @@ def test_matcher_golden(ctx, name, impl):
     ctx.set_impl("bf16")
 
 
+@pytest.mark.parametrize("name", CASES)
+def test_matcher_golden_streamed(ctx, name):
+    """The golden matcher cases on the register-streamed int8 kernel (match_s.hip)."""
+    g = golden(name)
+    ctx.set_impl("i8")
+    ctx.set_match_kernel("streamed")
+    load_case(ctx, g)
+    ctx.match()
+    ctx.ratio(0.75)
+    idx1, d1, d2, good = ctx.match_result()
+    assert np.array_equal(idx1, g["idx1"])
+    assert np.array_equal(d1.view(np.uint32), g["d1"].view(np.uint32))
+    assert np.array_equal(d2.view(np.uint32), g["d2"].view(np.uint32))
+    assert np.array_equal(good, g["good"])
+
+
 @pytest.mark.parametrize("impl", IMPLS)
 def test_matcher_edges(ctx, impl):
     g = golden("matcher_edges")
@@ -585,7 +601,7 @@ def _results_equal_getters(ctx, affined=True):
             assert np.array_equal(r["affine"][k], a[k]), k
     else:
         assert "affine" not in r
-    p = ctx.postprocess()
+    p = ctx.postprocess_getter()
     for k in p:
         assert np.array_equal(r["post"][k], p[k]), k
 

@@ -132,9 +132,9 @@ def test_pipeline_postprocess_golden(ctx, name):
     ctx.upload_db(g["db_des"])
     ctx.upload_queries(g["q_des"], kp(g, "q_"))
     ctx.pipeline(tuple(int(v) for v in g["shape"]), int(g["bins"]))
-    r = ctx.postprocess()
+    r = ctx.postprocess_getter()                # sod_postprocess
     assert np.array_equal(r["bin_index"], g["surv_index"])
-    f = ctx.results(post=True)["post"]          # the one-transfer form: the same outputs
+    f = ctx.postprocess()                       # the one-transfer form: the same outputs
     for k in r:
         assert np.array_equal(f[k], r[k]), k
     # the survivors' x / y means redone with glibc (sod_set_post_exact, default): main.py's
