@@ -58,42 +58,50 @@ def calculate_bin_index(object_pose, bins, query_image_shape, ctx=None):
     return int(idx[0]), int(idx[1]), int(idx[2]), int(idx[3])
 
 
-def posebins_from_device(res, pair_of, size_of=None, token=None):
+def posebins_from_device(res, pair_of, size_of=None, token=None, idx=None):
     """PoseBin objects from a device selection (``Context.valid_result()``): ``pair_of(q)``
     returns the (kpM, kpQ) pair of member query ``q``, called only when a bin's
     ``keypoint_pairs`` is first read (the members stay device arrays until then);
     ``size_of(q)`` the model image size (ints) used when a bin has a single vote (the
     reference keeps the int tuple then).  ``token`` names the device selection the bins
-    are bound to (``PoseBin.bind_device``)."""
+    are bound to (``PoseBin.bind_device``).  ``idx``: only those valid bins (indices into
+    the selection, in the given order)."""
     # no cyclic-GC passes while ~10^4 containers are made (they were half the time at C3;
     # none of these objects forms a cycle)
     gc_was_on = gc.isenabled()
     gc.disable()
     try:
-        return _posebins(res, pair_of, size_of, token)
+        return _posebins(res, pair_of, size_of, token, idx)
     finally:
         if gc_was_on:
             gc.enable()
 
 
-def _posebins(res, pair_of, size_of, token):
+def _posebins(res, pair_of, size_of, token, idx=None):
     mem = res["members"]
     # Python scalars in bulk (tolist): per-element numpy indexing was ~2 us per bin, 3 ms of
     # main.py's get_valid_bins at C3 (1 163 bins)
-    keys = [tuple(k) for k in np.asarray(res["keys"]).tolist()]
-    votes = np.asarray(res["votes"]).tolist()
+    if idx is None:
+        sel = range(len(res["votes"]))
+        keys = [tuple(k) for k in np.asarray(res["keys"]).tolist()]
+        votes = np.asarray(res["votes"]).tolist()
+        means = np.asarray(res["means"]).tolist()
+    else:
+        sel = [int(i) for i in idx]
+        keys = [tuple(k) for k in np.asarray(res["keys"])[sel].tolist()]
+        votes = np.asarray(res["votes"])[sel].tolist()
+        means = np.asarray(res["means"])[sel].tolist()
     off = np.asarray(res["offsets"]).tolist()
-    means = np.asarray(res["means"]).tolist()
     # each bin is PoseBin(key, size, votes, None, mean) + bind_device(token, i, members,
     # pair_of), its attributes set in one dict (the two calls cost ~1 us per bin on the host;
     # tests/test_keypoints.py checks the two constructions give equal objects)
     new = object.__new__
     out = []
-    for i, key in enumerate(keys):
+    for j, (i, key) in enumerate(zip(sel, keys)):
         a, e = off[i], off[i + 1]
         m = mem[a:e]
-        mu = means[i]
-        v = votes[i]
+        mu = means[j]
+        v = votes[j]
         size = size_of(int(mem[a])) if v == 1 and size_of is not None else (mu[4], mu[5])
         b = new(PoseBin)
         b.__dict__ = {"_pairs": [], "_lazy": (pair_of, m), "_dev": (token, i, m, None),

@@ -219,6 +219,15 @@ class Main:
                 vb = [self._table[tuple(int(v) for v in k)] for k in res["keys"]]
                 for i, b in enumerate(vb):
                     b.bind_device(tok, i, mem[off[i]:off[i + 1]], self._pair)
+            elif not self.valid_bins:
+                # main.py's case (a fresh list): the bins come straight from the device
+                # selection and their PoseBin objects are made on first access -- the
+                # device-resident affine pass builds only its survivors
+                self._valid_sel = (tok, res)
+                self.valid_bins = _DeviceBins(res, self._pair, self._size_of, tok)
+                self.keypoint_pairs = _LazyPairs(self.valid_bins)
+                self._valid_thr = threshold
+                return
             else:
                 vb = posebins_from_device(res, self._pair, self._size_of, tok)
             self._valid_sel = (tok, res)
@@ -242,6 +251,9 @@ class Main:
         if self._valid_sel is None or self._stage == "assigned":
             return False
         tok, res = self._valid_sel
+        vb = self.valid_bins
+        if isinstance(vb, _DeviceBins) and vb.unbuilt():   # untouched since the selection
+            return vb.token == tok
         if tok != self._sel_token or len(self.valid_bins) != len(res["keys"]):
             return False
         return all(b.device_index(tok) == i for i, b in enumerate(self.valid_bins))
@@ -265,15 +277,27 @@ class Main:
             votes, params = a["votes"].tolist(), a["params"].tolist()   # Python scalars in bulk
             survived = a["survived"].tolist()
             out = []
+            vb = self.valid_bins
             gc_was_on = gc.isenabled()
             gc.disable()          # (no cycles among these; GC passes were a third of the loop)
             try:
-                for i, b in enumerate(self.valid_bins):
-                    b.keep_device_members(alive[off[i]:off[i + 1]], kept[koff[i]:koff[i + 1]])
-                    b.votes = votes[i]
-                    b.affine_parameters = params[i]
-                    if survived[i]:
-                        out.append(b)
+                if isinstance(vb, _DeviceBins) and vb.unbuilt():
+                    # nobody has seen the bins: build the survivors only, as the loop below
+                    # leaves them (the others are dropped unseen)
+                    sidx = [i for i, k in enumerate(survived) if k]
+                    res = self._valid_sel[1]
+                    out = posebins_from_device(res, self._pair, self._size_of, vb.token, sidx)
+                    for i, b in zip(sidx, out):
+                        b.keep_device_members(alive[off[i]:off[i + 1]], kept[koff[i]:koff[i + 1]])
+                        b.votes = votes[i]
+                        b.affine_parameters = params[i]
+                else:
+                    for i, b in enumerate(vb):
+                        b.keep_device_members(alive[off[i]:off[i + 1]], kept[koff[i]:koff[i + 1]])
+                        b.votes = votes[i]
+                        b.affine_parameters = params[i]
+                        if survived[i]:
+                            out.append(b)
             finally:
                 if gc_was_on:
                     gc.enable()
@@ -341,13 +365,51 @@ class Main:
         return out
 
 
+class _DeviceBins(list):
+    """``Main.valid_bins`` straight from a device selection (valid_result's arrays): the
+    PoseBin objects are made on the first access through any list operation, all at once
+    and in selection order; ``len`` alone builds nothing.  Until then the device-resident
+    affine pass builds only the survivors (the others are dropped unseen) -- at C3 52 of
+    1 163 bins."""
+
+    def __init__(self, res, pair_of, size_of, token):
+        super().__init__()
+        self._src = (res, pair_of, size_of)
+        self.token = token
+
+    def unbuilt(self):
+        return self._src is not None
+
+    def _build(self):
+        if self._src is not None:
+            (res, pair_of, size_of), self._src = self._src, None
+            list.extend(self, posebins_from_device(res, pair_of, size_of, self.token))
+
+    def __len__(self):
+        if self._src is not None:
+            return len(self._src[0]["votes"])
+        return list.__len__(self)
+
+    for _m in ("__getitem__", "__iter__", "__contains__", "__repr__", "__eq__", "__ne__",
+               "__lt__", "__le__", "__gt__", "__ge__", "__reversed__", "index", "count", "copy",
+               "__add__", "__mul__", "__rmul__", "__reduce_ex__", "__sizeof__", "append",
+               "extend", "insert", "remove", "pop", "clear", "sort", "reverse", "__setitem__",
+               "__delitem__", "__iadd__", "__imul__"):
+        def _f(self, *a, _m=_m, **k):
+            self._build()
+            return getattr(list, _m)(self, *a, **k)
+        locals()[_m] = _f
+    del _m, _f
+
+
 class _LazyPairs(list):
     """``Main.keypoint_pairs`` (main.py:134-137): the valid bins' pairs concatenated, built
     on first use, so the pairs stay on the device until someone reads them."""
 
     def __init__(self, bins):
         super().__init__()
-        self._bins = list(bins)
+        # (an unbuilt device list is held as it is: copying it would build every bin)
+        self._bins = bins if isinstance(bins, _DeviceBins) and bins.unbuilt() else list(bins)
         self._built = False
 
     def _build(self):

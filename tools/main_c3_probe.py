@@ -26,6 +26,7 @@ for rep in range(3):   # run_matcher's parts
     t0 = time.perf_counter(); c.ratio(0.75); c.synchronize(); t["ratio+sync"] = time.perf_counter() - t0
     t0 = time.perf_counter(); c.float_order(); c.synchronize(); t["float_order"] = time.perf_counter() - t0
     t0 = time.perf_counter(); r = c.match_result(); t["match_result"] = time.perf_counter() - t0
+    t0 = time.perf_counter(); r = c.results(parts=("match",)); t["results(match)"] = time.perf_counter() - t0
     print("matcher parts", {k: round(v * 1e3, 3) for k, v in t.items()}, flush=True)
 for rep in range(4):
     t = {}
@@ -33,9 +34,11 @@ for rep in range(4):
     t0 = time.perf_counter(); m.apply_hough_transform(bins); c.synchronize(); t["hough+sync"] = time.perf_counter() - t0
     t0 = time.perf_counter(); c.select(5); c.synchronize(); t["select+sync"] = time.perf_counter() - t0
     t0 = time.perf_counter(); res = c.valid_result(); t["valid_result"] = time.perf_counter() - t0
+    t0 = time.perf_counter(); res = c.results(parts=("valid",))["valid"]; t["results(valid)"] = time.perf_counter() - t0
     t0 = time.perf_counter(); vb = posebins_from_device(res, m._pair, m._size_of, 1); t["posebins"] = time.perf_counter() - t0
     t0 = time.perf_counter(); m.valid_bins = []; m.get_valid_bins(5); t["get_valid_bins"] = time.perf_counter() - t0
     t0 = time.perf_counter(); m.apply_affine_parameters(4); t["affine"] = time.perf_counter() - t0
+    t0 = time.perf_counter(); m.post_process(); t["post_process"] = time.perf_counter() - t0
     m.valid_bins = []
     print("rep", rep, {k: round(v * 1e3, 3) for k, v in t.items()}, len(vb), flush=True)
 c.close()
