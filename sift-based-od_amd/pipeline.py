@@ -267,36 +267,44 @@ class Main:
         if self._device_resident():
             self.ctx.affine(self.image_query_size, POS_FACTOR * 4, POS_FACTOR * 4, threshold)
             a = self.ctx.results(parts=("affine",))["affine"]   # one transfer
-            offs = np.asarray(self._valid_sel[1]["offsets"])
-            off = offs.tolist()
-            alive = a["alive"].astype(bool)
-            # every bin's surviving members with one mask (per-bin masking was ~1 us a bin)
-            kept = np.asarray(self._valid_sel[1]["members"])[alive]
-            koff = np.concatenate([[0], np.cumsum(np.add.reduceat(alive.astype(np.int64), offs[:-1]))]).tolist() \
-                if len(off) > 1 else [0]
-            votes, params = a["votes"].tolist(), a["params"].tolist()   # Python scalars in bulk
-            survived = a["survived"].tolist()
-            out = []
+            res = self._valid_sel[1]
+            offs = np.asarray(res["offsets"])
+            alive = a["alive"]
+            survived = a["survived"]
             vb = self.valid_bins
             gc_was_on = gc.isenabled()
             gc.disable()          # (no cycles among these; GC passes were a third of the loop)
             try:
                 if isinstance(vb, _DeviceBins) and vb.unbuilt():
                     # nobody has seen the bins: build the survivors only, as the loop below
-                    # leaves them (the others are dropped unseen)
-                    sidx = [i for i, k in enumerate(survived) if k]
-                    res = self._valid_sel[1]
+                    # leaves them (the others are dropped unseen); per-survivor slices, not
+                    # a pass over every member
+                    sidx = np.nonzero(survived)[0].tolist()
                     out = posebins_from_device(res, self._pair, self._size_of, vb.token, sidx)
-                    for i, b in zip(sidx, out):
-                        b.keep_device_members(alive[off[i]:off[i + 1]], kept[koff[i]:koff[i + 1]])
-                        b.votes = votes[i]
-                        b.affine_parameters = params[i]
+                    votes = a["votes"][sidx].tolist()
+                    params = a["params"][sidx].tolist()
+                    mem = np.asarray(res["members"])
+                    lo_hi = offs.tolist()
+                    for j, (i, b) in enumerate(zip(sidx, out)):
+                        lo, hi = lo_hi[i], lo_hi[i + 1]
+                        al = alive[lo:hi]
+                        b.keep_device_members(al, mem[lo:hi][al])
+                        b.votes = votes[j]
+                        b.affine_parameters = params[j]
                 else:
+                    off = offs.tolist()
+                    # every bin's surviving members with one mask (per-bin masking was ~1 us a bin)
+                    kept = np.asarray(res["members"])[alive]
+                    koff = np.concatenate([[0], np.cumsum(np.add.reduceat(
+                        alive.astype(np.int64), offs[:-1]))]).tolist() if len(off) > 1 else [0]
+                    votes, params = a["votes"].tolist(), a["params"].tolist()   # scalars in bulk
+                    surv = survived.tolist()
+                    out = []
                     for i, b in enumerate(vb):
                         b.keep_device_members(alive[off[i]:off[i + 1]], kept[koff[i]:koff[i + 1]])
                         b.votes = votes[i]
                         b.affine_parameters = params[i]
-                        if survived[i]:
+                        if surv[i]:
                             out.append(b)
             finally:
                 if gc_was_on:
@@ -306,7 +314,7 @@ class Main:
                 # survivors' centroids as the reference computes them here (the host's cos /
                 # sin per member, sod_exact_means), so post_process's <= thresholds and the
                 # final pose see main.py's values bit for bit
-                sidx = [i for i, k in enumerate(survived) if k]
+                sidx = np.nonzero(survived)[0].tolist()
                 for b, (x, y) in zip(out, self.ctx.exact_means(sidx).tolist()):
                     b.centroid = (x, y)
             self.valid_bins = out
