@@ -161,8 +161,11 @@ int sod_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double
  * one-work-group Hough kernel), select_multi (1: multi-kernel selection for small windows),
  * sift_stream_mask, sift_sort_max, sift_desc_range_max, sift_layer_split, sift_side_mask,
  * sift_fork2, sift_early_desc, sift_direct, sift_eager_rank (SIFT scheduling A/B and the
- * rank / ranged-enumeration test paths), debug_sync (stderr trace of long stream waits).
- * None changes results.  SOD_EINVAL for an unknown name. */
+ * rank / ranged-enumeration test paths), debug_sync (stderr trace of long stream waits)
+ * change no result; affine_fma (1: remove_outliers' np.matmul(M, X), AffineParameters.py:145,
+ * evaluated as fma(m1, x, m2 y) like the host numpy's BLAS on an FMA CPU; 0: two roundings)
+ * selects the reference's own rounding, which the Python layer probes once per process.
+ * SOD_EINVAL for an unknown name. */
 int sod_set_option(sod_ctx* ctx, const char* name, int64_t value);
 int sod_get_option(sod_ctx* ctx, const char* name, int64_t* value);
 /* Matcher on a stream of its own (1) or on the context stream (0, default).  With 1 the

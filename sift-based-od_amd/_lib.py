@@ -38,6 +38,30 @@ class PipelineArgs(C.Structure):
                 ("y_factor", C.c_double), ("run_affine", C.c_int32)]
 
 
+_MATMUL_FMA = None
+
+
+def numpy_matmul_fma():
+    """1 when this host's numpy evaluates remove_outliers' 2x2 product np.matmul(M, X)
+    (AffineParameters.py:145) as fma(m1, x, m2*y) -- OpenBLAS's dgemv on an FMA CPU -- for
+    every probed value, 0 when as m1*x + m2*y (two roundings) or anything else; probed once
+    per process (exact fma by rational arithmetic)."""
+    global _MATMUL_FMA
+    if _MATMUL_FMA is None:
+        from fractions import Fraction
+        rng = np.random.default_rng(12345)
+        fma_all, differs = True, False
+        for m1, m2, x, y in zip(rng.uniform(-2, 2, 256), rng.uniform(-2, 2, 256),
+                                rng.uniform(0, 1500, 256), rng.uniform(0, 1000, 256)):
+            m1, m2, x, y = float(m1), float(m2), float(x), float(y)
+            r = float(np.matmul([[m1, m2], [m2, m1]], [x, y])[0])
+            f = float(Fraction(m1) * Fraction(x) + Fraction(m2 * y))
+            fma_all &= r == f
+            differs |= f != m1 * x + m2 * y
+        _MATMUL_FMA = 1 if fma_all and differs else 0
+    return _MATMUL_FMA
+
+
 class Results(C.Structure):
     """sod_results (sod.h): pointers into the context's page-locked staging buffer."""
     _fields_ = [("nq", C.c_int64), ("idx1", C.POINTER(C.c_int32)), ("d1", C.POINTER(C.c_float)),
@@ -232,6 +256,8 @@ class Context:
         self.n_total = 0
         self.bins = None
         self.db_gen = 0      # counts DB uploads / shares / impl switches (residency checks)
+        # the outlier test's M.X rounding of the reference on this host (AffineParameters.py:145)
+        self._chk(self._L.sod_set_option(self._h, b"affine_fma", numpy_matmul_fma()))
 
     # -- plumbing --
     def _chk(self, rc):
@@ -339,7 +365,8 @@ class Context:
 
     OPTIONS = ("match_qt", "match_pf", "hough_fused", "select_multi", "sift_stream_mask",
                "sift_sort_max", "sift_desc_range_max", "sift_layer_split", "sift_side_mask",
-               "sift_fork2", "sift_early_desc", "sift_direct", "sift_eager_rank", "debug_sync")
+               "sift_fork2", "sift_early_desc", "sift_direct", "sift_eager_rank", "debug_sync",
+               "affine_fma")
 
     def set_option(self, name, value):
         """A tuning / test switch of this context by name (sod.h sod_set_option); returns the

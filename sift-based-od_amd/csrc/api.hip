@@ -326,6 +326,7 @@ const OptEntry kOpts[] = {
     {"sift_early_desc", &sod_opts::sift_early_desc},
     {"sift_direct", &sod_opts::sift_direct},
     {"sift_eager_rank", &sod_opts::sift_eager_rank},
+    {"affine_fma", &sod_opts::affine_fma},
     {"debug_sync", &sod_opts::debug_sync},
 };
 const OptEntry* find_opt(const char* name) {

@@ -1692,7 +1692,8 @@ __device__ __forceinline__ void affine_groups(
     const float* __restrict__ qx, const float* __restrict__ qy, const int32_t* __restrict__ isig,
     int qw, int qh, const int32_t* __restrict__ bwh, double xf, double yf, int thr, int max_iter,
     const double* __restrict__ params_in, uint8_t* __restrict__ surv,
-    int32_t* __restrict__ votes, double* __restrict__ params, uint8_t* __restrict__ alive) {
+    int32_t* __restrict__ votes, double* __restrict__ params, uint8_t* __restrict__ alive,
+    int mxfma) {
   const int lane = threadIdx.x & (G - 1);                 // lane within the bin's group
   const int64_t NB = nb_dev ? (int64_t)nb_dev[0] : nb_host;
   // every group of the wave runs the loop the same number of times (shuffles need the
@@ -1779,8 +1780,11 @@ __device__ __forceinline__ void affine_groups(
         for (int t = 0; t < kAffU; ++t) {
           if (!al[t]) continue;
           const double x = fx[t], y = fy[t];
-          const double up = (prm[0] * x + prm[1] * y) + prm[4];
-          const double vp = (prm[2] * x + prm[3] * y) + prm[5];
+          // np.matmul(M, X) + T (AffineParameters.py:145-146): on a host whose numpy
+          // evaluates the 2x2 product as fma(m1, x, m2 y) (OpenBLAS dgemv, option
+          // affine_fma, set by the Python layer from a probe of np.matmul), the same
+          const double up = (mxfma ? fma(prm[0], x, prm[1] * y) : prm[0] * x + prm[1] * y) + prm[4];
+          const double vp = (mxfma ? fma(prm[2], x, prm[3] * y) : prm[2] * x + prm[3] * y) + prm[5];
           if (fabs(up - (double)fu[t]) > xref || fabs(vp - (double)fw[t]) > yref) {
             alive[j0 + (int64_t)t * G] = 0;
             ++dropped;
@@ -1811,11 +1815,12 @@ __global__ __launch_bounds__(256) void affine_kernel(
     const int32_t* __restrict__ bwh, double xf, double yf, int thr, int max_iter,
     const double* __restrict__ params_in,
     uint8_t* __restrict__ surv, int32_t* __restrict__ votes, double* __restrict__ params,
-    uint8_t* __restrict__ alive) {
+    uint8_t* __restrict__ alive, int mxfma) {
   constexpr int G = kAffG;
   affine_groups<G>((int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G,
                    (int64_t)gridDim.x * (blockDim.x / G), nb_host, nb_dev, off, mx, my, qx, qy,
-                   isig, qw, qh, bwh, xf, yf, thr, max_iter, params_in, surv, votes, params, alive);
+                   isig, qw, qh, bwh, xf, yf, thr, max_iter, params_in, surv, votes, params, alive,
+                   mxfma);
 }
 
 // The PoseBin means (blocks 0..nM-1) beside the affine verification (blocks nM..), one wave
@@ -1830,13 +1835,13 @@ __global__ __launch_bounds__(64) void means_affine_kernel(
     const float* __restrict__ mx, const float* __restrict__ my, const float* __restrict__ qx,
     const float* __restrict__ qy, const int32_t* __restrict__ isig, int qw, int qh, double xf,
     double yf, int thr, uint8_t* __restrict__ surv, int32_t* __restrict__ votes,
-    double* __restrict__ params, uint8_t* __restrict__ alive) {
+    double* __restrict__ params, uint8_t* __restrict__ alive, int mxfma) {
   __shared__ double xs[7][kMeansB];
   if ((int)blockIdx.x < nM)
     means_wave(blockIdx.x, nM, xs, scal, voff, members, pose, msize, rtab, means);
   else
     affine_groups<64>(blockIdx.x - nM, gridDim.x - nM, 0, scal, voff, mx, my, qx, qy, isig, qw, qh,
-                      nullptr, xf, yf, thr, 1 << 30, nullptr, surv, votes, params, alive);
+                      nullptr, xf, yf, thr, 1 << 30, nullptr, surv, votes, params, alive, mxfma);
 }
 
 }  // namespace
@@ -2456,7 +2461,8 @@ int launch_means_affine(sod_ctx* ctx, int32_t qw, int32_t qh, double xf, double 
                      ctx->scal.p, ctx->voff.p, ctx->members.p, ctx->pose.p,
                      reinterpret_cast<const int2*>(ctx->msize.p), ctx->rtab.p, ctx->means.p,
                      ctx->amx.p, ctx->amy.p, ctx->aqx.p, ctx->aqy.p, ctx->aisig.p, qw, qh, xf, yf,
-                     thr, ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p);
+                     thr, ctx->surv.p, ctx->fvotes.p, ctx->params.p, ctx->alive.p,
+                     ctx->opt.affine_fma);
   SOD_HIP(ctx, hipGetLastError());
   ++ctx->means_id;
   ctx->hread_id[ctx->hpar] = 0;   // stream order, as launch_means(ctx, true)
@@ -2512,7 +2518,8 @@ int launch_affine(sod_ctx* ctx, int64_t nb_host, bool count_on_device, const int
   const int wg = std::max(1, ctx->tail_cus() * 4);
   hipLaunchKernelGGL(affine_kernel, dim3(wg), dim3(256), 0, ctx->stream, nb_host,
                      count_on_device ? dev_count : nullptr, offsets, mx, my, qx, qy, isig, qw, qh,
-                     bwh, xf, yf, thr, max_iter, params_in, surv, votes, params, alive);
+                     bwh, xf, yf, thr, max_iter, params_in, surv, votes, params, alive,
+                     ctx->opt.affine_fma);
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }

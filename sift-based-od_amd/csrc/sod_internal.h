@@ -74,6 +74,8 @@ struct sod_opts {
   int sift_early_desc = 1;     // 0: descriptors after the sort, of the final list
   int sift_direct = 1;         // 0: a lone image's results copied after the sync
   int sift_eager_rank = 0;     // 1: the rank-path launches always enqueued with the sort
+  int affine_fma = 0;          // 1: remove_outliers' np.matmul(M, X) as fma(m1, x, m2 y) (the
+                               // host numpy's dgemv on an FMA CPU; set by the Python layer)
   int debug_sync = 0;          // 1: stderr trace of long stream waits and stream re-creation
 };
 

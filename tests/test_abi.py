@@ -94,3 +94,19 @@ def test_results_struct_layout(tmp_path):
                                           check=True).stdout.split()]
     assert got[0] == ctypes.sizeof(_lib.Results)
     assert got[1:] == [getattr(_lib.Results, f).offset for f in fields]
+
+
+def test_numpy_matmul_probe():
+    """The Python layer's probe of how this host's numpy rounds remove_outliers' 2x2 product
+    (AffineParameters.py:145): 1 = fma(m1, x, m2*y) on every probed value, 0 otherwise; it
+    agrees with a second, independent sample."""
+    from fractions import Fraction
+    import numpy as np
+    got = _lib.numpy_matmul_fma()
+    assert got in (0, 1)
+    rng = np.random.default_rng(99)
+    same = []
+    for m1, m2, x, y in rng.uniform(-3, 3, (200, 4)) * [1, 1, 500, 500]:
+        r = float(np.matmul([[m1, m2], [0.0, 1.0]], [x, y])[0])
+        same.append(r == float(Fraction(m1) * Fraction(x) + Fraction(float(m2 * y))))
+    assert all(same) == bool(got)

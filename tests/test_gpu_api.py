@@ -760,3 +760,53 @@ def test_select_one_workgroup_equals_multi_kernel(bins):
         dbkp, qkp, images = oracle_inputs(db, kp_)
         o = orc.run_pipeline(des, qkp, db.des, dbkp, images, bins, shape)
         assert_stages_equal_oracle(b["valid"], b["affine"], o["table"], o["valid"], o["affine"])
+
+
+def _threshold_members(n, seed):
+    """Members whose outlier test (AffineParameters.py:145-158) sits exactly on the x
+    tolerance under numpy's rounding of np.matmul(M, X) and one ulp past it under the
+    other rounding: tx chosen so that np.matmul(M, X)[0] + tx - u == x_ref exactly."""
+    rng = np.random.default_rng(seed)
+    prm, pts = [], []
+    while len(pts) < n:
+        m = rng.uniform(-1.5, 1.5, 4)
+        x, y = float(np.float32(rng.uniform(0, 1500))), float(np.float32(rng.uniform(0, 1000)))
+        u, v = float(np.float32(rng.uniform(0, 1500))), float(np.float32(rng.uniform(0, 1000)))
+        r = np.matmul([[m[0], m[1]], [m[2], m[3]]], [x, y])
+        plain = m[0] * x + m[1] * y
+        if r[0] == plain:
+            continue                     # this member does not tell the roundings apart
+        x_ref = 16.0                      # query width 2048, i_sigma 1, x_factor 128
+        tx = u + x_ref - r[0]
+        if (r[0] + tx) - u != x_ref:
+            continue
+        if ((plain + tx) - u > x_ref) == ((r[0] + tx) - u > x_ref):
+            continue
+        ty = v - r[1]                     # v well inside its tolerance
+        prm.append([m[0], m[1], m[2], m[3], tx, ty])
+        pts.append((x, y, u, v))
+    return np.array(prm), np.array(pts)
+
+
+def test_outlier_test_rounding_follows_numpy():
+    """remove_outliers' np.matmul(M, X) (AffineParameters.py:145) is evaluated with this
+    host's numpy rounding (option affine_fma, probed by the Python layer): members placed
+    exactly on the x tolerance under that rounding -- and one ulp off it under the other --
+    get the reference's keep / drop decision, bin by bin (one member per bin, params
+    given: one remove_outliers round, sod_affine_batch max_iter 1)."""
+    prm, pts = _threshold_members(64, 7)
+    n = len(prm)
+    with _lib.Context(0) as c:
+        fma = c.get_option("affine_fma")
+        assert fma == _lib.numpy_matmul_fma()
+        r = c.affine_batch(np.arange(n + 1), pts[:, 0], pts[:, 1], pts[:, 2], pts[:, 3],
+                           np.ones(n, np.int32), (2048, 2048), 128.0, 128.0, threshold=0,
+                           max_iter=1, params_in=prm)
+        ref = [orc.remove_outliers(p, [(q[0], q[1])], [(q[2], q[3])], 1, (2048, 2048),
+                                   128.0, 128.0)[0][0] for p, q in zip(prm, pts)]
+        assert np.array_equal(r["alive"], np.array(ref)), (fma, int((r["alive"] != ref).sum()))
+        c.set_option("affine_fma", 1 - fma)    # the other rounding disagrees on every member
+        r2 = c.affine_batch(np.arange(n + 1), pts[:, 0], pts[:, 1], pts[:, 2], pts[:, 3],
+                            np.ones(n, np.int32), (2048, 2048), 128.0, 128.0, threshold=0,
+                            max_iter=1, params_in=prm)
+        assert not np.any(r2["alive"] == np.array(ref))
