@@ -398,6 +398,13 @@ class _DeviceBins(list):
             return len(self._src[0]["votes"])
         return list.__len__(self)
 
+    def __radd__(self, other):
+        # `a_list + self`: list's concatenation reads the right operand's item array
+        # directly (C level, no method call), which is empty until built; a subclass's
+        # reflected method runs first
+        self._build()
+        return list.__add__(list(other), self)
+
     for _m in ("__getitem__", "__iter__", "__contains__", "__repr__", "__eq__", "__ne__",
                "__lt__", "__le__", "__gt__", "__ge__", "__reversed__", "index", "count", "copy",
                "__add__", "__mul__", "__rmul__", "__reduce_ex__", "__sizeof__", "append",
@@ -425,6 +432,10 @@ class _LazyPairs(list):
             self._built = True
             for b in self._bins:
                 super().extend(b.keypoint_pairs)
+
+    def __radd__(self, other):   # (see _DeviceBins.__radd__)
+        self._build()
+        return list.__add__(list(other), self)
 
     for _m in ("__len__", "__getitem__", "__iter__", "__contains__", "__repr__", "__eq__",
                "__reversed__", "index", "count", "copy", "__add__", "__mul__"):

@@ -71,3 +71,15 @@ def test_subset_equals_full_build_and_pairs():
     lp = _LazyPairs(vb)
     assert vb.unbuilt()                  # holding the pairs view builds nothing
     assert list(lp) == [p for b in full for p in b.keypoint_pairs]
+
+
+def test_left_concatenation_sees_the_bins():
+    """`a_list + bins` (list's C concatenation reads the right operand's items directly)
+    builds the lazy lists first."""
+    res = _res()
+    ref = posebins_from_device(res, _pair, _size, 4)
+    got = ["x"] + _DeviceBins(res, _pair, _size, 4)
+    assert got[0] == "x"
+    _same(got[1:], ref)
+    lp = _LazyPairs(_DeviceBins(res, _pair, _size, 4))
+    assert [] + lp == [p for b in ref for p in b.keypoint_pairs]
