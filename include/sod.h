@@ -302,6 +302,9 @@ typedef struct sod_pipeline_args {
   int32_t affine_threshold; /* 4   main.py:185            */
   double x_factor, y_factor; /* 128 = pos_factor*4 main.py:141,150 */
   int32_t run_affine;
+  /* SOD_RES_* parts to stage right behind the pipeline (0: none): the next
+   * sod_results_fetch of those parts only waits, when no other call came in between */
+  int32_t stage_parts;
 } sod_pipeline_args;
 int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* args);
 
@@ -310,9 +313,10 @@ int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* args);
  * requested parts -- SOD_RES_MATCH the match arrays, SOD_RES_VALID the valid bins (keys
  * decoded on the host, votes, offsets, members, PoseBin means), SOD_RES_AFFINE the affine
  * results, SOD_RES_POST the survivors' post-processing (relations on the device) -- into
- * page-locked host memory the context owns; one wait; the post-processing walk
+ * page-locked host memory the context owns (or finds them there, staged by the pipeline
+ * enqueue: sod_pipeline_args.stage_parts); one wait; the post-processing walk
  * (sod_postprocess's outputs) then runs on the host.  Pointers stay valid until the next
- * sod_results_fetch or sod_destroy.  SOD_ESTATE without sod_ratio_enqueue (MATCH) or
+ * sod_results_fetch, staging pipeline enqueue or sod_destroy.  SOD_ESTATE without sod_ratio_enqueue (MATCH) or
  * sod_select_enqueue (the other parts); AFFINE before sod_affine_enqueue and parts not
  * requested come back with count 0 / NULL.  The
  * same values as sod_match_get, sod_valid_get, sod_affine_get and sod_postprocess, bit for

@@ -35,7 +35,7 @@ class PipelineArgs(C.Structure):
     _fields_ = [("ratio", C.c_double), ("query_h", C.c_int32), ("query_w", C.c_int32),
                 ("bins", C.c_int32 * 4), ("vote_threshold", C.c_int32),
                 ("affine_threshold", C.c_int32), ("x_factor", C.c_double),
-                ("y_factor", C.c_double), ("run_affine", C.c_int32)]
+                ("y_factor", C.c_double), ("run_affine", C.c_int32), ("stage_parts", C.c_int32)]
 
 
 _MATMUL_FMA = None
@@ -551,8 +551,13 @@ class Context:
         return out
 
     def pipeline(self, query_shape, bins=15, ratio=0.75, vote_threshold=5, affine_threshold=4,
-                 x_factor=128.0, y_factor=128.0, run_affine=True):
+                 x_factor=128.0, y_factor=128.0, run_affine=True, stage=()):
+        """The whole path in one enqueue (sod_pipeline_enqueue); ``stage``: result parts
+        ("match", "valid", "affine", "post") staged right behind it, so that the next
+        ``results()`` of those parts only waits."""
         a = PipelineArgs()
+        for p in stage:
+            a.stage_parts |= self.RES[p]
         a.ratio = float(ratio)
         a.query_h, a.query_w = int(query_shape[0]), int(query_shape[1])
         for i, v in enumerate(bins4(bins)):

@@ -20,6 +20,7 @@ thread_local std::string g_err;  // errors before a ctx exists
 // so whatever comes next on the main stream sees their results.
 int set_dev(sod_ctx* ctx, bool join = true, bool flush = true) {
   if (!ctx) return SOD_EINVAL;
+  ++ctx->res_epoch;   // any call may change results: staged ones are no longer current
   SOD_HIP(ctx, hipSetDevice(ctx->device));
   if (flush) SOD_TRY(sod_means_flush(ctx));
   if (join && ctx->side_pending) {
@@ -1448,15 +1449,9 @@ int sod_affine_get(sod_ctx* ctx, uint8_t* survived, int32_t* votes, double* para
 }
 
 // ---- results staging -----------------------------------------------------------------
-int sod_results_fetch(sod_ctx* ctx, int parts, sod_results* out) {
-  SOD_TRY(set_dev(ctx));   // joins the side stream (PoseBin means)
-  if (!out) return sod_fail(ctx, SOD_EINVAL, "null output");
-  if (parts & ~SOD_RES_ALL) return sod_fail(ctx, SOD_EINVAL, "unknown result part");
-  if ((parts & SOD_RES_MATCH) && !ctx->ratio_done)
-    return sod_fail(ctx, SOD_ESTATE, "sod_ratio_enqueue first");
-  if ((parts & ~SOD_RES_MATCH) && !ctx->selected)
-    return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
-  if (ctx->selected) SOD_TRY(sod_guard_resolve(ctx));   // (patches the device results)
+// lay out `parts` of the current results in the page-locked buffer and enqueue the kernels
+// that write them there (state checks done by the caller, after set_dev)
+static int results_stage(sod_ctx* ctx, int parts, ResLayout* out) {
   const bool do_post = (parts & SOD_RES_POST) && ctx->selected;
   const bool do_valid = (parts & SOD_RES_VALID) && ctx->selected;
   const bool do_aff = (parts & SOD_RES_AFFINE) && ctx->selected && ctx->affined;
@@ -1493,23 +1488,55 @@ int sod_results_fetch(sod_ctx* ctx, int parts, sod_results* out) {
   L.pos = take((size_t)L.ncap * L.words * 8);
   L.ori = take((size_t)L.ncap * L.words * 8);
   L.total = o;
-  if (ctx->hres_n < L.total) {   // (nothing writes into the old buffer: every fetch waits)
+  if (ctx->hres_n < L.total) {
+    // a staging kernel of an earlier enqueue may still write into the old buffer
+    SOD_HIP(ctx, sod_stream_sync(ctx->stream));
     if (ctx->hres) (void)hipHostFree(ctx->hres);
     ctx->hres = nullptr;
     ctx->hres_n = 0;
     SOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->hres), L.total, hipHostMallocDefault));
     ctx->hres_n = L.total;
   }
-  reinterpret_cast<int64_t*>(ctx->hres + L.hdr)[2] = 0;
   SOD_TRY(launch_results_stage(ctx, L, do_post));
+  *out = L;
+  return SOD_OK;
+}
+
+int sod_results_fetch(sod_ctx* ctx, int parts, sod_results* out) {
+  if (!ctx) return SOD_EINVAL;
+  // staged by the pipeline enqueue (or an earlier fetch) and nothing called since
+  const bool reuse = ctx->staged_epoch == ctx->res_epoch && (parts & ~ctx->staged_parts) == 0;
+  SOD_TRY(set_dev(ctx));   // joins the side stream (PoseBin means)
+  if (!out) return sod_fail(ctx, SOD_EINVAL, "null output");
+  if (parts & ~SOD_RES_ALL) return sod_fail(ctx, SOD_EINVAL, "unknown result part");
+  if ((parts & SOD_RES_MATCH) && !ctx->ratio_done)
+    return sod_fail(ctx, SOD_ESTATE, "sod_ratio_enqueue first");
+  if ((parts & ~SOD_RES_MATCH) && !ctx->selected)
+    return sod_fail(ctx, SOD_ESTATE, "sod_select_enqueue first");
+  if (ctx->selected) SOD_TRY(sod_guard_resolve(ctx));   // (patches the device results)
+  const bool do_post = (parts & SOD_RES_POST) && ctx->selected;
+  const bool do_valid = (parts & SOD_RES_VALID) && ctx->selected;
+  const bool do_aff = (parts & SOD_RES_AFFINE) && ctx->selected && ctx->affined;
+  ResLayout L;
+  int staged = parts;
+  if (reuse) {
+    L = ctx->staged_L;
+    staged = ctx->staged_parts;
+  } else {
+    SOD_TRY(results_stage(ctx, parts, &L));
+  }
   SOD_HIP(ctx, sod_stream_sync(ctx->stream));
+  // the buffer holds these parts until the next call (a second fetch reads it again)
+  ctx->staged_L = L;
+  ctx->staged_parts = staged;
+  ctx->staged_epoch = ctx->res_epoch;
   const int64_t* hdr = reinterpret_cast<const int64_t*>(ctx->hres + L.hdr);
   const int64_t V = L.vcap ? hdr[0] : 0, M = L.vcap ? hdr[1] : 0;
   ResHost& r = ctx->res;
   const uint8_t* h = ctx->hres;
   *out = sod_results{};
-  out->nq = L.nq;
-  if (L.nq) {
+  out->nq = (parts & SOD_RES_MATCH) ? L.nq : 0;
+  if (out->nq) {
     out->idx1 = reinterpret_cast<const int32_t*>(h + L.idx1);
     out->d1 = reinterpret_cast<const float*>(h + L.d1);
     out->d2 = reinterpret_cast<const float*>(h + L.d2);
@@ -1574,6 +1601,18 @@ int sod_pipeline_enqueue(sod_ctx* ctx, const sod_pipeline_args* a) {
   if (a->run_affine)
     SOD_TRY(sod_affine_enqueue(ctx, a->query_w, a->query_h, a->x_factor, a->y_factor,
                                a->affine_threshold));
+  // the results' staging kernels right behind the pipeline (sod_results_fetch then only
+  // waits): not while the boundary guard is armed (its host resolve may still patch them)
+  if (a->stage_parts & ~SOD_RES_ALL) return sod_fail(ctx, SOD_EINVAL, "unknown result part");
+  if (a->stage_parts && ctx->trig_exact && ctx->selected) {
+    SOD_TRY(set_dev(ctx));   // the deferred PoseBin means run, the side stream joins
+    SOD_TRY(sod_guard_resolve(ctx));
+    ResLayout L;
+    SOD_TRY(results_stage(ctx, a->stage_parts, &L));
+    ctx->staged_L = L;
+    ctx->staged_parts = a->stage_parts;
+    ctx->staged_epoch = ctx->res_epoch;
+  }
   return SOD_OK;
 }
 

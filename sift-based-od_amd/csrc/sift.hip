@@ -2109,6 +2109,7 @@ int sod_sift_to_queries(sod_ctx* ctx) {
   ctx->winn = -1;
   ctx->n_qimg = 0;
   ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
+  ++ctx->res_epoch;   // staged results (sod_results_fetch) are stale now
   const int nimg = (int)W->shapes.size() / 2;
   if (nimg > 1) {
     std::vector<int32_t> off(W->off.begin(), W->off.end());

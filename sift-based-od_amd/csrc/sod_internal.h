@@ -221,6 +221,11 @@ struct sod_ctx {
   uint8_t* hres = nullptr;      // page-locked host buffer the staging kernel writes into
   size_t hres_n = 0;
   ResHost res;                  // host-side outputs (decoded keys, votes, post-processing)
+  // staged results still current: set by a staging pipeline enqueue or a fetch; every API
+  // call that can change results bumps res_epoch (set_dev, the SIFT query hand-over)
+  uint64_t res_epoch = 0, staged_epoch = ~0ull;
+  int staged_parts = 0;
+  ResLayout staged_L;
 
   // ---- SIFT on the device (sift.hip) ----
   SiftWork* sift = nullptr;

@@ -345,9 +345,13 @@ class Main:
         post-processing clusters / final poses).  When OpenCV's float order is not provably
         the squared-distance order (distances reaching 2048: not SIFT input), the stages are
         enqueued one by one with the float-order trainIdx in between (``run_matcher``)."""
+        parts = ("match", "valid") + (("affine",) if run_affine else ()) + \
+            (("post",) if post_process else ())
         if self._exact_order():
+            # results staged right behind the pipeline: the read below only waits
             self.ctx.pipeline(self.rgb_query.shape, bins, ratio, vote_threshold,
-                              affine_threshold, POS_FACTOR * 4.0, POS_FACTOR * 4.0, run_affine)
+                              affine_threshold, POS_FACTOR * 4.0, POS_FACTOR * 4.0, run_affine,
+                              stage=parts)
         else:
             self.ctx.match()
             self.ctx.ratio(ratio)
@@ -358,8 +362,7 @@ class Main:
                 self.ctx.affine(self.image_query_size, POS_FACTOR * 4.0, POS_FACTOR * 4.0,
                                 affine_threshold)
         # every result in one device -> host transfer and one wait (sod_results_fetch)
-        r = self.ctx.results(parts=("match", "valid") + (("affine",) if run_affine else ())
-                             + (("post",) if post_process else ()))
+        r = self.ctx.results(parts=parts)
         idx1, d1, d2, good = r["match"]
         out = {"idx1": idx1, "d1": d1, "d2": d2, "good": good, "valid": r["valid"]}
         if run_affine:

@@ -45,12 +45,12 @@ def test_abi_version_without_gpu():
 
 
 def test_pipeline_args_layout():
-    # sod_pipeline_args in sod.h: double, 2 x i32, i32[4], 2 x i32, 2 x double, i32
+    # sod_pipeline_args in sod.h: double, 2 x i32, i32[4], 2 x i32, 2 x double, 2 x i32
     a = _lib.PipelineArgs
     assert a.ratio.offset == 0
     assert a.query_h.offset == 8 and a.bins.offset == 16
     assert a.vote_threshold.offset == 32 and a.x_factor.offset == 40
-    assert a.run_affine.offset == 56 and ctypes.sizeof(a) == 64
+    assert a.run_affine.offset == 56 and a.stage_parts.offset == 60 and ctypes.sizeof(a) == 64
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):

@@ -582,10 +582,24 @@ def test_fused_pipeline_equals_dense(ctx, nq, thr, n_objects, decoy):
     # affine pass and without it (post-processing then over every valid bin: thousands at
     # thr 1, past the staging kernel's 1 024 relation rows -> its host-relations path)
     for run_affine in (True, False):
-        ctx.upload_queries(qs.des, qs.kp)
-        ctx.pipeline(qs.shape, (32, 32, 8, 12), ratio=0.75, vote_threshold=thr, affine_threshold=4,
-                     run_affine=run_affine)
-        _results_equal_getters(ctx, run_affine)
+        for stage in ((), ("match", "valid", "affine", "post")):
+            ctx.upload_queries(qs.des, qs.kp)
+            ctx.pipeline(qs.shape, (32, 32, 8, 12), ratio=0.75, vote_threshold=thr,
+                         affine_threshold=4, run_affine=run_affine, stage=stage)
+            _results_equal_getters(ctx, run_affine)
+    # staged behind the pipeline, then the selection redone at another threshold: the fetch
+    # must not hand back the staged (older) bins
+    ctx.upload_queries(qs.des, qs.kp)
+    ctx.pipeline(qs.shape, (32, 32, 8, 12), ratio=0.75, vote_threshold=thr, affine_threshold=4,
+                 stage=("match", "valid", "affine", "post"))
+    ctx.select(thr + 1)
+    r = ctx.results(parts=("valid",))
+    v = ctx.valid_result()
+    for k in ("keys", "votes", "offsets", "members", "means"):
+        assert np.array_equal(r["valid"][k], v[k]), k
+    r2 = ctx.results(parts=("valid",))               # (a second read of the same staging)
+    for k in ("keys", "votes", "offsets", "members", "means"):
+        assert np.array_equal(r2["valid"][k], v[k]), k
 
 
 def _results_equal_getters(ctx, affined=True):
