@@ -254,6 +254,9 @@ constexpr int gwords() { return SOD_I8_SLOTS && QT <= 4 ? kThrWords : 1; }
 #ifndef SOD_I8_SEEDSUB
 #define SOD_I8_SEEDSUB SPS // subtiles of the first stage the seed pass covers
 #endif
+#ifndef SOD_I8_SEEDSUB_QT2
+#define SOD_I8_SEEDSUB_QT2 16   // ... at 2 query tiles per wave (one query image; round 5)
+#endif
 #ifndef SOD_I8_SEEDPUB
 #define SOD_I8_SEEDPUB 1   // publish the seed thresholds to the other chunks right away
 #endif
@@ -610,7 +613,7 @@ __device__ __forceinline__ void match_unit(
 #pragma unroll
       for (int t = 0; t < QT; ++t) sm[t] = INT_MIN;
 #pragma unroll 1
-      for (int u = 0; u < SOD_I8_SEEDSUB; ++u) {
+      for (int u = 0; u < (QT <= 2 ? SOD_I8_SEEDSUB_QT2 : SOD_I8_SEEDSUB); ++u) {
         const uint8_t* nb = sb + u * kSub + lane * 16;
         const i32x4 a0 = *reinterpret_cast<const i32x4*>(nb);
         const i32x4 a1 = *reinterpret_cast<const i32x4*>(nb + 1024);
