@@ -1306,7 +1306,8 @@ int launch_match_i8(sod_ctx* ctx) {
   // one query image (<= 32 query tiles): 4 tiles per wave in two halves over the stage's
   // subtiles (match_unit, H = 2) instead of 2 tiles per wave (option match_halves)
   int H = 1;
-  if (!wide && ctx->opt.match_halves && ctx->opt.match_qt == 0 && ctx->nqt <= 32) {
+  if (!wide && ctx->opt.match_halves && ctx->opt.match_qt == 0 && ctx->nqt <= 32 &&
+      !sod_match_use_s(ctx)) {
     qt = 4;
     H = 2;
   }
