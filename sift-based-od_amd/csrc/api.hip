@@ -316,7 +316,6 @@ struct OptEntry {
 const OptEntry kOpts[] = {
     {"match_qt", &sod_opts::match_qt},
     {"match_pf", &sod_opts::match_pf},
-    {"match_halves", &sod_opts::match_halves},
     {"hough_fused", &sod_opts::hough_fused},
     {"select_multi", &sod_opts::select_multi},
     {"sift_stream_mask", &sod_opts::sift_stream_mask},

@@ -475,23 +475,14 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
 // PF = subtiles whose A fragments / norm words are read from LDS ahead of their MFMAs: 1
 // hides the LDS latency behind one subtile's MFMAs, which at 2-4 query tiles per wave (8-16
 // MFMAs per wave and subtile) is too short
-// H = 2 (one query image): the work-group's waves form two halves over the same queries,
-// each half taking every other subtile of a stage -- every A fragment read from LDS feeds
-// 2 QT MFMAs of 4 waves instead of 8 waves, and each half writes its own partial top-2
-// (slot 2 sp + half), which the merge reduces with the other chunks' (round 5)
-template <int QT, int PF, int H>
+template <int QT, int PF>
 __device__ __forceinline__ void match_unit(
     uint8_t* lds, int sp, int qb, const uint8_t* __restrict__ dbpack, const int* __restrict__ dn,
     int64_t nsub, const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt,
     int64_t nq_pad, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2, int* __restrict__ gthr, int seedload) {
-  static_assert(H == 1 || H == 2, "one or two halves");
-  constexpr int NQW = NW16 / H;   // query waves of the work-group
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wvh = __builtin_amdgcn_readfirstlane(wave);
-  // (H = 1: the round-4 kernel exactly -- half a compile-time 0)
-  const int qwave = H == 1 ? wvh : wvh % NQW, half = H == 1 ? 0 : wvh / NQW;
-  const int qt0 = (qb * NQW + qwave) * QT;
+  const int qt0 = (qb * NW16 + wave) * QT;
 #ifdef SOD_I8_TIME
   const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -550,8 +541,8 @@ __device__ __forceinline__ void match_unit(
   // times the exchange loads (gwords<QT>).
   constexpr bool kSlots = gwords<QT>() > 1;
   const int wq = __builtin_amdgcn_readfirstlane(wave);
-  const int ntile = max(0, min(QT, nqt - qt0));   // real tiles of the wave
-  const int64_t qw0 = (int64_t)qt0 * 16;          // the wave's first query
+  const int ntile = max(0, min(QT, nqt - (qb * NW16 + wq) * QT));   // real tiles of the wave
+  const int64_t qw0 = (int64_t)(qb * NW16 + wq) * QT * 16;   // the wave's first query
   int* const gw = gthr + qw0;
   // one descriptor over the three words of the slot (a padding tile's load reads the next
   // queries' words or, past the end, 0; its bound is never used)
@@ -559,8 +550,7 @@ __device__ __forceinline__ void match_unit(
       (void*)gthr, (short)0, (int)(kThrWords * nq_pad * 4), kRsrcWord3);
   uint8_t* const gl =
       lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64 * gwords<QT>());
-  // this chunk's best-row word (halves count as chunks of their own: distinct rows)
-  [[maybe_unused]] const int oslot = 1 + ((sp * H + half) & 1);
+  [[maybe_unused]] const int oslot = 1 + (sp & 1);   // this chunk's best-row word
 #endif
 #if SOD_I8_PIPE
   // accumulators, norms and first row of the subtile whose prefilter is pending; the
@@ -623,8 +613,7 @@ __device__ __forceinline__ void match_unit(
 #pragma unroll
       for (int t = 0; t < QT; ++t) sm[t] = INT_MIN;
 #pragma unroll 1
-      for (int i = 0; i < (QT <= 2 ? SOD_I8_SEEDSUB_QT2 : SOD_I8_SEEDSUB) / H; ++i) {
-        const int u = H * i + half;
+      for (int u = 0; u < (QT <= 2 ? SOD_I8_SEEDSUB_QT2 : SOD_I8_SEEDSUB); ++u) {
         const uint8_t* nb = sb + u * kSub + lane * 16;
         const i32x4 a0 = *reinterpret_cast<const i32x4*>(nb);
         const i32x4 a1 = *reinterpret_cast<const i32x4*>(nb + 1024);
@@ -692,12 +681,11 @@ __device__ __forceinline__ void match_unit(
 #endif
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
-      const int uj = H * j + half;
-      fa0[j] = *reinterpret_cast<const i32x4*>(sb + uj * kSub + lane * 16);
-      fa1[j] = *reinterpret_cast<const i32x4*>(sb + uj * kSub + 1024 + lane * 16);
-      fc[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(uj, 0));
+      fa0[j] = *reinterpret_cast<const i32x4*>(sb + j * kSub + lane * 16);
+      fa1[j] = *reinterpret_cast<const i32x4*>(sb + j * kSub + 1024 + lane * 16);
+      fc[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j, 0));
 #if !SOD_I8_LAZYP
-      fp[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(uj, 0) + kParOff);
+      fp[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j, 0) + kParOff);
 #endif
     }
 #if SOD_I8_UNROLL
@@ -705,9 +693,8 @@ __device__ __forceinline__ void match_unit(
 #else
 #pragma clang loop unroll(full)
 #endif
-    for (int i = 0; i < SPS / H; ++i) {
-      const int u = H * i + half;   // the subtile (i: the wave's step, a constant after unrolling)
-      const int js = i % PF;
+    for (int u = 0; u < SPS; ++u) {
+      const int js = u % PF;   // a constant after unrolling
       const i32x4 a0 = fa0[js], a1 = fa1[js], c = fc[js];   // c = floor(-||d'||^2 / 2)
 #if SOD_I8_LAZYP
       const uint8_t* p = nb0 + norm_off(u, 0) + kParOff;   // norm_off(u, g) = norm_off(u, 0) + 16 g
@@ -720,19 +707,19 @@ __device__ __forceinline__ void match_unit(
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq[t][0], c, 0, 0, 0);
 #if SOD_I8_DMA
       // piece u of the next stage (wave-uniform branch; u is a constant after unrolling)
-      const bool piece_here = i < kPiecesPerWave;
+      const bool piece_here = u < kPiecesPerWave;
       if (piece_here)
-        issue_piece(rs, refill + i * 1024, refill_off + i * 1024, lane);
+        issue_piece(rs, refill + u * 1024, refill_off + u * 1024, lane);
 #else
       const bool piece_here = false;
 #endif
-      if (i + PF < SPS / H) {   // the wave's step i + PF: its fragments in flight
-        const uint8_t* nb = sb + (u + H * PF) * kSub + lane * 16;
+      if (u + PF < SPS) {   // subtile u + PF's fragments in flight
+        const uint8_t* nb = sb + (u + PF) * kSub + lane * 16;
         fa0[js] = *reinterpret_cast<const i32x4*>(nb);
         fa1[js] = *reinterpret_cast<const i32x4*>(nb + 1024);
-        fc[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + H * PF, 0));
+        fc[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF, 0));
 #if !SOD_I8_LAZYP
-        fp[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + H * PF, 0) + kParOff);
+        fp[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF, 0) + kParOff);
 #endif
       }
 #pragma unroll
@@ -742,7 +729,7 @@ __device__ __forceinline__ void match_unit(
 #if SOD_I8_PIPE
       {
         // the pending subtile's index in the chunk decides dense / final / prefilter
-        const int64_t kp = s * SPS + u - H;
+        const int64_t kp = s * SPS + u - 1;
         const int mode = SOD_I8_SEED ? 0 : (kp < kDense - 1 ? 1 : (kp == kDense - 1 ? 2 : 0));
         tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
       }
@@ -757,7 +744,7 @@ __device__ __forceinline__ void match_unit(
       // raises t2 to them
       const bool xstage = kXEvery == 1 || s < kXDense || s % kXEvery == 0;   // wave-uniform
       // the wave's QT x 16 values of each word: QT*4 lanes x 16 B per word
-      if (share_load(H * i) && xstage && lane < QT * 4) {
+      if (share_load(u) && xstage && lane < QT * 4) {
 #pragma unroll
         for (int r = 0; r < gwords<QT>(); ++r)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -765,7 +752,7 @@ __device__ __forceinline__ void match_unit(
               (uint32_t)((qw0 + r * nq_pad) * 4) + (uint32_t)lane * 16u, 0, 0,
               16 /* sc1: past this XCD's L2 */);
       }
-      if (share_apply(H * i) && xstage && (SOD_I8_SHARE2 == 0 || H * i != 12 || s > 0)) {
+      if (share_apply(u) && xstage && (SOD_I8_SHARE2 == 0 || u != 12 || s > 0)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15);
         // publishing is a device-scope atomic per query (a memory-side transaction each):
@@ -831,7 +818,7 @@ __device__ __forceinline__ void match_unit(
     if (lane < 16 && qt < nqt) {
       const int64_t q = (int64_t)qt * 16 + lane;
       const int n2 = qn[q];
-      const int64_t o = (int64_t)(sp * H + half) * nq_pad + q;
+      const int64_t o = (int64_t)sp * nq_pad + q;
       // padding rows only win when the shard has fewer than two real rows: keep them huge
       pd1[o] = y1[t] < -(1 << 29) ? 3.0e38f : (float)(n2 - y1[t]);
       pidx[o] = id[t];
@@ -846,7 +833,7 @@ __device__ __forceinline__ void match_unit(
 __device__ unsigned long long g_stamps[4096][8];
 #endif
 
-template <int QT, int PF, int H>
+template <int QT, int PF>
 __global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
@@ -868,10 +855,10 @@ __global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
   // instead of all of them (bijective for any grid size; cdna_hip_programming.md T1)
   const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = blockIdx.x % 8;
   const unsigned u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blockIdx.x / 8;
-  match_unit<QT, PF, H>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
+  match_unit<QT, PF>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
              sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
 #else
-  match_unit<QT, PF, H>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
+  match_unit<QT, PF>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
              nq_pad, sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
 #endif
 #ifdef SOD_I8_STAMP
@@ -1302,16 +1289,8 @@ int launch_match_i8(sod_ctx* ctx) {
   const bool wide = ctx->impl == 2;
   const int rows = wide ? 32 : kSubRows;
   const int sps = wide ? w::SPS : SPS;
-  int qt = wide ? w::QT : pick_qt(ctx, ctx->nqt);
-  // one query image (<= 32 query tiles): 4 tiles per wave in two halves over the stage's
-  // subtiles (match_unit, H = 2) instead of 2 tiles per wave (option match_halves)
-  int H = 1;
-  if (!wide && ctx->opt.match_halves && ctx->opt.match_qt == 0 && ctx->nqt <= 32 &&
-      !sod_match_use_s(ctx)) {
-    qt = 4;
-    H = 2;
-  }
-  const int qt_per_wg = wide ? w::NW * w::QT : NW16 * qt / H;
+  const int qt = wide ? w::QT : pick_qt(ctx, ctx->nqt);
+  const int qt_per_wg = wide ? w::NW * w::QT : NW16 * qt;
   const int64_t nq_pad = (int64_t)ctx->nqt * rows;
   const int64_t qblocks = cdiv(ctx->nqt, qt_per_wg);
   const int64_t nstages = ctx->nsub / sps;
@@ -1337,7 +1316,7 @@ int launch_match_i8(sod_ctx* ctx) {
   hipStream_t ks;   // context stream, or the matcher's (sod_match_set_overlap)
   float *pd1, *pd2;
   int32_t* pidx;
-  SOD_TRY(sod_match_stream_begin(ctx, split * H * nq_pad, &ks, &pd1, &pidx, &pd2));
+  SOD_TRY(sod_match_stream_begin(ctx, split * nq_pad, &ks, &pd1, &pidx, &pd2));
   // shared thresholds, one array per partial-result slot: "nothing known" is bytes 0x80 (below
   // every reachable t2); the merge that releases a slot resets its array for the next launch,
   // a new slot layout (query count, kernel shape) resets BOTH slots here (stream_begin waited for both
@@ -1374,28 +1353,26 @@ int launch_match_i8(sod_ctx* ctx) {
                           ctx->nqt, nq_pad, (int)split, st_per_split * sps,
                           (int)ctx->row_offset, pd1, pidx, pd2, (int)qblocks);
   else {
-#define SOD_LAUNCH_I8(Q, P, HH)                                                               \
-  hipExtLaunchKernelGGL((match_i8_kernel<Q, P, HH>), dim3((unsigned)(qblocks * split)), dim3(NT16), 0, \
+#define SOD_LAUNCH_I8(Q, P)                                                                   \
+  hipExtLaunchKernelGGL((match_i8_kernel<Q, P>), dim3((unsigned)(qblocks * split)), dim3(NT16), 0, \
                         ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),  \
                         ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),       \
                         ctx->nqt, nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, \
                         pd1, pidx, pd2, (int)qblocks, gthr, seedload)
     const int pf = pick_pf(ctx, qt);
-    if (H == 2) {
-      SOD_LAUNCH_I8(4, 1, 2);
-    } else if (qt == 8) {
-      if (pf == 2) SOD_LAUNCH_I8(8, 2, 1); else SOD_LAUNCH_I8(8, 1, 1);
+    if (qt == 8) {
+      if (pf == 2) SOD_LAUNCH_I8(8, 2); else SOD_LAUNCH_I8(8, 1);
     } else if (qt == 4) {
-      if (pf == 2) SOD_LAUNCH_I8(4, 2, 1); else SOD_LAUNCH_I8(4, 1, 1);
+      if (pf == 2) SOD_LAUNCH_I8(4, 2); else SOD_LAUNCH_I8(4, 1);
     } else {
-      if (pf == 2) SOD_LAUNCH_I8(2, 2, 1); else SOD_LAUNCH_I8(2, 1, 1);
+      if (pf == 2) SOD_LAUNCH_I8(2, 2); else SOD_LAUNCH_I8(2, 1);
     }
 #undef SOD_LAUNCH_I8
   }
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(sod_match_stream_end(ctx, ee));
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, false));
-  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)(split * H), nq_pad, gthr,
+  SOD_TRY(launch_merge(ctx, pd1, pidx, pd2, (int)split, nq_pad, gthr,
                        ctx->nranks <= 1 && !ctx->comm));   // no exchange follows: final
   SOD_TRY(sod_stage_mark(ctx, kStageMerge, true));
   return sod_partials_merged(ctx);   // the slot is free again
