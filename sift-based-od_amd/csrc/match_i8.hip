@@ -834,7 +834,13 @@ __device__ unsigned long long g_stamps[4096][8];
 #endif
 
 template <int QT, int PF>
-__global__ __launch_bounds__(NT16, 1) void match_i8_kernel(
+#ifndef SOD_I8_MINB
+#define SOD_I8_MINB 1      // work-groups per CU the register allocation must allow
+#endif
+#ifndef SOD_I8_QT2_WGS
+#define SOD_I8_QT2_WGS 1   // work-groups per CU at 2 query tiles per wave (LDS permitting)
+#endif
+__global__ __launch_bounds__(NT16, SOD_I8_MINB) void match_i8_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
     int split, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
@@ -1296,7 +1302,8 @@ int launch_match_i8(sod_ctx* ctx) {
   const int64_t nstages = ctx->nsub / sps;
   // one round of work-groups (8 waves per CU): as few DB chunks as fill the chip (every chunk
   // restarts each query's running top-2, so more chunks mean more slow-path updates)
-  const int64_t slots = ((wide ? w::NW : NW16) == 4 ? 2LL : 1LL) * ctx->match_cus();   // in flight
+  const int64_t slots = ((wide ? w::NW : NW16) == 4 ? 2LL : 1LL) *
+                        (!wide && qt == 2 ? SOD_I8_QT2_WGS : 1) * ctx->match_cus();   // in flight
   // (rounded down: one work-group more than the slots would run as a second round)
   int64_t split = std::max<int64_t>(1, slots / qblocks);
   split = std::min<int64_t>(split, nstages);
