@@ -1202,8 +1202,9 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   const bool wide = ctx->impl == 2;
   const int rows = wide ? 32 : kSubRows;            // rows per subtile / queries per tile
   const int sub_bytes = wide ? w::kSub : kSub;
-  // DB padded to whole stages of both layouts (kStageRows and the 128-row wide stage)
-  const int64_t spad = std::max(kStageRows, 128);
+  // DB padded to whole stages of both layouts (kStageRows and the wide kernel's stage of
+  // w::SPS 32-row subtiles: 512 rows -- equal to kStageRows at the default 32 subtiles)
+  const int64_t spad = std::max<int64_t>(kStageRows, (int64_t)w::SPS * 32);
   const int64_t npad = db ? cdiv(n, spad) * spad : cdiv(n, rows) * rows;
   uint8_t* pack;
   int* norms;
