@@ -157,7 +157,7 @@ int sod_trig_exact(sod_ctx* ctx);
 int sod_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double* c);
 /* Tuning / test switches of this context, by name (integers; read at the next enqueue).
  * sod_create seeds each from the environment variable SOD_<NAME> once.  Names: match_qt,
- * match_pf (LDS-ring matcher tiles per wave / prefetch), hough_fused (0: never the
+ * match_pf, match_pair (LDS-ring matcher tiles per wave / prefetch / waves per query slice), hough_fused (0: never the
  * one-work-group Hough kernel), select_multi (1: multi-kernel selection for small windows),
  * sift_stream_mask, sift_sort_max, sift_desc_range_max, sift_layer_split, sift_side_mask,
  * sift_fork2, sift_early_desc, sift_direct, sift_eager_rank (SIFT scheduling A/B and the

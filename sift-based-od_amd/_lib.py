@@ -363,7 +363,7 @@ class Context:
 
     KERNELS = {"auto": 0, "ring": 1, "streamed": 2}
 
-    OPTIONS = ("match_qt", "match_pf", "hough_fused", "select_multi", "sift_stream_mask",
+    OPTIONS = ("match_qt", "match_pf", "match_pair", "hough_fused", "select_multi", "sift_stream_mask",
                "sift_sort_max", "sift_desc_range_max", "sift_layer_split", "sift_side_mask",
                "sift_fork2", "sift_early_desc", "sift_direct", "sift_eager_rank", "debug_sync",
                "affine_fma")

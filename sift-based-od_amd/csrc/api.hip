@@ -316,6 +316,7 @@ struct OptEntry {
 const OptEntry kOpts[] = {
     {"match_qt", &sod_opts::match_qt},
     {"match_pf", &sod_opts::match_pf},
+    {"match_pair", &sod_opts::match_pair},
     {"hough_fused", &sod_opts::hough_fused},
     {"select_multi", &sod_opts::select_multi},
     {"sift_stream_mask", &sod_opts::sift_stream_mask},

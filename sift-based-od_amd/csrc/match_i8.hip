@@ -205,6 +205,32 @@ __device__ __forceinline__ int norm_off(int u, int g) {
   return (row / kNormRows) * (8 * kNormRows) + (row % kNormRows) * 4;
 }
 
+#ifndef SOD_I8_ASMLDS
+// 1: the ring's fragment / c reads as ds_read_b128 in inline asm with counted waits of our
+// own.  The compiler tracks the LDS-DMA refill as an LDS event of another kind, so it can
+// only drain the LDS counter completely before the first use of any read (lgkmcnt(0) at
+// every subtile, the reads for the subtiles ahead included): prefetching further ahead
+// gained nothing.  LDS returns in order, the refill counts on vmcnt only, so waiting for
+// all but the reads issued after a subtile's own is exact.  2: at <= 2 query tiles per wave
+// (one image: -4 %; C2 at 4 tiles +3 %, C3 at 8 +0.3 %, round 5)
+#define SOD_I8_ASMLDS 2
+#endif
+// LDS byte address of a pointer into the work-group's LDS
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+// ds_read_b128 at a base address + an immediate offset (a constant after unrolling)
+__device__ __forceinline__ i32x4 lds_read16(uint32_t base, int off) {
+  i32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(off));
+  return v;
+}
+// wait until at most n LDS operations are outstanding; a, b, c are then ready (tied, so no
+// use of them is scheduled before the wait)
+__device__ __forceinline__ void lds_wait3(i32x4& a, i32x4& b, i32x4& c, int n) {
+  asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "i"(n));
+}
+
 // median of three (v_med3_i32): with y1 >= y2, med3(y1, y, y2) is the new second best
 __device__ __forceinline__ int imed3(int a, int b, int c) {
   int r;
@@ -297,6 +323,12 @@ constexpr int kShareAt[2] = {SOD_I8_SHARE_AT};
 __device__ __forceinline__ constexpr bool share_load(int u) { return u == kShareAt[0]; }
 __device__ __forceinline__ constexpr bool share_apply(int u) { return u == kShareAt[1]; }
 #endif
+#ifndef SOD_I8_XWAIT
+// 1: the exchange's apply point waits for the threshold load (vmcnt(0): also for the next
+// stage's refill pieces issued before it); 0: no wait -- the wave's LDS copy starts as
+// "nothing known" and every dword read is the old or the new copy, both valid bounds
+#define SOD_I8_XWAIT 1
+#endif
 #ifndef SOD_SHARED_T
 #define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
 #endif
@@ -355,9 +387,11 @@ struct MaxTree {
   }
 };
 
-#ifdef SOD_I8_TIME
-// diagnostic build only: per wave slot, s_memtime cycles inside the slow path and entries;
-// [.][2] whole work unit
+#if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
+// diagnostic builds only: per wave slot, s_memtime cycles.  SOD_I8_TIME: [0] inside the
+// slow path, [1] its entries, [2] the whole work unit.  SOD_I8_TIME2 (no slow-path timer):
+// [0] stage-top waits (vmcnt + barrier), [1] the seed pass, [2] the whole work unit,
+// [3] from the unit's start to the first stage's barrier
 __device__ unsigned long long g_tm[32768][4];
 #endif
 #ifdef SOD_I8_COUNT
@@ -373,7 +407,7 @@ __device__ unsigned long long g_counts[8];
 // mode (wave-uniform): 0 = prefilter; 1 = dense (the chunk's first subtiles, where
 // t2 is still -inf and every tile takes the exact update: the threshold exchange is
 // skipped); 2 = the last dense subtile (the exchange then sets every tile's t2).
-template <int QT>
+template <int QT, bool kAsm>
 __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin, int rowb,
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
                                             int (&id)[QT], bool early = false, int mode = 0,
@@ -393,7 +427,8 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
   for (int i = 0; i < 2 * QT; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);                            // MFMA
     if (i < 3 * QT / 2) __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);       // VALU
-    if (i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+    if (!kAsm && i >= 1 && i <= 4)
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                        // DS read
     if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);      // refill piece
   }
 #endif
@@ -418,7 +453,15 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
   if (any) {
 #endif
 #if SOD_I8_LAZYP
-    const i32x4 p = *reinterpret_cast<const i32x4*>(pin);
+    i32x4 p;
+    if constexpr (kAsm) {
+      // (an LDS read the compiler tracked here would make it drain the counter before every
+      // later fragment read that reuses its registers)
+      p = lds_read16(lds_addr(pin), 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p));
+    } else {
+      p = *reinterpret_cast<const i32x4*>(pin);
+    }
 #else
     const i32x4 p = pin;
 #endif
@@ -474,17 +517,32 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
 // writing the chunk's partial top-2 of every query to slot sp of pd1/pidx/pd2.
 // PF = subtiles whose A fragments / norm words are read from LDS ahead of their MFMAs: 1
 // hides the LDS latency behind one subtile's MFMAs, which at 2-4 query tiles per wave (8-16
-// MFMAs per wave and subtile) is too short
-template <int QT, int PF>
+// MFMAs per wave and subtile) is too short.
+// PAIR = waves per query slice: with 2, waves w and w + NW16/2 (the same SIMD) hold the same
+// queries and take the even / odd subtiles of every stage, so each 2 KiB subtile is read
+// from LDS by half the waves for twice the MFMAs (small query sets, where the 8 waves'
+// fragment reads keep the LDS array busy most of the MFMA time); their two partial top-2
+// lists merge through LDS at the end.
+template <int QT, int PF, int PAIR>
 __device__ __forceinline__ void match_unit(
     uint8_t* lds, int sp, int qb, const uint8_t* __restrict__ dbpack, const int* __restrict__ dn,
     int64_t nsub, const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt,
     int64_t nq_pad, int64_t sub_per_split, int row_offset, float* __restrict__ pd1,
     int* __restrict__ pidx, float* __restrict__ pd2, int* __restrict__ gthr, int seedload) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qt0 = (qb * NW16 + wave) * QT;
-#ifdef SOD_I8_TIME
+  constexpr int NQW = NW16 / PAIR;                  // query slices per work-group
+  constexpr int SUBS = SPS / PAIR;                  // subtiles per stage and wave
+  static_assert(PAIR == 1 || (PAIR == 2 && kNormRows % 32 == 0 && kShareAt[0] % 2 == 0 &&
+                              kShareAt[1] % 2 == 0 && kPiecesPerWave <= SUBS),
+                "paired waves: odd subtiles sit 64 B after the even ones in the norm ring");
+  const int qwave = wave % NQW, par = wave / NQW;   // query slice, subtile phase
+  constexpr bool kAsm = SOD_I8_ASMLDS == 1 || (SOD_I8_ASMLDS == 2 && QT <= 2);
+  const int qt0 = (qb * NQW + qwave) * QT;
+#if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
   const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef SOD_I8_TIME2
+  unsigned long long tw_sum = 0, tw_seed = 0, tw_pro = 0;
 #endif
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
@@ -521,7 +579,7 @@ __device__ __forceinline__ void match_unit(
     t2[t] = INT_MIN >> 1;
     id[t] = 0x7fffffff;
   }
-  const int rowl = row_offset + (int)(s_lo * kSubRows) + (lane >> 4) * 4;
+  const int rowl = row_offset + (int)(s_lo * kSubRows) + (lane >> 4) * 4 + par * kSubRows;
 #if SOD_I8_XCHUNK
   // Chunks of the same queries share their prefilter thresholds: gthr[q] = max over chunks of
   // the t2 (= query-wide second best >> 1) they published.  A chunk holding t2 has two rows
@@ -539,18 +597,24 @@ __device__ __forceinline__ void match_unit(
   // Layout: gthr[r * nq_pad + q], r = 0: t2, 1: even best, 2: odd best (h units).  The
   // kernel at 8 query tiles per wave (C3) leaves the slots out: no time gained there, three
   // times the exchange loads (gwords<QT>).
-  constexpr bool kSlots = gwords<QT>() > 1;
+  constexpr int GW = gwords<QT / PAIR>();
+  constexpr bool kSlots = GW > 1;
   const int wq = __builtin_amdgcn_readfirstlane(wave);
-  const int ntile = max(0, min(QT, nqt - (qb * NW16 + wq) * QT));   // real tiles of the wave
-  const int64_t qw0 = (int64_t)(qb * NW16 + wq) * QT * 16;   // the wave's first query
+  const int qwq = wq % NQW;
+  const int ntile = max(0, min(QT, nqt - (qb * NQW + qwq) * QT));   // real tiles of the wave
+  const int64_t qw0 = (int64_t)(qb * NQW + qwq) * QT * 16;   // the wave's first query
   int* const gw = gthr + qw0;
   // one descriptor over the three words of the slot (a padding tile's load reads the next
   // queries' words or, past the end, 0; its bound is never used)
   const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
       (void*)gthr, (short)0, (int)(kThrWords * nq_pad * 4), kRsrcWord3);
   uint8_t* const gl =
-      lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64 * gwords<QT>());
+      lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64 * GW);
   [[maybe_unused]] const int oslot = 1 + (sp & 1);   // this chunk's best-row word
+#if !SOD_I8_XWAIT
+  for (int i = lane; i < QT * 16 * GW; i += 64) reinterpret_cast<int*>(gl)[i] = INT_MIN;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // before the first threshold DMA
+#endif
 #endif
 #if SOD_I8_PIPE
   // accumulators, norms and first row of the subtile whose prefilter is pending; the
@@ -568,6 +632,9 @@ __device__ __forceinline__ void match_unit(
 
   int slot = 0;
   for (int64_t s = 0; s < nst; ++s) {
+#ifdef SOD_I8_TIME2
+    const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
+#endif
     // the wave's loads of stage s are complete when at most the later prefetched stages'
     // loads remain in flight (vector memory returns in order)
     const int64_t younger = min<int64_t>(kRing - 2, nst - 1 - s);   // stages issued after s
@@ -578,6 +645,11 @@ __device__ __forceinline__ void match_unit(
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+#ifdef SOD_I8_TIME2
+    const unsigned long long tw1 = __builtin_amdgcn_s_memtime();
+    tw_sum += tw1 - tw0;
+    if (s == 0) tw_pro = tw1 - tu0;
+#endif
     // every wave has finished stage s-1, so its slot takes stage s+kRing-1
 #if SOD_I8_DMA
     // (descriptor pieces spread over this stage's first subtiles below; norms now)
@@ -597,8 +669,10 @@ __device__ __forceinline__ void match_unit(
                   nring + ((s + kRing - 1) % kNormRing) * kStageNorm, wave, lane);
     }
 #endif
-    const uint8_t* sb = lds + slot * kStageBytes;
-    const uint8_t* nb0 = nring + (s % kNormRing) * kStageNorm + norm_off(0, lane >> 4);
+    // (the wave's subtile phase folded in: subtile u of the wave is u * PAIR + par)
+    const uint8_t* sb = lds + slot * kStageBytes + par * kSub;
+    const uint8_t* nb0 =
+        nring + (s % kNormRing) * kStageNorm + norm_off(0, lane >> 4) + par * (kSubRows * 4);
 #if SOD_I8_SEED
     if (s == 0) {
       // Seed pass: the chunk's first stage through the MFMAs once with no top-2 work, only a
@@ -613,7 +687,7 @@ __device__ __forceinline__ void match_unit(
 #pragma unroll
       for (int t = 0; t < QT; ++t) sm[t] = INT_MIN;
 #pragma unroll 1
-      for (int u = 0; u < (QT <= 2 ? SOD_I8_SEEDSUB_QT2 : SOD_I8_SEEDSUB); ++u) {
+      for (int u = 0; u < (QT / PAIR <= 2 ? SOD_I8_SEEDSUB_QT2 : SOD_I8_SEEDSUB); u += PAIR) {
         const uint8_t* nb = sb + u * kSub + lane * 16;
         const i32x4 a0 = *reinterpret_cast<const i32x4*>(nb);
         const i32x4 a1 = *reinterpret_cast<const i32x4*>(nb + 1024);
@@ -651,12 +725,12 @@ __device__ __forceinline__ void match_unit(
       // than it saves when the DB stream dominates (many chunks of few queries: 500 x 1M,
       // 124 chunks, 0.078 vs 0.070 ms), so the launch enables it up to 64 chunks only, and
       // the one-image kernel (QT 2) does not carry the code (its mere presence cost 2-3 %)
-      if (QT >= 4 && seedload) {
+      if (QT / PAIR >= 4 && seedload) {
         int gq[QT][kThrWords];
 #pragma unroll
         for (int t = 0; t < QT; ++t)   // one load per query (lanes 0-15), then to its groups
 #pragma unroll
-          for (int r = 0; r < gwords<QT>(); ++r)
+          for (int r = 0; r < GW; ++r)
             gq[t][r] = lane < 16 && t < ntile
                            ? __hip_atomic_load(gw + r * nq_pad + 16 * t + lane,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -672,6 +746,10 @@ __device__ __forceinline__ void match_unit(
         }
       }
 #endif
+#ifdef SOD_I8_TIME2
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      tw_seed = __builtin_amdgcn_s_memtime() - tw1;
+#endif
     }
 #endif
     slot = slot + 1 == kRing ? 0 : slot + 1;
@@ -679,22 +757,36 @@ __device__ __forceinline__ void match_unit(
 #if !SOD_I8_LAZYP
     i32x4 fp[PF];
 #endif
+    static_assert(!kAsm || SOD_I8_LAZYP, "asm reads: the parity words stay on the slow path");
+    [[maybe_unused]] const uint32_t sbl = lds_addr(sb) + lane * 16, nbl = lds_addr(nb0);
+    if constexpr (kAsm) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        fa0[j] = lds_read16(sbl, j * PAIR * kSub);
+        fa1[j] = lds_read16(sbl, j * PAIR * kSub + 1024);
+        fc[j] = lds_read16(nbl, norm_off(j * PAIR, 0));
+      }
+    } else {
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
-      fa0[j] = *reinterpret_cast<const i32x4*>(sb + j * kSub + lane * 16);
-      fa1[j] = *reinterpret_cast<const i32x4*>(sb + j * kSub + 1024 + lane * 16);
-      fc[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j, 0));
+      fa0[j] = *reinterpret_cast<const i32x4*>(sb + j * PAIR * kSub + lane * 16);
+      fa1[j] = *reinterpret_cast<const i32x4*>(sb + j * PAIR * kSub + 1024 + lane * 16);
+      fc[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j * PAIR, 0));
 #if !SOD_I8_LAZYP
-      fp[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j, 0) + kParOff);
+      fp[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j * PAIR, 0) + kParOff);
 #endif
+    }
     }
 #if SOD_I8_UNROLL
 #pragma unroll SOD_I8_UNROLL
 #else
 #pragma clang loop unroll(full)
 #endif
-    for (int u = 0; u < SPS; ++u) {
-      const int js = u % PF;   // a constant after unrolling
+    for (int ju = 0; ju < SUBS; ++ju) {
+      const int u = ju * PAIR;   // the wave's subtile (plus par, folded into sb / nb0 / rowl)
+      const int js = ju % PF;    // a constant after unrolling
+      // (asm reads) this subtile's three reads done; the subtiles' ahead may be in flight
+      if constexpr (kAsm) lds_wait3(fa0[js], fa1[js], fc[js], 3 * min(PF - 1, SUBS - 1 - ju));
       const i32x4 a0 = fa0[js], a1 = fa1[js], c = fc[js];   // c = floor(-||d'||^2 / 2)
 #if SOD_I8_LAZYP
       const uint8_t* p = nb0 + norm_off(u, 0) + kParOff;   // norm_off(u, g) = norm_off(u, 0) + 16 g
@@ -707,19 +799,24 @@ __device__ __forceinline__ void match_unit(
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq[t][0], c, 0, 0, 0);
 #if SOD_I8_DMA
       // piece u of the next stage (wave-uniform branch; u is a constant after unrolling)
-      const bool piece_here = u < kPiecesPerWave;
+      const bool piece_here = ju < kPiecesPerWave;
       if (piece_here)
-        issue_piece(rs, refill + u * 1024, refill_off + u * 1024, lane);
+        issue_piece(rs, refill + ju * 1024, refill_off + ju * 1024, lane);
 #else
       const bool piece_here = false;
 #endif
-      if (u + PF < SPS) {   // subtile u + PF's fragments in flight
-        const uint8_t* nb = sb + (u + PF) * kSub + lane * 16;
+      if (kAsm && ju + PF < SUBS) {   // the fragments PF subtiles ahead in flight
+        fa0[js] = lds_read16(sbl, (u + PF * PAIR) * kSub);
+        fa1[js] = lds_read16(sbl, (u + PF * PAIR) * kSub + 1024);
+        fc[js] = lds_read16(nbl, norm_off(u + PF * PAIR, 0));
+      }
+      if (!kAsm && ju + PF < SUBS) {
+        const uint8_t* nb = sb + (u + PF * PAIR) * kSub + lane * 16;
         fa0[js] = *reinterpret_cast<const i32x4*>(nb);
         fa1[js] = *reinterpret_cast<const i32x4*>(nb + 1024);
-        fc[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF, 0));
+        fc[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF * PAIR, 0));
 #if !SOD_I8_LAZYP
-        fp[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF, 0) + kParOff);
+        fp[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF * PAIR, 0) + kParOff);
 #endif
       }
 #pragma unroll
@@ -729,9 +826,9 @@ __device__ __forceinline__ void match_unit(
 #if SOD_I8_PIPE
       {
         // the pending subtile's index in the chunk decides dense / final / prefilter
-        const int64_t kp = s * SPS + u - 1;
+        const int64_t kp = s * SPS + u - PAIR;
         const int mode = SOD_I8_SEED ? 0 : (kp < kDense - 1 ? 1 : (kp == kDense - 1 ? 2 : 0));
-        tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
+        tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t) accp[t] = acc[t];
@@ -746,14 +843,16 @@ __device__ __forceinline__ void match_unit(
       // the wave's QT x 16 values of each word: QT*4 lanes x 16 B per word
       if (share_load(u) && xstage && lane < QT * 4) {
 #pragma unroll
-        for (int r = 0; r < gwords<QT>(); ++r)
+        for (int r = 0; r < GW; ++r)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               rg, (lds_void*)(gl + r * QT * 64), 16,
               (uint32_t)((qw0 + r * nq_pad) * 4) + (uint32_t)lane * 16u, 0, 0,
               16 /* sc1: past this XCD's L2 */);
       }
       if (share_apply(u) && xstage && (SOD_I8_SHARE2 == 0 || u != 12 || s > 0)) {
+#if SOD_I8_XWAIT
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15);
         // publishing is a device-scope atomic per query (a memory-side transaction each):
         // every stage while the thresholds still move fast, then every kPublishEvery-th
@@ -789,7 +888,7 @@ __device__ __forceinline__ void match_unit(
       }
 #endif
 #else
-      tile_update<QT>(acc, p, rowb, y1, y2, t2, id);
+      tile_update<QT, kAsm>(acc, p, rowb, y1, y2, t2, id);
 #endif
     }
   }
@@ -797,7 +896,7 @@ __device__ __forceinline__ void match_unit(
   // threshold load) must land before the work-group's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if SOD_I8_PIPE
-  tile_update<QT>(accp, pp, rowp, y1, y2, t2, id, false,
+  tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, false,
                   !SOD_I8_SEED && nst * SPS <= kDense ? 1 : 0);
 #endif
 #ifdef SOD_I8_COUNT
@@ -806,7 +905,35 @@ __device__ __forceinline__ void match_unit(
 #ifdef SOD_I8_TIME
   if (lane == 0) atomicAdd(&g_tm[(blockIdx.x * 8 + wave) & 32767][2], __builtin_amdgcn_s_memtime() - tu0);
 #endif
+#ifdef SOD_I8_TIME2
+  if (lane == 0) {
+    unsigned long long* const g = g_tm[(blockIdx.x * NW16 + wave) & 32767];
+    atomicAdd(&g[0], tw_sum);
+    atomicAdd(&g[1], tw_seed);
+    atomicAdd(&g[2], __builtin_amdgcn_s_memtime() - tu0);
+    atomicAdd(&g[3], tw_pro);
+  }
+#endif
 
+  if constexpr (PAIR == 2) {
+    // the odd-phase wave hands its lanes' top-2 to the even-phase wave of the same queries
+    // (the ring is free: every wave's DMA landed before the barrier, no wave reads it again)
+    __builtin_amdgcn_s_barrier();
+    int* const xl = reinterpret_cast<int*>(lds) + (qwave * QT) * 3 * 64 + lane;
+    if (par == 1) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        xl[(3 * t) * 64] = y1[t];
+        xl[(3 * t + 1) * 64] = id[t];
+        xl[(3 * t + 2) * 64] = y2[t];
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    if (par == 1) return;
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+      merge2i(y1[t], id[t], y2[t], xl[(3 * t) * 64], xl[(3 * t + 1) * 64], xl[(3 * t + 2) * 64]);
+  }
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
 #pragma unroll
@@ -833,7 +960,7 @@ __device__ __forceinline__ void match_unit(
 __device__ unsigned long long g_stamps[4096][8];
 #endif
 
-template <int QT, int PF>
+template <int QT, int PF, int PAIR>
 #ifndef SOD_I8_MINB
 #define SOD_I8_MINB 1      // work-groups per CU the register allocation must allow
 #endif
@@ -847,7 +974,7 @@ __global__ __launch_bounds__(NT16, SOD_I8_MINB) void match_i8_kernel(
     int* __restrict__ pidx, float* __restrict__ pd2, int nqb, int* __restrict__ gthr,
     int seedload) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageBytes + kNormRing * kStageNorm +
-                                                     SOD_I8_XCHUNK * NW16 * QT * 64 * gwords<QT>()];
+                                                     SOD_I8_XCHUNK * NW16 * QT * 64 * gwords<QT / PAIR>()];
 #ifdef SOD_I8_STAMP
   unsigned long long t0 = 0, r0 = 0;
   if (threadIdx.x == 0) {
@@ -861,10 +988,10 @@ __global__ __launch_bounds__(NT16, SOD_I8_MINB) void match_i8_kernel(
   // instead of all of them (bijective for any grid size; cdna_hip_programming.md T1)
   const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = blockIdx.x % 8;
   const unsigned u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blockIdx.x / 8;
-  match_unit<QT, PF>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
+  match_unit<QT, PF, PAIR>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
              sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
 #else
-  match_unit<QT, PF>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
+  match_unit<QT, PF, PAIR>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
              nq_pad, sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
 #endif
 #ifdef SOD_I8_STAMP
@@ -975,6 +1102,7 @@ __device__ __forceinline__ void tile_update_w(const i32x16& acc, const uint8_t* 
   }
 }
 
+template <int QT>   // 32-query tiles per wave (w::QT by default; option match_qt 1 / 2 / 4)
 __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
     const uint8_t* __restrict__ dbpack, const int* __restrict__ dn, int64_t nsub,
     const uint8_t* __restrict__ qpack, const int* __restrict__ qn, int nqt, int64_t nq_pad,
@@ -987,7 +1115,7 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
   const unsigned unit = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + blockIdx.x / 8;
   const int sp = (int)(unit / nqb);
   const int qb = (int)(unit % nqb);
-  const int qt0 = (qb * w::NW + wave) * w::QT;
+  const int qt0 = (qb * w::NW + wave) * QT;
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / w::SPS;
@@ -1001,18 +1129,18 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
       issue_stage_w(dbpack, dn, npad, s_lo + j * w::SPS, lds + j * w::kStageBytes,
                     nring + j * w::kStageNorm, wave, lane);
 
-  i32x4 bq[w::QT][4];
+  i32x4 bq[QT][4];
 #pragma unroll
-  for (int t = 0; t < w::QT; ++t)
+  for (int t = 0; t < QT; ++t)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int qt = qt0 + t;
       bq[t][k] = qt < nqt ? *reinterpret_cast<const i32x4*>(qpack + ((int64_t)qt * 4 + k) * 1024 + lane * 16)
                           : i32x4{0, 0, 0, 0};
     }
-  int y1[w::QT], y2[w::QT], t2[w::QT], id[w::QT];
+  int y1[QT], y2[QT], t2[QT], id[QT];
 #pragma unroll
-  for (int t = 0; t < w::QT; ++t) {
+  for (int t = 0; t < QT; ++t) {
     y1[t] = INT_MIN;
     y2[t] = INT_MIN;
     t2[t] = INT_MIN >> 1;
@@ -1058,7 +1186,7 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
       const int rowb = rowl + (int)((s * w::SPS + u) * 32);
       i32x16 accq;   // the previous tile of this subtile
 #pragma unroll
-      for (int t = 0; t < w::QT; ++t) {
+      for (int t = 0; t < QT; ++t) {
         i32x16 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], bq[t][0], c, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[1], bq[t][1], acc, 0, 0, 0);
         if (t == 0 && u + 1 < w::SPS) {   // next subtile's fragments in flight
@@ -1071,7 +1199,7 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[2], bq[t][2], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[3], bq[t][3], acc, 0, 0, 0);
         if (t == 0)
-          tile_update_w(accp, pp, rowp, y1[w::QT - 1], y2[w::QT - 1], t2[w::QT - 1], id[w::QT - 1]);
+          tile_update_w(accp, pp, rowp, y1[QT - 1], y2[QT - 1], t2[QT - 1], id[QT - 1]);
         else
           tile_update_w(accq, pu, rowb, y1[t - 1], y2[t - 1], t2[t - 1], id[t - 1]);
         accq = acc;
@@ -1081,10 +1209,10 @@ __global__ __launch_bounds__(w::NT) void match_i8w_kernel(
       rowp = rowb;
     }
   }
-  tile_update_w(accp, pp, rowp, y1[w::QT - 1], y2[w::QT - 1], t2[w::QT - 1], id[w::QT - 1]);
+  tile_update_w(accp, pp, rowp, y1[QT - 1], y2[QT - 1], t2[QT - 1], id[QT - 1]);
 
 #pragma unroll
-  for (int t = 0; t < w::QT; ++t) {
+  for (int t = 0; t < QT; ++t) {
     if (y1[t] != INT_MIN) id[t] += 4 * h;   // the lane half's row offset
     const int o1 = __shfl_xor(y1[t], 32), oi = __shfl_xor(id[t], 32), o2 = __shfl_xor(y2[t], 32);
     merge2i(y1[t], id[t], y2[t], o1, oi, o2);
@@ -1239,7 +1367,7 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   return SOD_OK;
 }
 
-#ifdef SOD_I8_TIME
+#if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
 extern "C" int sod_debug_times(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tm), sizeof(g_tm)) != hipSuccess) return 1;
   if (reset) {
@@ -1283,6 +1411,15 @@ static int pick_qt(const sod_ctx* ctx, int32_t nqt) {
   return 2;
 }
 
+// waves per query slice (match_unit's PAIR); option match_pair overrides
+static int pick_pair(const sod_ctx* ctx, int qt) {
+  {
+    const int v = ctx->opt.match_pair;
+    if (v == 1 || (v == 2 && qt >= 4)) return v;
+  }
+  return 1;
+}
+
 // LDS prefetch distance (subtiles) per query tiles per wave; option match_pf overrides
 static int pick_pf(const sod_ctx* ctx, int qt) {
   {
@@ -1296,15 +1433,24 @@ int launch_match_i8(sod_ctx* ctx) {
   const bool wide = ctx->impl == 2;
   const int rows = wide ? 32 : kSubRows;
   const int sps = wide ? w::SPS : SPS;
-  const int qt = wide ? w::QT : pick_qt(ctx, ctx->nqt);
-  const int qt_per_wg = wide ? w::NW * w::QT : NW16 * qt;
+  const int wqt = ctx->opt.match_qt == 1 || ctx->opt.match_qt == 2 ? ctx->opt.match_qt : w::QT;
+  const int qt = wide ? wqt : pick_qt(ctx, ctx->nqt);
+  const int pair = wide ? 1 : pick_pair(ctx, qt);
+  const int qt_per_wg = wide ? w::NW * qt : NW16 / pair * qt;
   const int64_t nq_pad = (int64_t)ctx->nqt * rows;
   const int64_t qblocks = cdiv(ctx->nqt, qt_per_wg);
   const int64_t nstages = ctx->nsub / sps;
   // one round of work-groups (8 waves per CU): as few DB chunks as fill the chip (every chunk
   // restarts each query's running top-2, so more chunks mean more slow-path updates)
-  const int64_t slots = ((wide ? w::NW : NW16) == 4 ? 2LL : 1LL) *
-                        (!wide && qt == 2 ? SOD_I8_QT2_WGS : 1) * ctx->match_cus();   // in flight
+  // (work-groups per CU: as many as asked for and the LDS holds -- the ring kernel's 128 KiB
+  // ring leaves room for one, whatever its wave count)
+  const int64_t lds_wg = kRing * kStageBytes + kNormRing * kStageNorm +
+                         (int64_t)SOD_I8_XCHUNK * NW16 * qt * 64 * kThrWords;   // (at most)
+  const int64_t per_cu = wide ? ((w::NW == 4) ? 2 : 1)
+                              : std::max<int64_t>(1, std::min<int64_t>(
+                                    (NW16 == 4 ? 2 : 1) * (qt == 2 ? SOD_I8_QT2_WGS : 1),
+                                    (160 * 1024) / lds_wg));
+  const int64_t slots = per_cu * ctx->match_cus();   // in flight
   // (rounded down: one work-group more than the slots would run as a second round)
   int64_t split = std::max<int64_t>(1, slots / qblocks);
   split = std::min<int64_t>(split, nstages);
@@ -1355,25 +1501,32 @@ int launch_match_i8(sod_ctx* ctx) {
   if (use_s)
     SOD_TRY(launch_match_s_kernel(ctx, ks, eb, ee, pd1, pidx, pd2, gthr, split, st_per_split));
   else if (wide)
-    hipExtLaunchKernelGGL(match_i8w_kernel, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0,
-                          ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),
-                          ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),
-                          ctx->nqt, nq_pad, (int)split, st_per_split * sps,
-                          (int)ctx->row_offset, pd1, pidx, pd2, (int)qblocks);
+  {
+#define SOD_LAUNCH_I8W(Q)                                                                     \
+    hipExtLaunchKernelGGL(match_i8w_kernel<Q>, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0, \
+                          ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),  \
+                          ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),       \
+                          ctx->nqt, nq_pad, (int)split, st_per_split * sps,                       \
+                          (int)ctx->row_offset, pd1, pidx, pd2, (int)qblocks)
+    if (qt == 1) SOD_LAUNCH_I8W(1); else if (qt == 2) SOD_LAUNCH_I8W(2); else SOD_LAUNCH_I8W(w::QT);
+#undef SOD_LAUNCH_I8W
+  }
   else {
-#define SOD_LAUNCH_I8(Q, P)                                                                   \
-  hipExtLaunchKernelGGL((match_i8_kernel<Q, P>), dim3((unsigned)(qblocks * split)), dim3(NT16), 0, \
+#define SOD_LAUNCH_I8(Q, P, R)                                                                \
+  hipExtLaunchKernelGGL((match_i8_kernel<Q, P, R>), dim3((unsigned)(qblocks * split)), dim3(NT16), 0, \
                         ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),  \
                         ctx->nsub, ctx->qpack.p, reinterpret_cast<const int*>(ctx->qn.p),       \
                         ctx->nqt, nq_pad, (int)split, st_per_split * sps, (int)ctx->row_offset, \
                         pd1, pidx, pd2, (int)qblocks, gthr, seedload)
     const int pf = pick_pf(ctx, qt);
-    if (qt == 8) {
-      if (pf == 2) SOD_LAUNCH_I8(8, 2); else SOD_LAUNCH_I8(8, 1);
+    if (pair == 2) {   // paired waves: 4 or 8 query tiles per wave, prefetch 1
+      if (qt == 8) SOD_LAUNCH_I8(8, 1, 2); else SOD_LAUNCH_I8(4, 1, 2);
+    } else if (qt == 8) {
+      if (pf == 2) SOD_LAUNCH_I8(8, 2, 1); else SOD_LAUNCH_I8(8, 1, 1);
     } else if (qt == 4) {
-      if (pf == 2) SOD_LAUNCH_I8(4, 2); else SOD_LAUNCH_I8(4, 1);
+      if (pf == 2) SOD_LAUNCH_I8(4, 2, 1); else SOD_LAUNCH_I8(4, 1, 1);
     } else {
-      if (pf == 2) SOD_LAUNCH_I8(2, 2); else SOD_LAUNCH_I8(2, 1);
+      if (pf == 2) SOD_LAUNCH_I8(2, 2, 1); else SOD_LAUNCH_I8(2, 1, 1);
     }
 #undef SOD_LAUNCH_I8
   }

@@ -63,6 +63,7 @@ struct ResHost {
 struct sod_opts {
   int match_qt = 0;            // int8 ring kernel query tiles per wave: 0 by query count; 2, 4, 8
   int match_pf = 0;            // its LDS prefetch distance: 0 default (1); 1, 2
+  int match_pair = 0;          // its waves per query slice: 0 by query count; 1, 2 (4+ tiles)
   int hough_fused = 1;         // 0: never the one-work-group Hough kernel (parity tests)
   int select_multi = 0;        // 1: small windows take the multi-kernel selection too
   int sift_stream_mask = -1;   // -1: only the lone image's slot CU-masked; 0 none; 2 all

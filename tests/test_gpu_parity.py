@@ -131,9 +131,11 @@ def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
     assert np.array_equal(good, orc.ratio_test(f1, f2))
 
 
-@pytest.mark.parametrize("qt", ["2", "4", "8", "streamed"])
+@pytest.mark.parametrize("qt", ["2", "4", "8", "4p", "8p", "w1", "w2", "streamed"])
 def test_matcher_query_tiles_shared_thresholds(ctx, qt):
-    """int8 matcher with each query-tile count per wave (option match_qt; "streamed": the
+    """int8 matcher with each query-tile count per wave (option match_qt; "4p" / "8p": paired
+    waves, option match_pair = 2, each wave of a pair taking every other subtile; "w1" / "w2":
+    the 32x32x32 kernel, impl i8w, at 1 / 2 tiles of 32 queries per wave; "streamed": the
     register-streamed kernel, match_s.hip, whose DB ranges exchange top-2 lists) over a DB split into
     many chunks, so the chunks exchange prefilter thresholds mid-run: DB rows duplicated far
     apart (other chunks) make exact distance ties ACROSS chunks -- a shared threshold must
@@ -142,7 +144,8 @@ def test_matcher_query_tiles_shared_thresholds(ctx, qt):
     if qt == "streamed":
         ctx.set_match_kernel("streamed")
     else:
-        ctx.set_option("match_qt", int(qt))
+        ctx.set_option("match_qt", int(qt.strip("pw")))
+        ctx.set_option("match_pair", 2 if qt.endswith("p") else 1)
     rng = np.random.default_rng(31)
     ndb, nq = 150000, 2000
     db = synthetic.sift_like_descriptors(rng, ndb)
@@ -155,6 +158,11 @@ def test_matcher_query_tiles_shared_thresholds(ctx, qt):
     # mid-DB: the seed equals both winners' value, which must still pass (>=)
     db[1:8] = db[0]
     db[75001:75005] = db[75000]
+    # equal rows in neighbouring subtiles (the two waves of a pair: even / odd subtiles), the
+    # later copy first in its own subtile
+    db[16] = db[0]
+    db[75017] = db[75000]
+    db[75035] = db[75000]
     q[900:950] = db[0]
     q[950:1000] = db[75000]
     # duplicates spread over chunks of both parities (the best-row slots: the even-chunk and
@@ -165,7 +173,7 @@ def test_matcher_query_tiles_shared_thresholds(ctx, qt):
     q[1100:1200] = db[33000:33100]
     q[1200:1300] = np.clip(db[47000:47100].astype(int) + rng.integers(-1, 2, (100, 128)), 0, 255)
     q[1300:1400] = db[61000:61100]
-    ctx.set_impl("i8")
+    ctx.set_impl("i8w" if qt.startswith("w") else "i8")
     ctx.upload_db(db)
     ctx.upload_queries(q)
     for _ in range(2):        # the second launch reuses the reset threshold slot

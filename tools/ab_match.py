@@ -83,6 +83,13 @@ if hasattr(ctx._L, "sod_debug_times"):   # diagnostic build: slow-path cycles pe
     ctx.synchronize()
     ctx._L.sod_debug_times(tm.ctypes.data_as(C.c_void_p), 0)
     cyc, n, tot = tm[:, 0].astype(np.float64), tm[:, 1].astype(np.float64), tm[:, 2].astype(np.float64)
+    if os.environ.get("TIME2"):   # SOD_I8_TIME2 build: stage waits / seed / prologue per wave
+        live = tot > 0
+        med = lambda a: float(np.median(a[live]))  # noqa: E731
+        print("per wave (median cycles): unit %.0f, stage-top waits %.0f (%.1f %%), seed %.0f, "
+              "start to first barrier %.0f" % (med(tot), med(cyc), 100.0 * cyc[live].sum() / tot[live].sum(),
+                                               med(n), med(tm[:, 3].astype(np.float64))), flush=True)
+        cyc = np.zeros(1)
     print("slow path: %.0f cycles per entry, %.2f entries per wave, %.1f %% of the waves' cycles "
           "(work unit median %.0f cycles)" % (cyc.sum() / max(n.sum(), 1), n.sum() / max((tot > 0).sum(), 1),
                                              100.0 * cyc.sum() / max(tot.sum(), 1), np.median(tot[tot > 0])),

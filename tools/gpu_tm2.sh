@@ -1,0 +1,8 @@
+# where a work unit's cycles go (SOD_I8_TIME2 build): stage-top waits, seed, start-up;
+# one image, C2 and C3 shapes
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/tm2; mkdir -p $O
+for a in "500 1000" "10000 100" "50000 1000"; do
+  TIME2=1 SOD_LIB_PATH=tools/variants/libtm2.so timeout -k 10 300 python3 tools/ab_match.py $a i8 > $O/tm2_${a// /_}.log 2>&1 || { tail -5 $O/tm2_${a// /_}.log; exit 1; }
+  grep -E "match|per wave" $O/tm2_${a// /_}.log
+done
