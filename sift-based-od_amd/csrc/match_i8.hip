@@ -390,8 +390,8 @@ struct MaxTree {
 #if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
 // diagnostic builds only: per wave slot, s_memtime cycles.  SOD_I8_TIME: [0] inside the
 // slow path, [1] its entries, [2] the whole work unit.  SOD_I8_TIME2 (no slow-path timer):
-// [0] stage-top waits (vmcnt + barrier), [1] the seed pass, [2] the whole work unit,
-// [3] from the unit's start to the first stage's barrier
+// [0] stage-top waits (vmcnt + barrier), [1] the seed pass (SOD_I8_TIME2=2: the vmcnt part
+// of [0]), [2] the whole work unit, [3] from the unit's start to the first stage's barrier
 __device__ unsigned long long g_tm[32768][4];
 #endif
 #ifdef SOD_I8_COUNT
@@ -542,7 +542,7 @@ __device__ __forceinline__ void match_unit(
   const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
 #endif
 #ifdef SOD_I8_TIME2
-  unsigned long long tw_sum = 0, tw_seed = 0, tw_pro = 0;
+  unsigned long long tw_sum = 0, tw_seed = 0, tw_pro = 0, tw_vm = 0;
 #endif
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
@@ -644,7 +644,12 @@ __device__ __forceinline__ void match_unit(
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLoadsPerStage) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if SOD_I8_TIME2 == 2
+    tw_vm += __builtin_amdgcn_s_memtime() - tw0;   // the wave's own refill pieces
+#endif
+#ifndef SOD_I8_NOBAR   // (diagnostic timing build only: no stage barrier, WRONG results)
     __builtin_amdgcn_s_barrier();
+#endif
 #ifdef SOD_I8_TIME2
     const unsigned long long tw1 = __builtin_amdgcn_s_memtime();
     tw_sum += tw1 - tw0;
@@ -909,7 +914,7 @@ __device__ __forceinline__ void match_unit(
   if (lane == 0) {
     unsigned long long* const g = g_tm[(blockIdx.x * NW16 + wave) & 32767];
     atomicAdd(&g[0], tw_sum);
-    atomicAdd(&g[1], tw_seed);
+    atomicAdd(&g[1], SOD_I8_TIME2 == 2 ? tw_vm : tw_seed);   // (2: the vmcnt part of [0])
     atomicAdd(&g[2], __builtin_amdgcn_s_memtime() - tu0);
     atomicAdd(&g[3], tw_pro);
   }
