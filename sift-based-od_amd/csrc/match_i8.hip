@@ -513,6 +513,98 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
   }
 }
 
+#ifndef SOD_I8_WINQT
+// prefilter windows of two subtiles at up to this many query tiles per wave (0: off): per
+// tile one v_max3 on the window's first subtile, then max3, max3, max and the compare on the
+// second -- 5 VALU and one ballot / branch per two subtiles instead of 6 and two
+#define SOD_I8_WINQT 0
+#endif
+// the window's first subtile: wm = max of three of its four values per tile (the fourth
+// stays in the kept accumulators)
+template <int QT, bool kAsm>
+__device__ __forceinline__ void window_first(const i32x4 (&acc)[QT], int (&wm)[QT], bool vmem) {
+#pragma unroll
+  for (int t = 0; t < QT; ++t) wm[t] = max(max(acc[t][0], acc[t][1]), acc[t][2]);
+#if SOD_I8_SGB
+#pragma unroll
+  for (int i = 0; i < 2 * QT; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);                            // MFMA
+    if (i < QT) __builtin_amdgcn_sched_group_barrier(0x2, 1, 0);                // VALU
+    if (!kAsm && i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);      // refill piece
+  }
+#endif
+}
+// exact top-2 update of one tile's four rows (the slow path's inner loop)
+__device__ __forceinline__ void exact4(const i32x4& a, const i32x4& p, int rowb, int& y1,
+                                       int& y2, int& id) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int y = 2 * a[r] | p[r];
+    const bool gt = y > y1;
+    y2 = imed3(y1, y, y2);
+    id = gt ? rowb + r : id;
+    y1 = gt ? y : y1;
+  }
+}
+template <bool kAsm>
+__device__ __forceinline__ i32x4 parity_words(const uint8_t* pin) {
+  i32x4 p;
+  if constexpr (kAsm) {
+    p = lds_read16(lds_addr(pin), 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p));
+  } else {
+    p = *reinterpret_cast<const i32x4*>(pin);
+  }
+  return p;
+}
+// the window's second subtile: the compare over both subtiles' rows, and on a hit the exact
+// update of the first subtile's rows, then the second's (row order: ties keep the lower row)
+template <int QT, bool kAsm>
+__device__ __forceinline__ void window_second(const i32x4 (&accw)[QT], const uint8_t* pw,
+                                              int roww, const i32x4 (&acc)[QT],
+                                              const uint8_t* pin, int rowb, const int (&wm)[QT],
+                                              int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
+                                              int (&id)[QT], bool vmem) {
+  uint64_t hit[QT];
+  uint64_t any = 0;
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int m = max(max(max(wm[t], accw[t][3]), acc[t][0]),
+                      max(max(acc[t][1], acc[t][2]), acc[t][3]));
+    hit[t] = __builtin_amdgcn_ballot_w64(m >= t2[t]);
+    any |= hit[t];
+  }
+#if SOD_I8_SGB
+#pragma unroll
+  for (int i = 0; i < 2 * QT; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);                            // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);                            // VALU
+    if (!kAsm && i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);      // refill piece
+  }
+#endif
+  if (__builtin_expect(any != 0, 0)) {
+    const i32x4 p0 = parity_words<kAsm>(pw);
+    const i32x4 p1 = parity_words<kAsm>(pin);
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      if (hit[t]) {
+        exact4(accw[t], p0, roww, y1[t], y2[t], id[t]);
+        exact4(acc[t], p1, rowb, y1[t], y2[t], id[t]);
+#if SOD_SHARED_T
+        int g1 = y1[t], g2 = y2[t];
+        top2_xor32(g1, g2);
+        top2_xor16(g1, g2);
+        t2[t] = max(t2[t], g2 >> 1);
+#else
+        t2[t] = max(t2[t], y2[t] >> 1);
+#endif
+      }
+    }
+  }
+}
+
 // One work unit: query block qb (NW16*QT tiles) against DB chunk sp (sub_per_split subtiles),
 // writing the chunk's partial top-2 of every query to slot sp of pd1/pidx/pd2.
 // PF = subtiles whose A fragments / norm words are read from LDS ahead of their MFMAs: 1
@@ -537,6 +629,7 @@ __device__ __forceinline__ void match_unit(
                 "paired waves: odd subtiles sit 64 B after the even ones in the norm ring");
   const int qwave = wave % NQW, par = wave / NQW;   // query slice, subtile phase
   constexpr bool kAsm = SOD_I8_ASMLDS == 1 || (SOD_I8_ASMLDS == 2 && QT <= 2);
+  constexpr bool kWin = SOD_I8_PIPE && SOD_I8_SEED && SOD_I8_LAZYP && QT / PAIR <= SOD_I8_WINQT;
   const int qt0 = (qb * NQW + qwave) * QT;
 #if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
   const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
@@ -628,6 +721,16 @@ __device__ __forceinline__ void match_unit(
   i32x4 pp = {0, 0, 0, 0};
 #endif
   int rowp = 0;
+  // the open window's first subtile (kWin): its accumulators, parity words, rows, partial max
+  [[maybe_unused]] i32x4 accw[QT];
+  [[maybe_unused]] int wm[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    accw[t] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
+    wm[t] = INT_MIN;
+  }
+  [[maybe_unused]] const uint8_t* pw = nring;
+  [[maybe_unused]] int roww = 0;
 #endif
 
   int slot = 0;
@@ -833,7 +936,22 @@ __device__ __forceinline__ void match_unit(
         // the pending subtile's index in the chunk decides dense / final / prefilter
         const int64_t kp = s * SPS + u - PAIR;
         const int mode = SOD_I8_SEED ? 0 : (kp < kDense - 1 ? 1 : (kp == kDense - 1 ? 2 : 0));
-        tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
+        if constexpr (kWin) {
+          // the pending subtile opens a window when it is the stage's even one (stages hold an
+          // even number of the wave's subtiles, so windows never straddle a stage)
+          if (ju % 2 == 1) {
+            window_first<QT, kAsm>(accp, wm, piece_here);
+#pragma unroll
+            for (int t = 0; t < QT; ++t) accw[t] = accp[t];
+            pw = pp;
+            roww = rowp;
+          } else {
+            window_second<QT, kAsm>(accw, pw, roww, accp, pp, rowp, wm, y1, y2, t2, id,
+                                    piece_here);
+          }
+        } else {
+          tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
+        }
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t) accp[t] = acc[t];
@@ -901,8 +1019,13 @@ __device__ __forceinline__ void match_unit(
   // threshold load) must land before the work-group's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if SOD_I8_PIPE
-  tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, false,
-                  !SOD_I8_SEED && nst * SPS <= kDense ? 1 : 0);
+  if constexpr (kWin) {   // the last subtile closes the last window
+    static_assert(SUBS % 2 == 0, "windows of two subtiles tile a stage");
+    window_second<QT, kAsm>(accw, pw, roww, accp, pp, rowp, wm, y1, y2, t2, id, false);
+  } else {
+    tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, false,
+                          !SOD_I8_SEED && nst * SPS <= kDense ? 1 : 0);
+  }
 #endif
 #ifdef SOD_I8_COUNT
   if (lane == 0) atomicAdd(&g_counts[2], (unsigned long long)(nst * SPS));
