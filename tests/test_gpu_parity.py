@@ -131,10 +131,12 @@ def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
     assert np.array_equal(good, orc.ratio_test(f1, f2))
 
 
-@pytest.mark.parametrize("qt", ["2", "4", "8", "4p", "8p", "w1", "w2", "streamed"])
+@pytest.mark.parametrize("qt", ["2", "2f", "4", "8", "4p", "8p", "w1", "w2", "streamed"])
 def test_matcher_query_tiles_shared_thresholds(ctx, qt):
     """int8 matcher with each query-tile count per wave (option match_qt; "4p" / "8p": paired
-    waves, option match_pair = 2, each wave of a pair taking every other subtile; "w1" / "w2":
+    waves, option match_pair = 2, each wave of a pair taking every other subtile; "2f": 2 tiles
+    with the LDS fragments read two subtiles ahead (option match_pf = 2: the inline-asm reads'
+    counted waits then leave the next subtile's reads in flight); "w1" / "w2":
     the 32x32x32 kernel, impl i8w, at 1 / 2 tiles of 32 queries per wave; "streamed": the
     register-streamed kernel, match_s.hip, whose DB ranges exchange top-2 lists) over a DB split into
     many chunks, so the chunks exchange prefilter thresholds mid-run: DB rows duplicated far
@@ -144,8 +146,9 @@ def test_matcher_query_tiles_shared_thresholds(ctx, qt):
     if qt == "streamed":
         ctx.set_match_kernel("streamed")
     else:
-        ctx.set_option("match_qt", int(qt.strip("pw")))
+        ctx.set_option("match_qt", int(qt.strip("pwf")))
         ctx.set_option("match_pair", 2 if qt.endswith("p") else 1)
+        ctx.set_option("match_pf", 2 if qt.endswith("f") else 1)
     rng = np.random.default_rng(31)
     ndb, nq = 150000, 2000
     db = synthetic.sift_like_descriptors(rng, ndb)
