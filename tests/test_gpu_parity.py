@@ -112,6 +112,39 @@ def test_streamed_matcher_vs_oracle(ctx, nq, ndb, seed):
         assert np.array_equal(good, g["good"])
 
 
+@pytest.mark.parametrize("shape", ["pair4", "pair8", "pf2", "w1"])
+@pytest.mark.parametrize("nq,ndb,seed", [(1, 2, 0), (17, 1000, 1), (700, 4099, 2), (3000, 60000, 3)])
+def test_matcher_vs_oracle_options(ctx, nq, ndb, seed, shape):
+    """The matcher shapes behind options, bit for bit against the oracle on odd sizes: paired
+    waves at 4 / 8 query tiles (match_pair = 2: partial top-2 lists of the two subtile phases
+    merged through LDS), two-ahead LDS prefetch (match_pf = 2, counted asm waits at 2 tiles),
+    and the 32x32x32 kernel at one 32-query tile per wave."""
+    rng = np.random.default_rng(seed)
+    if shape == "w1":
+        ctx.set_impl("i8w")
+        ctx.set_option("match_qt", 1)
+    else:
+        ctx.set_impl("i8")
+        ctx.set_option("match_qt", {"pair4": 4, "pair8": 8, "pf2": 2}[shape])
+        ctx.set_option("match_pair", 2 if shape.startswith("pair") else 1)
+        ctx.set_option("match_pf", 2 if shape == "pf2" else 1)
+    db = synthetic.sift_like_descriptors(rng, ndb)
+    q = synthetic.sift_like_descriptors(rng, nq)
+    q[: nq // 3] = db[rng.integers(0, ndb, nq // 3)]      # exact hits (d1 = 0)
+    if ndb >= 64:
+        db[16:20] = db[0:4]                               # equal rows in neighbouring subtiles
+        q[nq // 3: nq // 3 + min(4, nq - nq // 3)] = db[0:min(4, nq - nq // 3)]
+    ctx.upload_db(db)
+    ctx.upload_queries(q)
+    ctx.match()
+    ctx.ratio(0.75)
+    idx1, d1, d2, good = ctx.match_result()
+    e1, f1, f2 = orc.knn2_match(q, db)
+    assert np.array_equal(idx1, e1)
+    assert np.array_equal(d1, f1) and np.array_equal(d2, f2)
+    assert np.array_equal(good, orc.ratio_test(f1, f2))
+
+
 @pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("nq,ndb,seed", [(1, 2, 0), (17, 1000, 1), (700, 4099, 2), (3000, 60000, 3)])
 def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
