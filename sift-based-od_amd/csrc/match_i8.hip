@@ -513,6 +513,11 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
   }
 }
 
+#ifndef SOD_I8_DEEPQT
+// prefilter two subtiles behind the MFMAs (not one) at up to this many query tiles per wave
+// (0: off): more independent MFMAs between an accumulator's last MFMA and its test
+#define SOD_I8_DEEPQT 0
+#endif
 #ifndef SOD_I8_WINQT
 // prefilter windows of two subtiles at up to this many query tiles per wave (0: off): per
 // tile one v_max3 on the window's first subtile, then max3, max3, max and the compare on the
@@ -630,6 +635,8 @@ __device__ __forceinline__ void match_unit(
   const int qwave = wave % NQW, par = wave / NQW;   // query slice, subtile phase
   constexpr bool kAsm = SOD_I8_ASMLDS == 1 || (SOD_I8_ASMLDS == 2 && QT <= 2);
   constexpr bool kWin = SOD_I8_PIPE && SOD_I8_SEED && SOD_I8_LAZYP && QT / PAIR <= SOD_I8_WINQT;
+  constexpr bool kDeep = SOD_I8_PIPE && SOD_I8_SEED && SOD_I8_LAZYP && !kWin &&
+                         QT / PAIR <= SOD_I8_DEEPQT;
   const int qt0 = (qb * NQW + qwave) * QT;
 #if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
   const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
@@ -731,6 +738,12 @@ __device__ __forceinline__ void match_unit(
   }
   [[maybe_unused]] const uint8_t* pw = nring;
   [[maybe_unused]] int roww = 0;
+  // the subtile before the pending one (kDeep)
+  [[maybe_unused]] i32x4 accq[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) accq[t] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
+  [[maybe_unused]] const uint8_t* pq = nring;
+  [[maybe_unused]] int rowq = 0;
 #endif
 
   int slot = 0;
@@ -949,6 +962,12 @@ __device__ __forceinline__ void match_unit(
             window_second<QT, kAsm>(accw, pw, roww, accp, pp, rowp, wm, y1, y2, t2, id,
                                     piece_here);
           }
+        } else if constexpr (kDeep) {
+          tile_update<QT, kAsm>(accq, pq, rowq, y1, y2, t2, id, false, 0, piece_here);
+#pragma unroll
+          for (int t = 0; t < QT; ++t) accq[t] = accp[t];
+          pq = pp;
+          rowq = rowp;
         } else {
           tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
         }
@@ -1022,6 +1041,9 @@ __device__ __forceinline__ void match_unit(
   if constexpr (kWin) {   // the last subtile closes the last window
     static_assert(SUBS % 2 == 0, "windows of two subtiles tile a stage");
     window_second<QT, kAsm>(accw, pw, roww, accp, pp, rowp, wm, y1, y2, t2, id, false);
+  } else if constexpr (kDeep) {   // the last two subtiles, in row order
+    tile_update<QT, kAsm>(accq, pq, rowq, y1, y2, t2, id, false, 0);
+    tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, false, 0);
   } else {
     tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, false,
                           !SOD_I8_SEED && nst * SPS <= kDense ? 1 : 0);
