@@ -13,7 +13,8 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;
 
 // MODE 0: MFMAs only; 1: + prefilter VALU; 2: + ballot / branch; 3: + the next subtile's A
 // fragments and c words from LDS (3 ds_read_b128, as the ring kernel); 4: the same two
-// subtiles ahead
+// subtiles ahead.  (Modes 3 / 4 also add the loaded c to the running c -- 4 v_add per subtile
+// the ring kernel does not have -- so they overstate the reads' cost by that VALU.)
 template <int QT, int MODE>
 __global__ __launch_bounds__(512, 1) void probe(const i32x4* __restrict__ in, int* out, int iters,
                                                 unsigned long long* clk) {
