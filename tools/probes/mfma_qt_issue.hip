@@ -13,7 +13,7 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;
 
 // MODE 0: MFMAs only; 1: + prefilter VALU; 2: + ballot / branch; 3: + the next subtile's A
 // fragments and c words from LDS (3 ds_read_b128, as the ring kernel); 4: the same two
-// subtiles ahead.  (Modes 3 / 4 also add the loaded c to the running c -- 4 v_add per subtile
+// subtiles ahead; 5: the two fragment reads only (c in registers).  (Modes 3 / 4 also add the loaded c to the running c -- 4 v_add per subtile
 // the ring kernel does not have -- so they overstate the reads' cost by that VALU.)
 template <int QT, int MODE>
 __global__ __launch_bounds__(512, 1) void probe(const i32x4* __restrict__ in, int* out, int iters,
@@ -53,6 +53,11 @@ __global__ __launch_bounds__(512, 1) void probe(const i32x4* __restrict__ in, in
         a0 = lds[(nu * 3) * 64 + lane];
         a1 = lds[(nu * 3 + 1) * 64 + lane];
         c = lds[(nu * 3 + 2) * 64 + (lane >> 4) * 16] + c;
+      } else if constexpr (MODE == 5) {   // the fragments only (c words held for the stage)
+        const int nu = (u + 1) & 7;
+        a0 = lds[(nu * 3) * 64 + lane];
+        a1 = lds[(nu * 3 + 1) * 64 + lane];
+        c[0] += 1;
       } else if constexpr (MODE == 4) {   // two subtiles ahead
         const int nu = (u + 2) & 7;
         a0 = a0n;
@@ -143,7 +148,7 @@ int main() {
   CK(hipMalloc(&clk, 512 * sizeof(unsigned long long)));
   if (run<2, 0>(in, out, clk, hclk) || run<2, 1>(in, out, clk, hclk) || run<2, 2>(in, out, clk, hclk) ||
       run<2, 3>(in, out, clk, hclk) || run<4, 0>(in, out, clk, hclk) || run<4, 2>(in, out, clk, hclk) ||
-      run<2, 4>(in, out, clk, hclk) || run<4, 3>(in, out, clk, hclk) || run<4, 4>(in, out, clk, hclk) ||
+      run<2, 4>(in, out, clk, hclk) || run<2, 5>(in, out, clk, hclk) || run<4, 5>(in, out, clk, hclk) || run<4, 3>(in, out, clk, hclk) || run<4, 4>(in, out, clk, hclk) ||
       run<8, 0>(in, out, clk, hclk) || run<8, 2>(in, out, clk, hclk) || run<8, 3>(in, out, clk, hclk) ||
       run<8, 4>(in, out, clk, hclk))
     return 1;
