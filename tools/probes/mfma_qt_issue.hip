@@ -13,12 +13,15 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;
 
 // MODE 0: MFMAs only; 1: + prefilter VALU; 2: + ballot / branch; 3: + the next subtile's A
 // fragments and c words from LDS (3 ds_read_b128, as the ring kernel); 4: the same two
-// subtiles ahead; 5: the two fragment reads only (c in registers).  (Modes 3 / 4 also add the loaded c to the running c -- 4 v_add per subtile
+// subtiles ahead; 5: the two fragment reads only (c in registers); 6: 5 + the LDS-DMA refill
+// at the kernel's bytes per subtile (the compiler then drains the LDS counter per read).  (Modes 3 / 4 also add the loaded c to the running c -- 4 v_add per subtile
 // the ring kernel does not have -- so they overstate the reads' cost by that VALU.)
 template <int QT, int MODE>
 __global__ __launch_bounds__(512, 1) void probe(const i32x4* __restrict__ in, int* out, int iters,
-                                                unsigned long long* clk) {
+                                                unsigned long long* clk, const uint8_t* __restrict__ g) {
   __shared__ i32x4 lds[8 * 3 * 64];
+  __shared__ __attribute__((aligned(16))) uint8_t ring[16 * 1024];   // MODE 6: LDS-DMA target
+  const int wv = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < 8 * 3 * 64; i += blockDim.x) lds[i] = in[i % (64 * 16)];
   __syncthreads();
@@ -58,6 +61,20 @@ __global__ __launch_bounds__(512, 1) void probe(const i32x4* __restrict__ in, in
         a0 = lds[(nu * 3) * 64 + lane];
         a1 = lds[(nu * 3 + 1) * 64 + lane];
         c[0] += 1;
+      } else if constexpr (MODE == 6) {   // mode 5 + the ring's LDS-DMA refill rate: one 1 KiB
+        const int nu = (u + 1) & 7;       // piece per wave on 2 of every 8 subtiles (2 KiB
+        a0 = lds[(nu * 3) * 64 + lane];   // per subtile and CU, as the kernel's 64 KiB stage
+        a1 = lds[(nu * 3 + 1) * 64 + lane];   // over 32 subtiles)
+        c[0] += 1;
+        if (u < 2) {
+          const uint8_t* src = g + ((int64_t)blockIdx.x * 1024 + (it & 63) * 16 + wv * 2 + u) * 1024;
+          __builtin_amdgcn_global_load_lds(src + lane * 16,
+                                           (__attribute__((address_space(3))) void*)(ring + (wv * 2 + u) * 1024),
+                                           16, 0, 0);
+        }
+        // (loads of three iterations ago must have landed: ~24 subtiles of prefetch window,
+        // as the kernel's one 32-subtile stage)
+        if (u == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else if constexpr (MODE == 4) {   // two subtiles ahead
         const int nu = (u + 2) & 7;
         a0 = a0n;
@@ -106,7 +123,8 @@ __global__ __launch_bounds__(512, 1) void probe(const i32x4* __restrict__ in, in
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 template <int QT, int MODE>
-int run(const i32x4* in, int* out, unsigned long long* clk, unsigned long long* hclk) {
+int run(const i32x4* in, int* out, unsigned long long* clk, unsigned long long* hclk,
+        const uint8_t* g) {
   const int iters = 2000, nwg = 256;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -114,7 +132,7 @@ int run(const i32x4* in, int* out, unsigned long long* clk, unsigned long long* 
   float ms = 0;
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL((probe<QT, MODE>), dim3(nwg), dim3(512), 0, 0, in, out, iters, clk);
+    hipLaunchKernelGGL((probe<QT, MODE>), dim3(nwg), dim3(512), 0, 0, in, out, iters, clk, g);
     CK(hipEventRecord(e1, 0));
     CK(hipDeviceSynchronize());
     CK(hipEventElapsedTime(&ms, e0, e1));
@@ -146,11 +164,16 @@ int main() {
   CK(hipMemset(in, 1, 64 * 64 * sizeof(i32x4)));
   CK(hipMalloc(&out, 256 * 512 * sizeof(int)));
   CK(hipMalloc(&clk, 512 * sizeof(unsigned long long)));
-  if (run<2, 0>(in, out, clk, hclk) || run<2, 1>(in, out, clk, hclk) || run<2, 2>(in, out, clk, hclk) ||
-      run<2, 3>(in, out, clk, hclk) || run<4, 0>(in, out, clk, hclk) || run<4, 2>(in, out, clk, hclk) ||
-      run<2, 4>(in, out, clk, hclk) || run<2, 5>(in, out, clk, hclk) || run<4, 5>(in, out, clk, hclk) || run<4, 3>(in, out, clk, hclk) || run<4, 4>(in, out, clk, hclk) ||
-      run<8, 0>(in, out, clk, hclk) || run<8, 2>(in, out, clk, hclk) || run<8, 3>(in, out, clk, hclk) ||
-      run<8, 4>(in, out, clk, hclk))
+  uint8_t* g;   // 256 work-groups x 64 x 16 KiB of DMA source (256 MiB: streamed, past the caches)
+  CK(hipMalloc(&g, (size_t)256 * 1024 * 1024));
+  CK(hipMemset(g, 3, (size_t)256 * 1024 * 1024));
+  if (run<2, 0>(in, out, clk, hclk, g) || run<2, 1>(in, out, clk, hclk, g) || run<2, 2>(in, out, clk, hclk, g) ||
+      run<2, 3>(in, out, clk, hclk, g) || run<4, 0>(in, out, clk, hclk, g) || run<4, 2>(in, out, clk, hclk, g) ||
+      run<2, 4>(in, out, clk, hclk, g) || run<2, 5>(in, out, clk, hclk, g) || run<4, 5>(in, out, clk, hclk, g) ||
+      run<2, 6>(in, out, clk, hclk, g) || run<4, 6>(in, out, clk, hclk, g) ||
+      run<2, 7>(in, out, clk, hclk, g) || run<4, 7>(in, out, clk, hclk, g) || run<4, 3>(in, out, clk, hclk, g) || run<4, 4>(in, out, clk, hclk, g) ||
+      run<8, 0>(in, out, clk, hclk, g) || run<8, 2>(in, out, clk, hclk, g) || run<8, 3>(in, out, clk, hclk, g) ||
+      run<8, 4>(in, out, clk, hclk, g))
     return 1;
   return 0;
 }
