@@ -142,6 +142,12 @@ class Dist:
     def sum(self, x):
         return self.store.sum(x) if self.store else x
 
+    def gather_json(self, obj):
+        """Every rank's JSON-able ``obj``, in rank order (rank 0 reports them)."""
+        if not self.store:
+            return [obj]
+        return [json.loads(b.decode()) for b in self.store.allgather_bytes(json.dumps(obj).encode())]
+
     def close(self):
         if self.store:
             self.store.close()
@@ -487,6 +493,7 @@ def main():
     sync_all()
     for c in ctxs:
         c.set_match_timing(stride)  # counted from the first timed launch
+        c.host_wait_ms(reset=True)
     t0 = time.perf_counter()
     host = 0.0                      # host time spent enqueueing (the calls return unsynced)
     for _ in range(a.steps):
@@ -498,6 +505,8 @@ def main():
     t1 = time.perf_counter()
     el = D.max(t1 - t0)
     ms_per_step = 1000.0 * el / a.steps
+    # the enqueue calls' host time split: blocked on the device (slot wait) vs host work
+    blocked_ms = sum(c.host_wait_ms(reset=True) for c in ctxs)
 
     # ---- matcher kernel time inside the timed region: begin/end HIP events recorded around
     # every launch on the matcher's own stream (sod_match_times), read back afterwards ----
@@ -584,6 +593,16 @@ def main():
     n_votes = int(votes.sum())
     aff = ctx.affine_result() if run_affine else None
     idx1, d1, d2, good = ctx.match_result()
+    # self-verifying multi-rank record: the communicator as RCCL reports
+    # it on every rank, and how many of the merged global winners (good matches) each shard
+    # contributed -- every rank holds the same merged result, so each counts all shards and
+    # its own count must agree with the others'
+    cinfo = comm.info() if comm is not None else None
+    winners = np.bincount((idx1 // n_shard).astype(np.int64), minlength=world).tolist()
+    good_winners = np.bincount((idx1[good] // n_shard).astype(np.int64), minlength=world).tolist()
+    rank_rec = D.gather_json({"rank": rank, "comm": cinfo, "shard_winners": winners,
+                              "own_shard_winners": winners[rank],
+                              "shard_good_winners": good_winners})
 
     # Hough stage roofline: algorithmic bytes 52 per good match (query kp 16 +
     # model kp 16 + idx 4 + centroid 16) + 4 per bin (the count written out) over the
@@ -626,6 +645,10 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": ms_per_step,
         "host_enqueue_ms_per_step": 1000.0 * host / a.steps,
+        # of which blocked waiting for the device (a launch waits for the merge that last read
+        # its partial-result slot: two steps in flight) / the host's own work
+        "host_blocked_ms_per_step": blocked_ms / a.steps,
+        "host_cpu_enqueue_ms_per_step": (1000.0 * host - blocked_ms) / a.steps,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -638,7 +661,13 @@ def main():
             "bins": list(bins), "parallelism": "db-shard%d" % world,
             "query_streams": ncontexts, "matcher_overlap": bool(overlap),
             "cu_reserve_per_xcd": reserve, "matcher_streams": a.matcher_streams,
-            "comm": a.comm if world > 1 else None},
+            "comm": a.comm if world > 1 else None,
+            "rccl_nranks": cinfo["nranks"] if cinfo and cinfo["kind"] == "rccl" else None,
+            "rccl_rank": cinfo["rank"] if cinfo and cinfo["kind"] == "rccl" else None},
+        "ranks": rank_rec,
+        # per shard: queries whose merged nearest row (trainIdx) it holds / of those, good
+        "shard_winners": winners,
+        "shard_good_winners": good_winners,
         "hough_votes_per_s": n_votes / (ms_per_step / 1000.0),
         "hough_stage_votes_per_s": n_votes / (t_hough / 1000.0),
         "hough_votes": n_votes,

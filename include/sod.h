@@ -80,6 +80,11 @@ int sod_set_match_timing(sod_ctx* ctx, int on);
  * boundary (higher throughput for mid-size query sets; a launch's events then span the
  * overlap).  Results are unchanged. */
 int sod_set_matcher_streams(sod_ctx* ctx, int n);
+/* Host time (ns) the enqueue calls spent BLOCKED waiting for the device since the last reset:
+ * a matcher launch waits for the merge that last read its partial-result slot (two launches
+ * in flight at most).  Enqueue wall time minus this is the host's own work.  reset != 0 zeroes
+ * the counter after reading it.  (No reference counterpart: measurement.) */
+int sod_host_wait_ns(sod_ctx* ctx, int64_t* ns, int reset);
 
 /* ---- database (replaces main.py:36-66 flattening + GenerateDatabaseInfo.py format) --
  * Keypoints and the per-image table cover the WHOLE database (replicated on every
@@ -438,6 +443,10 @@ int sod_hough_partial_set(sod_ctx* ctx, const uint32_t* counts, const uint32_t* 
 int sod_comm_unique_id(uint8_t out[SOD_UNIQUE_ID_BYTES]);
 int sod_comm_init(sod_ctx* ctx, int32_t nranks, int32_t rank,
                   const uint8_t id[SOD_UNIQUE_ID_BYTES]);
+/* The ctx's RCCL communicator as RCCL itself reports it (ncclCommCount,
+ * ncclCommUserRank): a multi-GPU record can show that the collectives ran over nranks
+ * ranks.  SOD_ESTATE when no communicator was created.  (No reference counterpart.) */
+int sod_comm_info(sod_ctx* ctx, int32_t* nranks, int32_t* rank);
 
 #ifdef __cplusplus
 }

@@ -42,24 +42,39 @@ _MATMUL_FMA = None
 
 
 def numpy_matmul_fma():
-    """1 when this host's numpy evaluates remove_outliers' 2x2 product np.matmul(M, X)
-    (AffineParameters.py:145) as fma(m1, x, m2*y) -- OpenBLAS's dgemv on an FMA CPU -- for
-    every probed value, 0 when as m1*x + m2*y (two roundings) or anything else; probed once
-    per process (exact fma by rational arithmetic)."""
-    global _MATMUL_FMA
+    """How this host's numpy rounds remove_outliers' 2x2 product np.matmul(M, X)
+    (AffineParameters.py:145), both output rows, probed once per process against exact
+    rational arithmetic: 1 when every row is fma(m_r0, x, m_r1*y) (OpenBLAS's dgemv on an FMA
+    CPU), 2 when fma(m_r1, y, m_r0*x) (the other contraction order), 0 when m_r0*x + m_r1*y
+    (two roundings).  The affine kernel follows the mode given (option affine_fma).  A host
+    matching none of the three on every probe gets 0 (and ``MATMUL_FMA_CONSISTENT`` False):
+    its rare boundary cases are then parity-unpinned."""
+    global _MATMUL_FMA, MATMUL_FMA_CONSISTENT
     if _MATMUL_FMA is None:
         from fractions import Fraction
+
+        def fma(a, b, c):
+            return float(Fraction(a) * Fraction(b) + Fraction(c))
         rng = np.random.default_rng(12345)
-        fma_all, differs = True, False
-        for m1, m2, x, y in zip(rng.uniform(-2, 2, 256), rng.uniform(-2, 2, 256),
-                                rng.uniform(0, 1500, 256), rng.uniform(0, 1000, 256)):
-            m1, m2, x, y = float(m1), float(m2), float(x), float(y)
-            r = float(np.matmul([[m1, m2], [m2, m1]], [x, y])[0])
-            f = float(Fraction(m1) * Fraction(x) + Fraction(m2 * y))
-            fma_all &= r == f
-            differs |= f != m1 * x + m2 * y
-        _MATMUL_FMA = 1 if fma_all and differs else 0
+        ok = {0: True, 1: True, 2: True}
+        seen = {0: False, 1: False, 2: False}   # the mode is told apart from the others
+        for row in rng.uniform(-2, 2, (256, 6)):
+            a, b, c, d = (float(v) for v in row[:4])
+            x, y = float(row[4] * 750 + 750), float(row[5] * 500 + 500)
+            r = np.matmul([[a, b], [c, d]], [x, y]).tolist()
+            for m0, m1, got in ((a, b, r[0]), (c, d, r[1])):
+                cand = {0: m0 * x + m1 * y, 1: fma(m0, x, m1 * y), 2: fma(m1, y, m0 * x)}
+                for k, v in cand.items():
+                    ok[k] &= got == v
+                    seen[k] |= any(v != w for w in cand.values())
+        modes = [k for k in (1, 2, 0) if ok[k]]
+        MATMUL_FMA_CONSISTENT = bool(modes)
+        # ties (a probe set where two modes never differ) resolve to the listed order
+        _MATMUL_FMA = next((k for k in modes if seen[k]), modes[0] if modes else 0)
     return _MATMUL_FMA
+
+
+MATMUL_FMA_CONSISTENT = True
 
 
 class Results(C.Structure):
@@ -139,6 +154,7 @@ SIGNATURES = {
     "sod_match_set_impl": (C.c_int, [c_ctx, C.c_int]),
     "sod_match_set_kernel": (C.c_int, [c_ctx, C.c_int]),
     "sod_trig_exact": (C.c_int, [c_ctx]),
+    "sod_host_wait_ns": (C.c_int, [c_ctx, c_i64p, C.c_int]),
     "sod_glibc_sincos": (C.c_int, [c_ctx, C.c_int64, c_vp, c_vp, c_vp]),
     "sod_results_fetch": (C.c_int, [c_ctx, C.c_int, C.POINTER(Results)]),
     "sod_set_option": (C.c_int, [c_ctx, C.c_char_p, C.c_int64]),
@@ -193,6 +209,7 @@ SIGNATURES = {
     "sod_sift_to_queries": (C.c_int, [c_ctx]),
     "sod_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
     "sod_comm_init": (C.c_int, [c_ctx, C.c_int32, C.c_int32, C.POINTER(C.c_uint8 * UNIQUE_ID_BYTES)]),
+    "sod_comm_info": (C.c_int, [c_ctx, c_i32p, c_i32p]),
 }
 
 _lib = None
@@ -348,6 +365,13 @@ class Context:
                                              else int(impl)))
         self.db_gen += 1
 
+    def host_wait_ms(self, reset=True):
+        """Host time (ms) enqueue calls spent blocked on the device (the partial-result slot
+        wait) since the last reset (sod_host_wait_ns)."""
+        v = C.c_int64()
+        self._chk(self._L.sod_host_wait_ns(self._h, C.byref(v), 1 if reset else 0))
+        return v.value / 1e6
+
     def trig_exact(self):
         """True when the device's cos / sin are this host's libm bit for bit (then poses,
         bins and PoseBin means equal the reference's without any host redo)."""
@@ -366,7 +390,7 @@ class Context:
     OPTIONS = ("match_qt", "match_pf", "match_pair", "hough_fused", "select_multi", "sift_stream_mask",
                "sift_sort_max", "sift_desc_range_max", "sift_layer_split", "sift_side_mask",
                "sift_fork2", "sift_early_desc", "sift_direct", "sift_eager_rank", "debug_sync",
-               "affine_fma")
+               "affine_fma", "trig_exact")
 
     def set_option(self, name, value):
         """A tuning / test switch of this context by name (sod.h sod_set_option); returns the
@@ -870,6 +894,13 @@ class Context:
     def comm_init(self, nranks, rank, uid):
         buf = (C.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(uid)
         self._chk(self._L.sod_comm_init(self._h, int(nranks), int(rank), C.byref(buf)))
+
+    def comm_info(self):
+        """(nranks, rank) of this context's RCCL communicator as RCCL reports them
+        (sod_comm_info: ncclCommCount / ncclCommUserRank)."""
+        n, r = C.c_int32(), C.c_int32()
+        self._chk(self._L.sod_comm_info(self._h, C.byref(n), C.byref(r)))
+        return n.value, r.value
 
 
 def bins4(bins):

@@ -89,6 +89,18 @@ int sod_inputs_end(sod_ctx* ctx) {
   SOD_HIP(ctx, hipEventRecord(ctx->ev_inputs, ctx->stream));
   return SOD_OK;
 }
+// the slot wait below, with the host time it blocks accumulated (sod_host_wait_ns): what part
+// of an enqueue call is waiting for the device rather than host work
+static int slot_wait(sod_ctx* ctx, hipEvent_t ev) {
+  const hipError_t q = hipEventQuery(ev);
+  if (q == hipSuccess) return SOD_OK;
+  (void)hipGetLastError();
+  const auto t0 = std::chrono::steady_clock::now();
+  SOD_HIP(ctx, hipEventSynchronize(ev));
+  ctx->host_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now() - t0).count();
+  return SOD_OK;
+}
 static bool stream_idle(hipStream_t s) {
   const hipError_t q = hipStreamQuery(s);
   if (q == hipSuccess) return true;
@@ -121,7 +133,7 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
                   stream_idle(ctx->mstream2));
   if (ctx->mk_main) {
     *ks = ctx->stream;
-    if (ctx->overlap) SOD_HIP(ctx, hipEventSynchronize(ctx->ev_merged[ctx->pslot]));
+    if (ctx->overlap) SOD_TRY(slot_wait(ctx, ctx->ev_merged[ctx->pslot]));
     return SOD_OK;
   }
   *ks = ctx->mstream_of(ctx->pslot);
@@ -138,7 +150,7 @@ int sod_match_stream_begin(sod_ctx* ctx, int64_t n, hipStream_t* ks, float** d1,
   // between two back-to-back matcher launches costs ~6 us per launch, C2 0.166 vs 0.160 ms per
   // step); it bounds a context to two matcher launches in flight, and the merge it waits for
   // ran right after the launch before the previous one, so the wait is normally over already
-  SOD_HIP(ctx, hipEventSynchronize(ctx->ev_merged[ctx->pslot]));
+  SOD_TRY(slot_wait(ctx, ctx->ev_merged[ctx->pslot]));
   // a new slot size moves the slots' boundaries: the other slot's last merge must be done too
   if (resized) SOD_TRY(wait_unless_done(ctx, *ks, ctx->ev_merged[ctx->pslot ^ 1]));
   return SOD_OK;
@@ -330,6 +342,7 @@ const OptEntry kOpts[] = {
     {"sift_eager_rank", &sod_opts::sift_eager_rank},
     {"affine_fma", &sod_opts::affine_fma},
     {"debug_sync", &sod_opts::debug_sync},
+    {"trig_exact", &sod_opts::trig_exact},
 };
 const OptEntry* find_opt(const char* name) {
   for (const OptEntry& o : kOpts)
@@ -343,16 +356,33 @@ void opts_from_env(sod_opts& op) {
     for (const char* c = o.name; *c; ++c) env += (char)std::toupper((unsigned char)*c);
     if (const char* e = std::getenv(env.c_str())) op.*(o.field) = std::atoi(e);
   }
-  if (op.debug_sync) sod_debug_sync = 1;
+  if (op.debug_sync) op.debug_sync = 1;
 }
+// ctx->trig_exact from the probe and the option (-1 auto, 0 forced fallback)
+void apply_trig_opt(sod_ctx* ctx) { ctx->trig_exact = ctx->trig_probe && ctx->opt.trig_exact != 0; }
 }  // namespace
 
 int sod_set_option(sod_ctx* ctx, const char* name, int64_t value) {
   if (!ctx) return SOD_EINVAL;
   const OptEntry* o = find_opt(name);
   if (!o) return sod_fail(ctx, SOD_EINVAL, std::string("unknown option ") + (name ? name : "(null)"));
+  if (value < INT32_MIN || value > INT32_MAX)
+    return sod_fail(ctx, SOD_EINVAL, std::string("option ") + name + " out of the int range");
+  if (o->field == &sod_opts::trig_exact) {
+    if (value < -1 || value > 1)
+      return sod_fail(ctx, SOD_EINVAL, "trig_exact must be -1 (auto), 0 (fallback) or 1");
+    if (value == 1 && !ctx->trig_probe)
+      return sod_fail(ctx, SOD_EINVAL,
+                      "trig_exact 1 refused: this host's libm cos / sin differ from the device's");
+  }
+  if (o->field == &sod_opts::debug_sync) {
+    const int on = value != 0;
+    if (on != ctx->opt.debug_sync) sod_debug_sync += on ? 1 : -1;
+    ctx->opt.debug_sync = on;
+    return SOD_OK;
+  }
   ctx->opt.*(o->field) = (int)value;
-  sod_debug_sync = ctx->opt.debug_sync != 0;
+  if (o->field == &sod_opts::trig_exact) apply_trig_opt(ctx);
   return SOD_OK;
 }
 
@@ -370,6 +400,7 @@ int sod_create(int device, sod_ctx** out) {
   sod_ctx* ctx = new sod_ctx();
   ctx->device = device;
   opts_from_env(ctx->opt);
+  if (ctx->opt.debug_sync) ++sod_debug_sync;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) {
@@ -378,7 +409,8 @@ int sod_create(int device, sod_ctx** out) {
     if (e == hipSuccess) {
       ctx->num_cus = prop.multiProcessorCount;
       ctx->gfx950 = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
-      ctx->trig_exact = sod_host_trig_matches_device();
+      ctx->trig_probe = sod_host_trig_matches_device();
+      apply_trig_opt(ctx);
       int nx = 0;
       if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, device) == hipSuccess && nx > 0)
         ctx->num_xcds = nx;
@@ -398,6 +430,7 @@ int sod_create(int device, sod_ctx** out) {
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_matched1);
   if (e != hipSuccess) {
     g_err = std::string("sod_create: ") + hipGetErrorString(e);
+    if (ctx->opt.debug_sync) --sod_debug_sync;
     delete ctx;
     return SOD_EHIP;
   }
@@ -480,6 +513,7 @@ void sod_destroy(sod_ctx* ctx) {
   if (ctx->mstream) (void)hipStreamDestroy(ctx->mstream);
   if (ctx->mstream2) (void)hipStreamDestroy(ctx->mstream2);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->opt.debug_sync) --sod_debug_sync;
   delete ctx;
 }
 
@@ -1010,6 +1044,13 @@ int sod_match_set_impl(sod_ctx* ctx, int impl) {
     ctx->nqt = 0;
     ctx->matched = ctx->ratio_done = ctx->houghed = ctx->selected = ctx->affined = false;
   }
+  return SOD_OK;
+}
+
+int sod_host_wait_ns(sod_ctx* ctx, int64_t* ns, int reset) {
+  if (!ctx || !ns) return SOD_EINVAL;
+  *ns = ctx->host_wait_ns;
+  if (reset) ctx->host_wait_ns = 0;
   return SOD_OK;
 }
 
@@ -1855,6 +1896,19 @@ int sod_comm_init(sod_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[S
     return sod_fail(ctx, SOD_ECOMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
   }
   ctx->comm_max_channels = cap;
+  return SOD_OK;
+}
+
+int sod_comm_info(sod_ctx* ctx, int32_t* nranks, int32_t* rank) {
+  if (!ctx || !nranks || !rank) return SOD_EINVAL;
+  if (!ctx->comm) return sod_fail(ctx, SOD_ESTATE, "no RCCL communicator (sod_comm_init)");
+  int n = 0, r = -1;
+  ncclResult_t e = ncclCommCount(ctx->comm, &n);
+  if (e == ncclSuccess) e = ncclCommUserRank(ctx->comm, &r);
+  if (e != ncclSuccess)
+    return sod_fail(ctx, SOD_ECOMM, std::string("ncclCommCount/UserRank: ") + ncclGetErrorString(e));
+  *nranks = n;
+  *rank = r;
   return SOD_OK;
 }
 

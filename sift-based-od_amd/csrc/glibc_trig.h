@@ -1,5 +1,14 @@
 // glibc_trig.h -- glibc's double sin / cos, bit for bit, on the host and on the device.
 //
+// Licence: this file restates the algorithm of the GNU C Library's
+// sysdeps/ieee754/dbl-64/s_sin.c (glibc 2.35; Copyright (C) 2001-2022 Free Software
+// Foundation, Inc., originally IBM Accurate Mathematical Library, written by International
+// Business Machines Corp.), and glibc_trig_tab.h holds that library's constants and sin / cos
+// table.  The GNU C Library is free software under the GNU Lesser General Public License,
+// version 2.1 or (at your option) any later version; this file and glibc_trig_tab.h are
+// distributed under those same terms (LGPL-2.1-or-later), separately from the rest of this
+// repository.  See https://www.gnu.org/licenses/old-licenses/lgpl-2.1.html.
+//
 // Why: HoughTransformHelperFunctions.py:31-35 (estimate_object_pose) rotates each match's
 // model offset with Python's math.cos / math.sin, i.e. glibc's libm.  Those results are not
 // correctly rounded (about 0.15 % of angles in [0, 2 pi) differ from the correctly rounded

@@ -1780,11 +1780,16 @@ __device__ __forceinline__ void affine_groups(
         for (int t = 0; t < kAffU; ++t) {
           if (!al[t]) continue;
           const double x = fx[t], y = fy[t];
-          // np.matmul(M, X) + T (AffineParameters.py:145-146): on a host whose numpy
-          // evaluates the 2x2 product as fma(m1, x, m2 y) (OpenBLAS dgemv, option
-          // affine_fma, set by the Python layer from a probe of np.matmul), the same
-          const double up = (mxfma ? fma(prm[0], x, prm[1] * y) : prm[0] * x + prm[1] * y) + prm[4];
-          const double vp = (mxfma ? fma(prm[2], x, prm[3] * y) : prm[2] * x + prm[3] * y) + prm[5];
+          // np.matmul(M, X) + T (AffineParameters.py:145-146) rounded as this host's numpy
+          // does (option affine_fma, set by the Python layer from a probe of np.matmul):
+          // 1 = fma(m1, x, m2 y) (OpenBLAS dgemv on an FMA CPU), 2 = fma(m2, y, m1 x),
+          // 0 = m1 x + m2 y
+          const double up = (mxfma == 1   ? fma(prm[0], x, prm[1] * y)
+                             : mxfma == 2 ? fma(prm[1], y, prm[0] * x)
+                                          : prm[0] * x + prm[1] * y) + prm[4];
+          const double vp = (mxfma == 1   ? fma(prm[2], x, prm[3] * y)
+                             : mxfma == 2 ? fma(prm[3], y, prm[2] * x)
+                                          : prm[2] * x + prm[3] * y) + prm[5];
           if (fabs(up - (double)fu[t]) > xref || fabs(vp - (double)fw[t]) > yref) {
             alive[j0 + (int64_t)t * G] = 0;
             ++dropped;
@@ -2027,6 +2032,7 @@ int launch_hough(sod_ctx* ctx, int64_t own_lo, int64_t own_hi) {
   SOD_HIP(ctx, hipGetLastError());
   SOD_TRY(launch_hist(ctx));
   ctx->guard_done = ctx->trig_exact;   // nothing listed: no read-back before the results
+  if (ctx->trig_exact) ctx->guard_flagged = ctx->guard_patched = 0;   // (not a stale count)
   ctx->hist_dense = true;
   return SOD_OK;
 }
@@ -2432,6 +2438,7 @@ int launch_hough_small(sod_ctx* ctx, int32_t thr) {
                         ctx->aqx.p, ctx->aqy.p, ctx->aisig.p);
   SOD_HIP(ctx, hipGetLastError());
   ctx->guard_done = ctx->trig_exact;
+  if (ctx->trig_exact) ctx->guard_flagged = ctx->guard_patched = 0;
   ctx->hist_dense = false;
   ctx->gathered = true;
   // the PoseBin means wait for the affine enqueue, which runs them in the same launch

@@ -57,9 +57,6 @@ constexpr int NT16 = NW16 * 64;
 #ifndef SOD_I8_SPS
 #define SOD_I8_SPS 32    // 512-row stages: 64 KiB, two slots (measured +1 % over 256-row x 3)
 #endif
-#ifndef SOD_I8_UNROLL
-#define SOD_I8_UNROLL 0    // subtile-loop unroll (0 = full)
-#endif
 constexpr int SPS = SOD_I8_SPS;   // subtiles per stage (one barrier per stage)
 constexpr int kStageRows = SPS * 16;
 constexpr int kSub = 2048;     // bytes per 16-row subtile
@@ -166,16 +163,11 @@ __device__ __forceinline__ void issue_norms(const int* __restrict__ dn, int64_t 
   if (lane < 2 * L) glds16(src, slot_norm + wave * (8 * R));
 }
 
-#ifndef SOD_I8_DMA
-#define SOD_I8_DMA 1       // 1: descriptor refill as buffer loads (SGPR offsets, no address VALU),
-#endif                     //    one 1 KiB piece per subtile over the stage; 0: burst at the barrier
 #ifndef SOD_I8_XCHUNK
 #define SOD_I8_XCHUNK 1    // thresholds shared between the DB chunks of a query (global max)
 #endif
-#if SOD_I8_DMA || SOD_I8_XCHUNK
 // buffer descriptor word 3 for CDNA (raw, untyped, 32-bit format field as the loads ignore it)
 constexpr int kRsrcWord3 = 0x00020000;
-#endif
 
 // one 1 KiB piece of a stage: lane i's 16 B land at slot + 16 i (M0 = the LDS piece base)
 __device__ __forceinline__ void issue_piece(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_piece,
@@ -249,18 +241,6 @@ __device__ __forceinline__ void merge2i(int& y1, int& i1, int& y2, int o1, int o
   }
 }
 
-#ifndef SOD_I8_PIPE
-#define SOD_I8_PIPE 1      // prefilter subtile u while the MFMAs of subtile u+1 run
-#endif
-#ifndef SOD_I8_SGB
-#define SOD_I8_SGB 1       // explicit MFMA / VALU interleave of the subtile block (+3 %)
-#endif
-#ifndef SOD_I8_COLD
-#define SOD_I8_COLD 1      // mark the slow path unlikely (compact hot loop in the i-cache)
-#endif
-#ifndef SOD_I8_XCD
-#define SOD_I8_XCD 1       // XCD-aware work-group -> (chunk, query block) order
-#endif
 #ifndef SOD_I8_SLOTS
 #define SOD_I8_SLOTS 1     // shared bound from the best rows of the even / odd DB chunks
 #endif
@@ -270,9 +250,6 @@ template <int QT>
 constexpr int gwords() { return SOD_I8_SLOTS && QT <= 4 ? kThrWords : 1; }
 #ifndef SOD_I8_SEEDSLOT
 #define SOD_I8_SEEDSLOT 1  // the seed's best row goes out with the seed's t2
-#endif
-#ifndef SOD_I8_LAZYP
-#define SOD_I8_LAZYP 1     // parity words read from LDS on the slow path only
 #endif
 #ifndef SOD_I8_SEED
 #define SOD_I8_SEED 1      // seed pass over a chunk's first stage instead of the dense phase
@@ -295,13 +272,6 @@ constexpr int gwords() { return SOD_I8_SLOTS && QT <= 4 ? kThrWords : 1; }
 constexpr int64_t kDense = SOD_I8_DENSE;
 // shared-threshold exchange points (subtiles of a stage, SOD_I8_XCHUNK): the DMA issued at
 // kShareLoad[i] is applied at kShareApply[i] (the same stage when it is later, else the next)
-#ifndef SOD_I8_SHARE2
-#define SOD_I8_SHARE2 0
-#endif
-#if SOD_I8_SHARE2
-__device__ __forceinline__ constexpr bool share_load(int u) { return u == 8 || u == 24; }
-__device__ __forceinline__ constexpr bool share_apply(int u) { return u == 20 || u == 12; }
-#else
 #ifndef SOD_I8_PUB_EVERY
 #define SOD_I8_PUB_EVERY 1   // 4 measured: 5 % less L2-miss traffic, time unchanged
 #endif
@@ -322,16 +292,6 @@ constexpr int64_t kXDense = SOD_I8_XDENSE, kXEvery = SOD_I8_XEVERY;
 constexpr int kShareAt[2] = {SOD_I8_SHARE_AT};
 __device__ __forceinline__ constexpr bool share_load(int u) { return u == kShareAt[0]; }
 __device__ __forceinline__ constexpr bool share_apply(int u) { return u == kShareAt[1]; }
-#endif
-#ifndef SOD_I8_XWAIT
-// 1: the exchange's apply point waits for the threshold load (vmcnt(0): also for the next
-// stage's refill pieces issued before it); 0: no wait -- the wave's LDS copy starts as
-// "nothing known" and every dword read is the old or the new copy, both valid bounds
-#define SOD_I8_XWAIT 1
-#endif
-#ifndef SOD_SHARED_T
-#define SOD_SHARED_T 1     // prefilter threshold = the query's 2nd best over all lane groups
-#endif
 
 constexpr int kRing = SOD_I8_RING;
 constexpr int kLoadsPerStage = kPiecesPerWave + 1;   // vm instructions per wave per stage
@@ -361,11 +321,7 @@ __device__ __forceinline__ int max_xor3216(int a) {
   return max((int)p[0], (int)p[1]);
 }
 
-#if SOD_I8_LAZYP
 #define PARITY_T const uint8_t*   // LDS address of the lane's 4 parity words
-#else
-#define PARITY_T i32x4            // the parity words
-#endif
 
 // max of N values as a v_max3 tree (ceil((N-1)/2) VALU), fully unrolled
 template <int N>
@@ -387,18 +343,6 @@ struct MaxTree {
   }
 };
 
-#if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
-// diagnostic builds only: per wave slot, s_memtime cycles.  SOD_I8_TIME: [0] inside the
-// slow path, [1] its entries, [2] the whole work unit.  SOD_I8_TIME2 (no slow-path timer):
-// [0] stage-top waits (vmcnt + barrier), [1] the seed pass (SOD_I8_TIME2=2: the vmcnt part
-// of [0]), [2] the whole work unit, [3] from the unit's start to the first stage's barrier
-__device__ unsigned long long g_tm[32768][4];
-#endif
-#ifdef SOD_I8_COUNT
-// diagnostic build only: [0] slow-path entries, [1] hit tiles, [2] wave-subtiles,
-// [3] entries and [4] hit tiles within the first 64 subtiles of a chunk
-__device__ unsigned long long g_counts[8];
-#endif
 
 // prefilter + exact top-2 update of one 16x16 tile set (see the file comment).  Each lane
 // keeps the exact top-2 (with index) of ITS rows; the prefilter threshold is the query's
@@ -410,8 +354,7 @@ __device__ unsigned long long g_counts[8];
 template <int QT, bool kAsm>
 __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin, int rowb,
                                             int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
-                                            int (&id)[QT], bool early = false, int mode = 0,
-                                            bool vmem = false) {
+                                            int (&id)[QT], int mode = 0, bool vmem = false) {
   uint64_t hit[QT];
   uint64_t any = 0;
 #pragma unroll
@@ -420,7 +363,6 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
     hit[t] = __builtin_amdgcn_ballot_w64(m >= t2[t]);
     any |= hit[t];
   }
-#if SOD_I8_SGB
   // interleave this block (the subtile's 16 MFMAs, next-subtile LDS reads, the previous
   // subtile's prefilter) as MFMA, 2 VALU, MFMA, 2 VALU, ...
 #pragma unroll
@@ -431,28 +373,7 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                        // DS read
     if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);      // refill piece
   }
-#endif
-#if SOD_I8_COLD
   if (__builtin_expect(any != 0, 0)) {   // slow path laid out away from the hot loop
-#ifdef SOD_I8_TIME
-    const unsigned long long tsp0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef SOD_I8_COUNT
-    if ((threadIdx.x & 63) == 0) {
-      unsigned nh = 0;
-      for (int t = 0; t < QT; ++t) nh += hit[t] != 0;
-      atomicAdd(&g_counts[0], 1ull);
-      atomicAdd(&g_counts[1], (unsigned long long)nh);
-      if (early) {
-        atomicAdd(&g_counts[3], 1ull);
-        atomicAdd(&g_counts[4], (unsigned long long)nh);
-      }
-    }
-#endif
-#else
-  if (any) {
-#endif
-#if SOD_I8_LAZYP
     i32x4 p;
     if constexpr (kAsm) {
       // (an LDS read the compiler tracked here would make it drain the counter before every
@@ -462,9 +383,6 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
     } else {
       p = *reinterpret_cast<const i32x4*>(pin);
     }
-#else
-    const i32x4 p = pin;
-#endif
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
       if (hit[t]) {
@@ -477,134 +395,20 @@ __device__ __forceinline__ void tile_update(const i32x4 (&acc)[QT], PARITY_T pin
           y1[t] = gt ? y : y1[t];
         }
         if (mode == 0) {
-#if SOD_SHARED_T
           int g1 = y1[t], g2 = y2[t];
           top2_xor32(g1, g2);
           top2_xor16(g1, g2);
           t2[t] = max(t2[t], g2 >> 1);   // never below a shared bound already applied
-#else
-          t2[t] = max(t2[t], y2[t] >> 1);
-#endif
         }
       }
     }
     if (mode == 2) {
 #pragma unroll
       for (int t = 0; t < QT; ++t) {
-#if SOD_SHARED_T
         int g1 = y1[t], g2 = y2[t];
         top2_xor32(g1, g2);
         top2_xor16(g1, g2);
         t2[t] = max(t2[t], g2 >> 1);
-#else
-        t2[t] = max(t2[t], y2[t] >> 1);
-#endif
-      }
-    }
-#ifdef SOD_I8_TIME
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const unsigned long long tsp1 = __builtin_amdgcn_s_memtime();
-    if ((threadIdx.x & 63) == 0) {
-      const int wslot = (blockIdx.x * 8 + (threadIdx.x >> 6)) & 32767;
-      atomicAdd(&g_tm[wslot][0], tsp1 - tsp0);
-      atomicAdd(&g_tm[wslot][1], 1ull);
-    }
-#endif
-  }
-}
-
-#ifndef SOD_I8_DEEPQT
-// prefilter two subtiles behind the MFMAs (not one) at up to this many query tiles per wave
-// (0: off): more independent MFMAs between an accumulator's last MFMA and its test
-#define SOD_I8_DEEPQT 0
-#endif
-#ifndef SOD_I8_WINQT
-// prefilter windows of two subtiles at up to this many query tiles per wave (0: off): per
-// tile one v_max3 on the window's first subtile, then max3, max3, max and the compare on the
-// second -- 5 VALU and one ballot / branch per two subtiles instead of 6 and two
-#define SOD_I8_WINQT 0
-#endif
-// the window's first subtile: wm = max of three of its four values per tile (the fourth
-// stays in the kept accumulators)
-template <int QT, bool kAsm>
-__device__ __forceinline__ void window_first(const i32x4 (&acc)[QT], int (&wm)[QT], bool vmem) {
-#pragma unroll
-  for (int t = 0; t < QT; ++t) wm[t] = max(max(acc[t][0], acc[t][1]), acc[t][2]);
-#if SOD_I8_SGB
-#pragma unroll
-  for (int i = 0; i < 2 * QT; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);                            // MFMA
-    if (i < QT) __builtin_amdgcn_sched_group_barrier(0x2, 1, 0);                // VALU
-    if (!kAsm && i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);      // refill piece
-  }
-#endif
-}
-// exact top-2 update of one tile's four rows (the slow path's inner loop)
-__device__ __forceinline__ void exact4(const i32x4& a, const i32x4& p, int rowb, int& y1,
-                                       int& y2, int& id) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int y = 2 * a[r] | p[r];
-    const bool gt = y > y1;
-    y2 = imed3(y1, y, y2);
-    id = gt ? rowb + r : id;
-    y1 = gt ? y : y1;
-  }
-}
-template <bool kAsm>
-__device__ __forceinline__ i32x4 parity_words(const uint8_t* pin) {
-  i32x4 p;
-  if constexpr (kAsm) {
-    p = lds_read16(lds_addr(pin), 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p));
-  } else {
-    p = *reinterpret_cast<const i32x4*>(pin);
-  }
-  return p;
-}
-// the window's second subtile: the compare over both subtiles' rows, and on a hit the exact
-// update of the first subtile's rows, then the second's (row order: ties keep the lower row)
-template <int QT, bool kAsm>
-__device__ __forceinline__ void window_second(const i32x4 (&accw)[QT], const uint8_t* pw,
-                                              int roww, const i32x4 (&acc)[QT],
-                                              const uint8_t* pin, int rowb, const int (&wm)[QT],
-                                              int (&y1)[QT], int (&y2)[QT], int (&t2)[QT],
-                                              int (&id)[QT], bool vmem) {
-  uint64_t hit[QT];
-  uint64_t any = 0;
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    const int m = max(max(max(wm[t], accw[t][3]), acc[t][0]),
-                      max(max(acc[t][1], acc[t][2]), acc[t][3]));
-    hit[t] = __builtin_amdgcn_ballot_w64(m >= t2[t]);
-    any |= hit[t];
-  }
-#if SOD_I8_SGB
-#pragma unroll
-  for (int i = 0; i < 2 * QT; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);                            // MFMA
-    __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);                            // VALU
-    if (!kAsm && i >= 1 && i <= 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    if (vmem && i == 6) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);      // refill piece
-  }
-#endif
-  if (__builtin_expect(any != 0, 0)) {
-    const i32x4 p0 = parity_words<kAsm>(pw);
-    const i32x4 p1 = parity_words<kAsm>(pin);
-#pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      if (hit[t]) {
-        exact4(accw[t], p0, roww, y1[t], y2[t], id[t]);
-        exact4(acc[t], p1, rowb, y1[t], y2[t], id[t]);
-#if SOD_SHARED_T
-        int g1 = y1[t], g2 = y2[t];
-        top2_xor32(g1, g2);
-        top2_xor16(g1, g2);
-        t2[t] = max(t2[t], g2 >> 1);
-#else
-        t2[t] = max(t2[t], y2[t] >> 1);
-#endif
       }
     }
   }
@@ -634,16 +438,7 @@ __device__ __forceinline__ void match_unit(
                 "paired waves: odd subtiles sit 64 B after the even ones in the norm ring");
   const int qwave = wave % NQW, par = wave / NQW;   // query slice, subtile phase
   constexpr bool kAsm = SOD_I8_ASMLDS == 1 || (SOD_I8_ASMLDS == 2 && QT <= 2);
-  constexpr bool kWin = SOD_I8_PIPE && SOD_I8_SEED && SOD_I8_LAZYP && QT / PAIR <= SOD_I8_WINQT;
-  constexpr bool kDeep = SOD_I8_PIPE && SOD_I8_SEED && SOD_I8_LAZYP && !kWin &&
-                         QT / PAIR <= SOD_I8_DEEPQT;
   const int qt0 = (qb * NQW + qwave) * QT;
-#if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
-  const unsigned long long tu0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef SOD_I8_TIME2
-  unsigned long long tw_sum = 0, tw_seed = 0, tw_pro = 0, tw_vm = 0;
-#endif
   const int64_t s_lo = (int64_t)sp * sub_per_split;
   const int64_t s_hi = min(nsub, s_lo + sub_per_split);
   const int64_t nst = (s_hi - s_lo) / SPS;
@@ -655,12 +450,10 @@ __device__ __forceinline__ void match_unit(
     if (j < nst)
       issue_stage(dbpack, dn, npad, s_lo + j * SPS, lds + j * kStageBytes, nring + j * kStageNorm,
                   wave, lane);
-#if SOD_I8_DMA
   static_assert(kRing == 2, "spread refill: the slot refilled during stage s is stage s-1's");
   // the chunk's descriptors as one buffer (< 2 GiB: launch_match_i8 sizes the chunks)
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(dbpack + s_lo * kSub), (short)0, (int)((s_hi - s_lo) * kSub), kRsrcWord3);
-#endif
 
   i32x4 bq[QT][2];
 #pragma unroll
@@ -711,46 +504,17 @@ __device__ __forceinline__ void match_unit(
   uint8_t* const gl =
       lds + kRing * kStageBytes + kNormRing * kStageNorm + wq * (QT * 64 * GW);
   [[maybe_unused]] const int oslot = 1 + (sp & 1);   // this chunk's best-row word
-#if !SOD_I8_XWAIT
-  for (int i = lane; i < QT * 16 * GW; i += 64) reinterpret_cast<int*>(gl)[i] = INT_MIN;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // before the first threshold DMA
 #endif
-#endif
-#if SOD_I8_PIPE
   // accumulators, norms and first row of the subtile whose prefilter is pending; the
   // initial "previous subtile" is empty (h = INT_MIN can never pass t2)
   i32x4 accp[QT];
 #pragma unroll
   for (int t = 0; t < QT; ++t) accp[t] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
-#if SOD_I8_LAZYP
   const uint8_t* pp = nring;   // never read before it is set (accp cannot pass t2)
-#else
-  i32x4 pp = {0, 0, 0, 0};
-#endif
   int rowp = 0;
-  // the open window's first subtile (kWin): its accumulators, parity words, rows, partial max
-  [[maybe_unused]] i32x4 accw[QT];
-  [[maybe_unused]] int wm[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    accw[t] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
-    wm[t] = INT_MIN;
-  }
-  [[maybe_unused]] const uint8_t* pw = nring;
-  [[maybe_unused]] int roww = 0;
-  // the subtile before the pending one (kDeep)
-  [[maybe_unused]] i32x4 accq[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) accq[t] = i32x4{INT_MIN, INT_MIN, INT_MIN, INT_MIN};
-  [[maybe_unused]] const uint8_t* pq = nring;
-  [[maybe_unused]] int rowq = 0;
-#endif
 
   int slot = 0;
   for (int64_t s = 0; s < nst; ++s) {
-#ifdef SOD_I8_TIME2
-    const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
-#endif
     // the wave's loads of stage s are complete when at most the later prefetched stages'
     // loads remain in flight (vector memory returns in order)
     const int64_t younger = min<int64_t>(kRing - 2, nst - 1 - s);   // stages issued after s
@@ -760,19 +524,8 @@ __device__ __forceinline__ void match_unit(
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLoadsPerStage) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if SOD_I8_TIME2 == 2
-    tw_vm += __builtin_amdgcn_s_memtime() - tw0;   // the wave's own refill pieces
-#endif
-#ifndef SOD_I8_NOBAR   // (diagnostic timing build only: no stage barrier, WRONG results)
     __builtin_amdgcn_s_barrier();
-#endif
-#ifdef SOD_I8_TIME2
-    const unsigned long long tw1 = __builtin_amdgcn_s_memtime();
-    tw_sum += tw1 - tw0;
-    if (s == 0) tw_pro = tw1 - tu0;
-#endif
     // every wave has finished stage s-1, so its slot takes stage s+kRing-1
-#if SOD_I8_DMA
     // (descriptor pieces spread over this stage's first subtiles below; norms now)
     if (s + 1 < nst)
       issue_norms<NW16, kStageRows>(dn, npad, (s_lo + (s + 1) * SPS) * kSubRows,
@@ -783,13 +536,6 @@ __device__ __forceinline__ void match_unit(
     uint8_t* const refill = lds + (slot == 0 ? 1 : 0) * kStageBytes + wv * kPiecesPerWave * 1024;
     const uint32_t refill_off =
         (uint32_t)(min<int64_t>(s + 1, nst - 1) * kStageBytes + wv * kPiecesPerWave * 1024);
-#else
-    if (s + kRing - 1 < nst) {
-      const int ns = slot == 0 ? kRing - 1 : slot - 1;
-      issue_stage(dbpack, dn, npad, s_lo + (s + kRing - 1) * SPS, lds + ns * kStageBytes,
-                  nring + ((s + kRing - 1) % kNormRing) * kStageNorm, wave, lane);
-    }
-#endif
     // (the wave's subtile phase folded in: subtile u of the wave is u * PAIR + par)
     const uint8_t* sb = lds + slot * kStageBytes + par * kSub;
     const uint8_t* nb0 =
@@ -867,18 +613,10 @@ __device__ __forceinline__ void match_unit(
         }
       }
 #endif
-#ifdef SOD_I8_TIME2
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      tw_seed = __builtin_amdgcn_s_memtime() - tw1;
-#endif
     }
 #endif
     slot = slot + 1 == kRing ? 0 : slot + 1;
     i32x4 fa0[PF], fa1[PF], fc[PF];
-#if !SOD_I8_LAZYP
-    i32x4 fp[PF];
-#endif
-    static_assert(!kAsm || SOD_I8_LAZYP, "asm reads: the parity words stay on the slow path");
     [[maybe_unused]] const uint32_t sbl = lds_addr(sb) + lane * 16, nbl = lds_addr(nb0);
     if constexpr (kAsm) {
 #pragma unroll
@@ -893,39 +631,24 @@ __device__ __forceinline__ void match_unit(
       fa0[j] = *reinterpret_cast<const i32x4*>(sb + j * PAIR * kSub + lane * 16);
       fa1[j] = *reinterpret_cast<const i32x4*>(sb + j * PAIR * kSub + 1024 + lane * 16);
       fc[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j * PAIR, 0));
-#if !SOD_I8_LAZYP
-      fp[j] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(j * PAIR, 0) + kParOff);
-#endif
     }
     }
-#if SOD_I8_UNROLL
-#pragma unroll SOD_I8_UNROLL
-#else
 #pragma clang loop unroll(full)
-#endif
     for (int ju = 0; ju < SUBS; ++ju) {
       const int u = ju * PAIR;   // the wave's subtile (plus par, folded into sb / nb0 / rowl)
       const int js = ju % PF;    // a constant after unrolling
       // (asm reads) this subtile's three reads done; the subtiles' ahead may be in flight
       if constexpr (kAsm) lds_wait3(fa0[js], fa1[js], fc[js], 3 * min(PF - 1, SUBS - 1 - ju));
       const i32x4 a0 = fa0[js], a1 = fa1[js], c = fc[js];   // c = floor(-||d'||^2 / 2)
-#if SOD_I8_LAZYP
       const uint8_t* p = nb0 + norm_off(u, 0) + kParOff;   // norm_off(u, g) = norm_off(u, 0) + 16 g
-#else
-      const i32x4 p = fp[js];
-#endif
       i32x4 acc[QT];
 #pragma unroll
       for (int t = 0; t < QT; ++t)
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq[t][0], c, 0, 0, 0);
-#if SOD_I8_DMA
       // piece u of the next stage (wave-uniform branch; u is a constant after unrolling)
       const bool piece_here = ju < kPiecesPerWave;
       if (piece_here)
         issue_piece(rs, refill + ju * 1024, refill_off + ju * 1024, lane);
-#else
-      const bool piece_here = false;
-#endif
       if (kAsm && ju + PF < SUBS) {   // the fragments PF subtiles ahead in flight
         fa0[js] = lds_read16(sbl, (u + PF * PAIR) * kSub);
         fa1[js] = lds_read16(sbl, (u + PF * PAIR) * kSub + 1024);
@@ -936,41 +659,16 @@ __device__ __forceinline__ void match_unit(
         fa0[js] = *reinterpret_cast<const i32x4*>(nb);
         fa1[js] = *reinterpret_cast<const i32x4*>(nb + 1024);
         fc[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF * PAIR, 0));
-#if !SOD_I8_LAZYP
-        fp[js] = *reinterpret_cast<const i32x4*>(nb0 + norm_off(u + PF * PAIR, 0) + kParOff);
-#endif
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t)
         acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq[t][1], acc[t], 0, 0, 0);
       const int rowb = rowl + (int)((s * SPS + u) * kSubRows);
-#if SOD_I8_PIPE
       {
         // the pending subtile's index in the chunk decides dense / final / prefilter
         const int64_t kp = s * SPS + u - PAIR;
         const int mode = SOD_I8_SEED ? 0 : (kp < kDense - 1 ? 1 : (kp == kDense - 1 ? 2 : 0));
-        if constexpr (kWin) {
-          // the pending subtile opens a window when it is the stage's even one (stages hold an
-          // even number of the wave's subtiles, so windows never straddle a stage)
-          if (ju % 2 == 1) {
-            window_first<QT, kAsm>(accp, wm, piece_here);
-#pragma unroll
-            for (int t = 0; t < QT; ++t) accw[t] = accp[t];
-            pw = pp;
-            roww = rowp;
-          } else {
-            window_second<QT, kAsm>(accw, pw, roww, accp, pp, rowp, wm, y1, y2, t2, id,
-                                    piece_here);
-          }
-        } else if constexpr (kDeep) {
-          tile_update<QT, kAsm>(accq, pq, rowq, y1, y2, t2, id, false, 0, piece_here);
-#pragma unroll
-          for (int t = 0; t < QT; ++t) accq[t] = accp[t];
-          pq = pp;
-          rowq = rowp;
-        } else {
-          tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, kp < 64, mode, piece_here);
-        }
+        tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, mode, piece_here);
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t) accp[t] = acc[t];
@@ -991,10 +689,8 @@ __device__ __forceinline__ void match_unit(
               (uint32_t)((qw0 + r * nq_pad) * 4) + (uint32_t)lane * 16u, 0, 0,
               16 /* sc1: past this XCD's L2 */);
       }
-      if (share_apply(u) && xstage && (SOD_I8_SHARE2 == 0 || u != 12 || s > 0)) {
-#if SOD_I8_XWAIT
+      if (share_apply(u) && xstage) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         const int* gv = reinterpret_cast<const int*>(gl) + (lane & 15);
         // publishing is a device-scope atomic per query (a memory-side transaction each):
         // every stage while the thresholds still move fast, then every kPublishEvery-th
@@ -1029,41 +725,13 @@ __device__ __forceinline__ void match_unit(
         }
       }
 #endif
-#else
-      tile_update<QT, kAsm>(acc, p, rowb, y1, y2, t2, id);
-#endif
     }
   }
   // LDS-DMA still in flight (the last stage's refill pieces re-read that stage, a shared-
   // threshold load) must land before the work-group's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if SOD_I8_PIPE
-  if constexpr (kWin) {   // the last subtile closes the last window
-    static_assert(SUBS % 2 == 0, "windows of two subtiles tile a stage");
-    window_second<QT, kAsm>(accw, pw, roww, accp, pp, rowp, wm, y1, y2, t2, id, false);
-  } else if constexpr (kDeep) {   // the last two subtiles, in row order
-    tile_update<QT, kAsm>(accq, pq, rowq, y1, y2, t2, id, false, 0);
-    tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, false, 0);
-  } else {
-    tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id, false,
-                          !SOD_I8_SEED && nst * SPS <= kDense ? 1 : 0);
-  }
-#endif
-#ifdef SOD_I8_COUNT
-  if (lane == 0) atomicAdd(&g_counts[2], (unsigned long long)(nst * SPS));
-#endif
-#ifdef SOD_I8_TIME
-  if (lane == 0) atomicAdd(&g_tm[(blockIdx.x * 8 + wave) & 32767][2], __builtin_amdgcn_s_memtime() - tu0);
-#endif
-#ifdef SOD_I8_TIME2
-  if (lane == 0) {
-    unsigned long long* const g = g_tm[(blockIdx.x * NW16 + wave) & 32767];
-    atomicAdd(&g[0], tw_sum);
-    atomicAdd(&g[1], SOD_I8_TIME2 == 2 ? tw_vm : tw_seed);   // (2: the vmcnt part of [0])
-    atomicAdd(&g[2], __builtin_amdgcn_s_memtime() - tu0);
-    atomicAdd(&g[3], tw_pro);
-  }
-#endif
+  tile_update<QT, kAsm>(accp, pp, rowp, y1, y2, t2, id,
+                        !SOD_I8_SEED && nst * SPS <= kDense ? 1 : 0);
 
   if constexpr (PAIR == 2) {
     // the odd-phase wave hands its lanes' top-2 to the even-phase wave of the same queries
@@ -1104,11 +772,6 @@ __device__ __forceinline__ void match_unit(
   }
 }
 
-#ifdef SOD_I8_STAMP
-// diagnostic build only: per work-group (s_memtime, s_memrealtime) at start and end, for
-// the in-kernel clock = d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS)
-__device__ unsigned long long g_stamps[4096][8];
-#endif
 
 template <int QT, int PF, int PAIR>
 #ifndef SOD_I8_MINB
@@ -1125,14 +788,6 @@ __global__ __launch_bounds__(NT16, SOD_I8_MINB) void match_i8_kernel(
     int seedload) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kStageBytes + kNormRing * kStageNorm +
                                                      SOD_I8_XCHUNK * NW16 * QT * 64 * gwords<QT / PAIR>()];
-#ifdef SOD_I8_STAMP
-  unsigned long long t0 = 0, r0 = 0;
-  if (threadIdx.x == 0) {
-    t0 = __builtin_amdgcn_s_memtime();
-    r0 = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
-#if SOD_I8_XCD
   // XCD-aware order: blocks b, b+8, ... share an XCD (and its L2); give each such group a
   // contiguous run of chunk-major units, so an XCD streams one or two DB chunks, in step,
   // instead of all of them (bijective for any grid size; cdna_hip_programming.md T1)
@@ -1140,25 +795,6 @@ __global__ __launch_bounds__(NT16, SOD_I8_MINB) void match_i8_kernel(
   const unsigned u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + blockIdx.x / 8;
   match_unit<QT, PF, PAIR>(lds, (int)(u / nqb), (int)(u % nqb), dbpack, dn, nsub, qpack, qn, nqt, nq_pad,
              sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
-#else
-  match_unit<QT, PF, PAIR>(lds, blockIdx.x % split, blockIdx.x / split, dbpack, dn, nsub, qpack, qn, nqt,
-             nq_pad, sub_per_split, row_offset, pd1, pidx, pd2, gthr, seedload);
-#endif
-#ifdef SOD_I8_STAMP
-  if (threadIdx.x == 0 && blockIdx.x < 4096) {
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
-    g_stamps[blockIdx.x][0] = t0;
-    g_stamps[blockIdx.x][1] = r0;
-    g_stamps[blockIdx.x][2] = t1;
-    g_stamps[blockIdx.x][3] = r1;
-    unsigned hwid, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_stamps[blockIdx.x][4] = hwid;
-    g_stamps[blockIdx.x][5] = xcc;
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1217,7 +853,6 @@ __device__ __forceinline__ void tile_update_w(const i32x16& acc, const uint8_t* 
   const int ma = max(max(max(max(max(max(acc[0], acc[1]), acc[2]), acc[3]), acc[4]), acc[5]), acc[6]);
   const int mb = max(max(max(max(max(max(acc[7], acc[8]), acc[9]), acc[10]), acc[11]), acc[12]), acc[13]);
   const int m = max(max(ma, mb), max(acc[14], acc[15]));
-#if SOD_I8_SGB
   // interleave: MFMA, MFMA, 4 VALU, MFMA, 5 VALU, MFMA (the previous tile's MFMA result
   // is read two MFMAs after its last MFMA)
   __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
@@ -1225,7 +860,6 @@ __device__ __forceinline__ void tile_update_w(const i32x16& acc, const uint8_t* 
   __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
   __builtin_amdgcn_sched_group_barrier(0x2, 5, 0);
   __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-#endif
   if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= t2) != 0, 0)) {
     // scalar row base materialised inside the slow path (readfirstlane is convergent, so
     // the 16 row numbers are not hoisted into the hot block as vector adds)
@@ -1242,13 +876,9 @@ __device__ __forceinline__ void tile_update_w(const i32x16& acc, const uint8_t* 
         y1 = gt ? y : y1;
       }
     }
-#if SOD_SHARED_T
     int g1 = y1, g2 = y2;
     top2_xor32(g1, g2);
     t2 = g2 >> 1;
-#else
-    t2 = y2 >> 1;
-#endif
   }
 }
 
@@ -1516,33 +1146,6 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   SOD_HIP(ctx, hipGetLastError());
   return SOD_OK;
 }
-
-#if defined(SOD_I8_TIME) || defined(SOD_I8_TIME2)
-extern "C" int sod_debug_times(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tm), sizeof(g_tm)) != hipSuccess) return 1;
-  if (reset) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_tm)) != hipSuccess) return 1;
-    if (hipMemset(p, 0, sizeof(g_tm)) != hipSuccess) return 1;
-  }
-  return 0;
-}
-#endif
-#ifdef SOD_I8_COUNT
-extern "C" int sod_debug_counts(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_counts), 64) != hipSuccess) return 1;
-  if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_counts), z, 64) != hipSuccess) return 1;
-  }
-  return 0;
-}
-#endif
-#ifdef SOD_I8_STAMP
-extern "C" int sod_debug_stamps(unsigned long long* out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 64) == hipSuccess ? 0 : 1;
-}
-#endif
 
 // Query tiles per wave for the 16x16x64 kernel.  A work-group holds 8*QT tiles; the chip is
 // filled by splitting the DB into chunks, and every chunk restarts its queries' top-2 (the

@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -75,9 +76,13 @@ struct sod_opts {
   int sift_early_desc = 1;     // 0: descriptors after the sort, of the final list
   int sift_direct = 1;         // 0: a lone image's results copied after the sync
   int sift_eager_rank = 0;     // 1: the rank-path launches always enqueued with the sort
-  int affine_fma = 0;          // 1: remove_outliers' np.matmul(M, X) as fma(m1, x, m2 y) (the
+  int affine_fma = 0;          // remove_outliers' np.matmul(M, X): 1 fma(m1, x, m2 y), 2 fma(m2, y, m1 x) (the
                                // host numpy's dgemv on an FMA CPU; set by the Python layer)
   int debug_sync = 0;          // 1: stderr trace of long stream waits and stream re-creation
+  int trig_exact = -1;         // -1: the probe decides (sod_host_trig_matches_device); 0: the
+                               // fallback forced -- boundary guard + host exact-means redo armed
+                               // as on a host whose libm differs (parity tests of that path);
+                               // 1: refused unless the probe agrees
 };
 
 struct sod_ctx {
@@ -279,6 +284,7 @@ struct sod_ctx {
   // process, sod_host_trig_matches_device): poses, bins and PoseBin means are the reference's
   // without the boundary guard's host redo or the exact-means redo, which stay armed otherwise
   bool trig_exact = false;
+  bool trig_probe = false;    // the probe's own answer (opt.trig_exact may force the fallback)
   // sod_exact_xy_means: bin list + record offsets, the pose records, their pinned host copy
   DevBuf<int32_t> xr_idx;
   DevBuf<double> xr_rec;
@@ -295,6 +301,7 @@ struct sod_ctx {
   // is on XCD i % 8) run the context / side streams; the matcher stream gets the rest
   int cu_reserve = 0;
   int reserved_cus = 0;
+  int64_t host_wait_ns = 0;     // host time blocked in enqueue calls on the slot wait
   int pslot = 0;                // partial-result slot of the last matcher launch
   int64_t pslot_n = 0;          // its size (elements per array)
 
@@ -323,7 +330,9 @@ struct sod_ctx {
 // polling returns within a query's cost of the end.  Longer waits (C3's 3.7 ms matcher)
 // fall back to the blocking call after the spin.
 constexpr int kSpinUs = 400;
-inline int sod_debug_sync = 0;   // any context's "debug_sync" option (diagnostics only)
+// live contexts whose "debug_sync" option is on (diagnostics only; counted, so one context
+// switching it off does not turn it off for another)
+inline std::atomic<int> sod_debug_sync{0};
 inline hipError_t sod_stream_sync(hipStream_t s) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {

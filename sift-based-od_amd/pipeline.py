@@ -208,7 +208,10 @@ class Main:
     def get_valid_bins(self, threshold=5):
         """``main.py:121-132``: bins with votes >= threshold, insertion order.  The bins'
         members stay on the device (``keypoint_pairs`` is built when first read), and so
-        does ``self.keypoint_pairs`` (a lazy concatenation)."""
+        does ``self.keypoint_pairs`` (a lazy concatenation).  As in the reference, a repeated
+        call appends only the bins not yet in ``valid_bins`` (which keeps the earlier
+        calls' bins), while ``keypoint_pairs`` is rebuilt from the bins at THIS call's
+        threshold alone, in hough_transform's insertion order (main.py:123-129)."""
         if self._stage == "assigned":
             vb = [b for b in self._table.values() if b.votes >= threshold]
         else:
@@ -237,7 +240,7 @@ class Main:
             if b.pose not in seen:
                 seen.add(b.pose)
                 self.valid_bins.append(b)
-        self.keypoint_pairs = _LazyPairs(self.valid_bins)
+        self.keypoint_pairs = _LazyPairs(vb)          # main.py:123,129: this threshold's bins
         self._valid_thr = threshold
 
     def update_keypoint_pairs(self):
@@ -253,7 +256,9 @@ class Main:
         tok, res = self._valid_sel
         vb = self.valid_bins
         if isinstance(vb, _DeviceBins) and vb.unbuilt():   # untouched since the selection
-            return vb.token == tok
+            # ... and that selection is still the device's (reading hough_transform selects
+            # again, at threshold 1)
+            return vb.token == tok == self._sel_token
         if tok != self._sel_token or len(self.valid_bins) != len(res["keys"]):
             return False
         return all(b.device_index(tok) == i for i, b in enumerate(self.valid_bins))

@@ -49,6 +49,12 @@ class RcclComm:
         uid = _lib.unique_id() if rank == 0 else None
         uid = broadcast_bytes(uid)
         ctx.comm_init(world, rank, uid)
+        self._ctx = ctx
+
+    def info(self):
+        """The communicator as RCCL itself reports it: {"kind", "nranks", "rank"}."""
+        n, r = self._ctx.comm_info()
+        return {"kind": self.kind, "nranks": n, "rank": r}
 
     def gather_candidates(self, ctx):
         ctx.match_allgather()
@@ -67,6 +73,10 @@ class HostComm:
         self._allgather = allgather
         self._allreduce = allreduce
 
+    def info(self):
+        """{"kind": "host", "nranks", "rank"}: the host exchange's own world (no RCCL)."""
+        return {"kind": self.kind, "nranks": self.world, "rank": self.rank}
+
     def gather_candidates(self, ctx):
         d1, idx, d2 = ctx.candidates()
         g1 = np.concatenate(self._allgather(d1))
@@ -79,6 +89,16 @@ class HostComm:
         cnt = self._allreduce(cnt.astype(np.int64), "sum").astype(np.uint32)
         fst = self._allreduce(fst.astype(np.int64), "min").astype(np.uint32)
         ctx.set_hough_partial(cnt, fst)
+
+
+def _store_file(name):
+    """A name a FileStore writes: ``gen``, ``<32 hex>_<key>``, ``.<name>.<rank>.tmp``, or one
+    of its own keys (join / ready / broadcast / all-gather / done) under any hex generation
+    or none (the files of a crashed run of an older format)."""
+    import re
+    return bool(name == "gen" or re.fullmatch(r"[0-9a-f]{32}_.+", name)
+                or re.fullmatch(r"\..+\.\d+\.tmp", name)
+                or re.fullmatch(r"(?:[0-9a-f]+_)?(?:ready|join_\d+|done_\d+|b\d+|g\d+_\d+)", name))
 
 
 class FileStore:
@@ -107,9 +127,11 @@ class FileStore:
         import os
         import tempfile
         self.world, self.rank, self.timeout = world, rank, timeout
+        self._own_dir = False
         if path is None:
             path = os.environ.get("SOD_STORE_DIR")
         if path is None:
+            self._own_dir = True          # sod_store_<run id>: made for this run, removed whole
             run = os.environ.get("TORCHELASTIC_RUN_ID")
             if not run or run == "none":
                 run = "%s_%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
@@ -134,11 +156,12 @@ class FileStore:
         import uuid
         t0 = time.perf_counter()
         if self.rank == 0:
-            for name in os.listdir(self.path):   # an earlier run's leftovers
-                try:
-                    os.remove(os.path.join(self.path, name))
-                except OSError:
-                    pass
+            for name in os.listdir(self.path):   # an earlier run's leftovers -- only files a
+                if _store_file(name):             # store writes (the path may be shared)
+                    try:
+                        os.remove(os.path.join(self.path, name))
+                    except OSError:
+                        pass
             self.gen = uuid.uuid4().hex
             self._put("gen", self.gen.encode())
             nonces = {}
@@ -251,9 +274,22 @@ class FileStore:
         self.barrier()                   # every rank has read everything it will read
         self.set("done_%d" % self.rank, b"")
         if self.rank == 0:
+            import os
             for r in range(self.world):
                 self.get("done_%d" % r)
-            shutil.rmtree(self.path, ignore_errors=True)
+            if self._own_dir:
+                shutil.rmtree(self.path, ignore_errors=True)
+            else:                        # a caller's directory: only the store's own files,
+                for name in os.listdir(self.path):   # then the directory if that emptied it
+                    if _store_file(name):
+                        try:
+                            os.remove(os.path.join(self.path, name))
+                        except OSError:
+                            pass
+                try:
+                    os.rmdir(self.path)
+                except OSError:
+                    pass
 
 
 class FileHostComm(HostComm):

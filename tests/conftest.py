@@ -40,3 +40,16 @@ def ctx(_ctx_session):
     yield _ctx_session
     for k, v in opts.items():          # a test's set_option stays in that test
         _ctx_session.set_option(k, v)
+
+
+@pytest.fixture(params=["auto", "fallback"])
+def trig(request, ctx):
+    """The device-trig parity mode (sod option trig_exact): "auto" = the probe's answer (on a
+    glibc-2.35 FMA host the device cos / sin are the host's and nothing is redone);
+    "fallback" = forced off, so the boundary guard (hough.hip sod_guard_resolve) and the host
+    exact-means redo (sod_exact_xy_means) run as on a host whose libm differs.  The ctx
+    fixture restores the option afterwards."""
+    ctx.set_option("trig_exact", -1 if request.param == "auto" else 0)
+    if request.param == "fallback":
+        assert not ctx.trig_exact()
+    return request.param

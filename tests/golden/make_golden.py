@@ -625,10 +625,65 @@ def main_keypoints():
         save("kpfields_" + name, **out)
 
 
+def main_repeat():
+    """get_valid_bins called twice on the same votes (main.py:121-132): ``valid_bins``
+    accumulates (earlier bins kept, new ones appended in insertion order) while
+    ``keypoint_pairs`` is rebuilt from the bins at the latest threshold only; then
+    apply_affine_parameters(4) on the accumulated list.  The edge_b15 and near_edge_b15
+    matches (votes spread over 1..12+); threshold sequences (5, 7), (7, 5) and (9, 3);
+    written to repeat_<case>.npz."""
+    import sod_pkg
+    sod_pkg.load()
+    ref_main, _ = import_reference()
+    from sift_based_od_amd.database import Keypoints
+    for name in ("edge_b15", "near_edge_b15"):
+        g = dict(np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False))
+        qkp = Keypoints(g["q_x"], g["q_y"], g["q_angle"], g["q_octave"])
+        dbkp = Keypoints(g["db_x"], g["db_y"], g["db_angle"], g["db_octave"])
+        shape = tuple(int(v) for v in g["shape"])
+        bins = int(g["bins"])
+        matches = [(int(q), int(m)) for q, m in zip(g["match_q"], g["match_m"])]
+        out = {}
+        for a, b in ((5, 7), (7, 5), (9, 3)):
+            M = ref_main.Main()
+            M.rgb_query = types.SimpleNamespace(shape=shape)
+            M.image_query_size = (shape[1], shape[0])
+            kq, km = kp_objects(qkp), kp_objects(dbkp)
+            ident = {}
+            for q, m in matches:
+                im = int(g["db_img"][m])
+                M.matching_keypoints.append(
+                    (km[m], kq[q], (int(g["size"][im][0]), int(g["size"][im][1])),
+                     (float(g["centroid"][im][0]), float(g["centroid"][im][1]))))
+                ident[(id(km[m]), id(kq[q]))] = q
+            M.apply_hough_transform(bins)
+            tag = "t%d_%d_" % (a, b)
+            for step, thr in enumerate((a, b)):
+                M.get_valid_bins(thr)
+                out[tag + "valid_keys%d" % step] = np.array([x.pose for x in M.valid_bins],
+                                                           np.int32).reshape(-1, 4)
+                out[tag + "pairs%d" % step] = np.array([ident[(id(p[0]), id(p[1]))]
+                                                       for p in M.keypoint_pairs], np.int32)
+            M.apply_affine_parameters(4)
+            sv = M.valid_bins
+            out[tag + "surv_keys"] = np.array([x.pose for x in sv], np.int32).reshape(-1, 4)
+            out[tag + "surv_votes"] = np.array([x.votes for x in sv], np.int32)
+            out[tag + "surv_params"] = np.array([list(map(float, x.affine_parameters))
+                                                 for x in sv], np.float64).reshape(-1, 6)
+            out[tag + "surv_pairs"] = np.array([ident[(id(p[0]), id(p[1]))]
+                                                for p in M.keypoint_pairs], np.int32)
+            print(name, "repeat", a, b, "valid",
+                  [len(out[tag + "valid_keys%d" % k]) for k in (0, 1)],
+                  "pairs", [len(out[tag + "pairs%d" % k]) for k in (0, 1)], "surv", len(sv))
+        save("repeat_" + name, **out)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["near_edge"]:
         main_near_edge()
     elif sys.argv[1:] == ["keypoints"]:
         main_keypoints()
+    elif sys.argv[1:] == ["repeat"]:
+        main_repeat()
     else:
         main()

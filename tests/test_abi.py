@@ -98,15 +98,21 @@ def test_results_struct_layout(tmp_path):
 
 def test_numpy_matmul_probe():
     """The Python layer's probe of how this host's numpy rounds remove_outliers' 2x2 product
-    (AffineParameters.py:145): 1 = fma(m1, x, m2*y) on every probed value, 0 otherwise; it
-    agrees with a second, independent sample."""
+    (AffineParameters.py:145) on BOTH output rows: 1 = fma(m_r0, x, m_r1*y), 2 =
+    fma(m_r1, y, m_r0*x), 0 = two roundings; a second, independent sample (other matrices,
+    both rows) is rounded exactly as the mode says."""
     from fractions import Fraction
     import numpy as np
+
+    def fma(a, b, c):
+        return float(Fraction(a) * Fraction(b) + Fraction(c))
     got = _lib.numpy_matmul_fma()
-    assert got in (0, 1)
+    assert got in (0, 1, 2)
+    assert _lib.MATMUL_FMA_CONSISTENT
     rng = np.random.default_rng(99)
-    same = []
-    for m1, m2, x, y in rng.uniform(-3, 3, (200, 4)) * [1, 1, 500, 500]:
-        r = float(np.matmul([[m1, m2], [0.0, 1.0]], [x, y])[0])
-        same.append(r == float(Fraction(m1) * Fraction(x) + Fraction(float(m2 * y))))
-    assert all(same) == bool(got)
+    for a, b, c, d, x, y in rng.uniform(-3, 3, (200, 6)) * [1, 1, 1, 1, 500, 500]:
+        r = np.matmul([[a, b], [c, d]], [x, y]).tolist()
+        for m0, m1, v in ((a, b, r[0]), (c, d, r[1])):
+            want = (fma(m0, x, m1 * y) if got == 1 else fma(m1, y, m0 * x) if got == 2
+                    else m0 * x + m1 * y)
+            assert v == want

@@ -57,4 +57,14 @@ def test_bench_two_ranks_host_comm(tmp_path):
     assert d["config"]["db_rows_total"] == 2 * d["config"]["db_rows_per_gpu"]
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["scaling"] == "weak"
     assert d["good_matches"] > 0 and d["valid_bins"] > 0
+    # self-verifying record: every rank's communicator and the winners each shard gave
+    assert d["config"]["rccl_nranks"] is None          # --comm host: no RCCL communicator
+    assert [r["rank"] for r in d["ranks"]] == [0, 1]
+    assert [r["comm"] for r in d["ranks"]] == [{"kind": "host", "nranks": 2, "rank": k}
+                                               for k in range(2)]
+    assert all(r["shard_winners"] == d["shard_winners"] for r in d["ranks"])
+    assert all(r["shard_good_winners"] == d["shard_good_winners"] for r in d["ranks"])
+    assert sum(d["shard_winners"]) == d["config"]["queries"] and min(d["shard_winners"]) > 0
+    assert sum(d["shard_good_winners"]) == d["good_matches"]
+    assert [r["own_shard_winners"] for r in d["ranks"]] == d["shard_winners"]
     assert not any(n.startswith("sod_store_") for n in os.listdir(tmp_path))   # store removed

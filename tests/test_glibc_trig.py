@@ -15,6 +15,7 @@ import math
 import os
 import shutil
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -32,6 +33,29 @@ def test_host_restatement_equals_host_libm(tmp_path):
     out = subprocess.run([str(exe), "300000"], capture_output=True, text=True, timeout=300)
     print(out.stdout)
     assert out.returncode == 0 and out.stdout.strip().endswith("OK"), out.stdout
+
+
+def test_table_generator_refuses_other_libm(tmp_path):
+    """tools/gen_glibc_trig.py reads fixed file offsets of ONE libm build: it regenerates the
+    committed glibc_trig_tab.h exactly from the library whose sha256 the header records, and
+    refuses (no output) any other file."""
+    import hashlib
+    gen = os.path.join(REPO, "tools", "gen_glibc_trig.py")
+    tab = open(os.path.join(REPO, "sift-based-od_amd", "csrc", "glibc_trig_tab.h")).read()
+    libm = "/lib/x86_64-linux-gnu/libm.so.6"
+    recorded = tab.split('#define GT_LIBM_SHA256 "')[1].split('"')[0]
+    if not os.path.exists(libm) or hashlib.sha256(open(libm, "rb").read()).hexdigest() != recorded:
+        pytest.skip("this host's libm is not the recorded build (the device path's probe, "
+                    "sod_trig_exact, then arms the host-libm fallback)")
+    r = subprocess.run([sys.executable, gen, "--check"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    # any other file: refused before a byte is emitted
+    other = tmp_path / "libm.so.6"
+    other.write_bytes(open(libm, "rb").read()[:-1] + b"\x01")
+    code = ("import runpy, sys; sys.argv = ['gen']; g = runpy.run_path(%r, run_name='x'); "
+            "g['load'](%r)" % (gen, str(other)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
+    assert r.returncode != 0 and "refusing" in (r.stderr + r.stdout)
 
 
 def _libm_sincos(x):

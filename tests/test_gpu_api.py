@@ -92,10 +92,16 @@ def test_perform_hough_transform_and_affine_dropins(name):
         assert changed == ch_ref and v.votes == sum(keep_ref) and n0 == len(keep_ref)
 
 
-def test_main_stages_match_golden():
+@pytest.mark.parametrize("trig", ["auto", "fallback"])
+def test_main_stages_match_golden(trig):
+    """main.py's stage sequence through Main against the reference's outputs; "fallback"
+    forces the host-libm redo paths (option trig_exact 0: boundary guard, exact means of
+    the survivors, pipeline.py) that a host whose libm differs from the device's takes."""
     g = golden("planted_b15")
     db = sod.SiftDatabase(g["db_des"], kp(g, "db_"), g["db_img"], g["centroid"], g["size"])
     m = sod.Main()
+    m.ctx.set_option("trig_exact", -1 if trig == "auto" else 0)
+    assert trig == "auto" or not m.ctx.trig_exact()
     m.set_database(db)
     m.get_query_features(g["q_des"], kp(g, "q_"), tuple(int(v) for v in g["shape"]))
     m.run_matcher()
@@ -124,6 +130,69 @@ def test_main_stages_match_golden():
     # survivors' centroids redone with glibc (sod_exact_means): main.py's final pose exactly
     assert np.array_equal(got.reshape(-1, 6).view(np.uint64),
                           np.asarray(g["final_pose"], np.float64).reshape(-1, 6).view(np.uint64))
+
+
+def _main_on_given_matches(g, seed=3):
+    """A Main whose run_matcher finds exactly the golden's (match_q, match_m) pairs: random
+    DB descriptors, query q's descriptor = DB row match_m[q] (d1 = 0, ratio test passes)."""
+    rng = np.random.default_rng(seed)
+    ndb, nq = len(g["db_x"]), len(g["q_x"])
+    assert np.array_equal(g["match_q"], np.arange(nq))        # every query is matched
+    db_des = rng.integers(0, 256, (ndb, 128)).astype(np.uint8)
+    m = sod.Main()
+    m.set_database(sod.SiftDatabase(db_des, kp(g, "db_"), g["db_img"], g["centroid"], g["size"]))
+    m.get_query_features(db_des[g["match_m"]], kp(g, "q_"), tuple(int(v) for v in g["shape"]))
+    m.run_matcher()
+    assert len(m.matching_keypoints) == nq
+    return m
+
+
+def _pair_queries(m, pairs):
+    qid = {id(v): k for k, v in m.kp_query._cache.items()}
+    return np.array([qid[id(p[1])] for p in pairs], np.int64)
+
+
+@pytest.mark.parametrize("name", ["edge_b15", "near_edge_b15"])
+@pytest.mark.parametrize("seq", [(5, 7), (7, 5), (9, 3)])
+@pytest.mark.parametrize("path", ["device", "tuples"])
+def test_get_valid_bins_repeated(name, seq, path):
+    """get_valid_bins called twice (main.py:121-132), against the reference run the same way
+    (repeat_<case> goldens): valid_bins keeps the first call's bins and appends the second
+    call's new ones in insertion order; keypoint_pairs holds only the LATEST threshold's bins'
+    pairs, in hough_transform order; apply_affine_parameters then verifies the accumulated
+    list.  ``tuples``: the matches assigned as tuples (the host-table path)."""
+    g, r = golden(name), golden("repeat_" + name)
+    m = _main_on_given_matches(g)
+    if path == "tuples":
+        m.matching_keypoints = list(m.matching_keypoints)
+    m.apply_hough_transform(int(g["bins"]))
+    tag = "t%d_%d_" % seq
+    for step, thr in enumerate(seq):
+        m.get_valid_bins(thr)
+        assert [b.pose for b in m.valid_bins] == [tuple(k) for k in r[tag + "valid_keys%d" % step]]
+        assert np.array_equal(_pair_queries(m, m.keypoint_pairs), r[tag + "pairs%d" % step])
+    m.apply_affine_parameters(4)
+    assert [b.pose for b in m.valid_bins] == [tuple(k) for k in r[tag + "surv_keys"]]
+    assert [b.votes for b in m.valid_bins] == list(r[tag + "surv_votes"])
+    for b, prm in zip(m.valid_bins, r[tag + "surv_params"]):
+        np.testing.assert_allclose(b.affine_parameters, prm, rtol=0, atol=1e-4)
+    assert np.array_equal(_pair_queries(m, m.keypoint_pairs), r[tag + "surv_pairs"])
+
+
+def test_hough_read_between_select_and_affine():
+    """Reading hough_transform after get_valid_bins selects again on the device (threshold 1);
+    apply_affine_parameters must still verify get_valid_bins' bins (the
+    device-resident shortcut checks that the device selection is still that one)."""
+    g = golden("edge_b15")
+    m = _main_on_given_matches(g)
+    m.apply_hough_transform(int(g["bins"]))
+    m.get_valid_bins(5)
+    assert len(m.hough_transform) == len(g["table_keys"])
+    m.apply_affine_parameters(4)
+    assert [b.pose for b in m.valid_bins] == [tuple(k) for k in g["surv_keys"]]
+    assert [b.votes for b in m.valid_bins] == list(g["surv_votes"])
+    for b, prm in zip(m.valid_bins, g["surv_params"]):
+        np.testing.assert_allclose(b.affine_parameters, prm, rtol=0, atol=1e-4)
 
 
 def _kf_rows(kps):
@@ -284,6 +353,10 @@ def test_rccl_single_rank_collectives():
         with _lib.Context(0) as c:
             if use_comm:
                 c.comm_init(1, 0, _lib.unique_id())
+                assert c.comm_info() == (1, 0)          # as RCCL reports it
+            else:
+                with pytest.raises(_lib.SodError):      # no communicator yet
+                    c.comm_info()
             c.set_keypoints(db.kp, db.img, db.centroid, db.size)
             c.upload_db(db.des)
             c.upload_queries(qs.des, qs.kp)
@@ -805,8 +878,34 @@ def test_outlier_test_rounding_follows_numpy():
         ref = [orc.remove_outliers(p, [(q[0], q[1])], [(q[2], q[3])], 1, (2048, 2048),
                                    128.0, 128.0)[0][0] for p, q in zip(prm, pts)]
         assert np.array_equal(r["alive"], np.array(ref)), (fma, int((r["alive"] != ref).sum()))
-        c.set_option("affine_fma", 1 - fma)    # the other rounding disagrees on every member
+        c.set_option("affine_fma", 0 if fma else 1)   # the other rounding disagrees on every member
         r2 = c.affine_batch(np.arange(n + 1), pts[:, 0], pts[:, 1], pts[:, 2], pts[:, 3],
                             np.ones(n, np.int32), (2048, 2048), 128.0, 128.0, threshold=0,
                             max_iter=1, params_in=prm)
         assert not np.any(r2["alive"] == np.array(ref))
+
+
+def test_set_option_validation(ctx):
+    """option values outside the int range are refused (not wrapped: 2^32-2 would
+    become -2, a 'default' sentinel); trig_exact takes -1 / 0 / 1, and 1 only when the host
+    libm probe agrees; debug_sync is counted per context (one context turning it off leaves
+    another's on)."""
+    for v in (2 ** 32 - 2, -(2 ** 31) - 1, 2 ** 40):
+        with pytest.raises(_lib.SodError):
+            ctx.set_option("sift_sort_max", v)
+    assert ctx.get_option("sift_sort_max") == -2
+    with pytest.raises(_lib.SodError):
+        ctx.set_option("trig_exact", 2)
+    ctx.set_option("trig_exact", 0)
+    assert not ctx.trig_exact()
+    ctx.set_option("trig_exact", -1)
+    if ctx.trig_exact():
+        ctx.set_option("trig_exact", 1)
+        assert ctx.trig_exact()
+    else:
+        with pytest.raises(_lib.SodError):
+            ctx.set_option("trig_exact", 1)
+    with _lib.Context(0) as other:
+        other.set_option("debug_sync", 1)
+        ctx.set_option("debug_sync", 0)
+        assert other.get_option("debug_sync") == 1

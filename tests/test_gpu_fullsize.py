@@ -29,7 +29,7 @@ def c3():
     return db, qs
 
 
-def test_c3_full_pipeline(ctx, c3):
+def test_c3_full_pipeline(ctx, c3, trig):
     db, qs = c3
     ctx.set_impl("i8")
     ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)

@@ -430,7 +430,7 @@ def test_pose_sweep(ctx):
         assert np.array_equal(pose[:, 2:], g["poses"][:, 2:])
 
 
-def test_pose_near_edge_guard(ctx):
+def test_pose_near_edge_guard(ctx, trig):
     """Poses within a few ulps of an x AND a y bin edge (make_golden.near_edge_sweep):
     indices AND x, y equal the reference's bit for bit.  With the device's glibc cos / sin
     (sod_trig_exact, round 5) no guard is armed and nothing is listed; on a host whose libm
@@ -487,7 +487,7 @@ def test_pipeline_golden(ctx, name, impl):
 
 
 @pytest.mark.parametrize("name", ["edge_b15", "edge_b6", "near_edge_b15", "near_edge_b32"])
-def test_hough_affine_edges(ctx, name):
+def test_hough_affine_edges(ctx, name, trig):
     g = golden(name)
     ctx.set_keypoints(kp(g, "db_"), g["db_img"], g["centroid"], g["size"])
     ctx.upload_queries(None, kp(g, "q_"))
@@ -563,7 +563,7 @@ def _same_hough(a, b):
 
 @pytest.mark.parametrize("name,ngroups", [("near_edge_b15", 78), ("near_edge_b32", 78),
                                           ("edge_b15", 0), ("edge_b6", 0)])
-def test_fused_hough_select_equals_dense(ctx, name, ngroups):
+def test_fused_hough_select_equals_dense(ctx, name, ngroups, trig):
     """The fused one-image launch (hough_small_kernel: pose, votes from a base-key hash, valid
     bins, members, affine inputs) equals the dense path (pose_kernel + hist_kernel +
     select_small_kernel + affine_gather_kernel) bit for bit -- bin table, valid bins, members,

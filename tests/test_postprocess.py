@@ -122,7 +122,7 @@ def test_device_post_batch_vs_oracle(ctx, n, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c1_b15", "planted_b15", "planted_b12"])
-def test_pipeline_postprocess_golden(ctx, name):
+def test_pipeline_postprocess_golden(ctx, name, trig):
     """Full device pipeline then post-processing over the survivors == main.py's final
     pose bit for bit (with the device's glibc cos / sin even without the host's redo of the
     survivors' x / y means, sod_set_post_exact(0))."""
@@ -152,7 +152,7 @@ def test_pipeline_postprocess_golden(ctx, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["edge_b15", "edge_b6"])
-def test_stage_api_postprocess_golden(ctx, name):
+def test_stage_api_postprocess_golden(ctx, name, trig):
     """Stage entry points on the golden matches (hough -> select -> affine), then the
     device post-processing over the survivors -> main.py's final_pose."""
     from helpers import kp

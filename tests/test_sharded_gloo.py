@@ -237,6 +237,28 @@ def test_file_store_ignores_an_unclosed_runs_files(tmp_path):
     assert not path.exists()   # close() removed the directory
 
 
+def test_file_store_keeps_unrelated_files(tmp_path):
+    """SOD_STORE_DIR may be a shared directory; a run there removes only the
+    files a store writes (its own and a crashed run's), never the directory's other files."""
+    import multiprocessing as mp
+    path = tmp_path / "shared"
+    path.mkdir()
+    for name in ("notes.txt", "gen2", "abc_def", "data.npz"):
+        (path / name).write_bytes(b"keep")
+    (path / "join_1").write_bytes(b"")                  # a crashed run's key: removed
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_store_rank, args=(str(path), 2, r, q)) for r in (0, 1)]
+    for p in procs:
+        p.start()
+    out = dict((r, (g, p)) for r, g, p in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert out[0][1] == out[1][1] == [b"r0", b"r1"]
+    assert sorted(os.listdir(path)) == ["abc_def", "data.npz", "gen2", "notes.txt"]
+
+
 def test_torch_host_comm_deprecated_shim():
     """TorchHostComm left the exports in round 4: the old names still resolve, with a
     DeprecationWarning, to a HostComm over torch.distributed."""
