@@ -145,12 +145,11 @@ int sod_match_enqueue(sod_ctx* ctx);
  * bf16 MFMA rate.  All are bit-exact; call before the descriptor uploads (the packed
  * layouts differ; switching drops uploaded descriptors). */
 int sod_match_set_impl(sod_ctx* ctx, int impl);
-/* Kernel shape of the int8 16x16x64 matcher (impl 1): 0 = by query count (default: the
- * LDS ring everywhere), 1 = LDS-ring kernel (queries stationary, 2-8 tiles per wave, DB
- * through LDS), 2 = register-streamed kernel (match_s.hip: a 512-query group resident per
- * wave, each wave streaming its own DB rows from HBM, DB ranges sharing bounds through
- * published top-2 lists; opt-in: slower than the ring at every measured size).
- * Same results bit for bit; replaces cv2.BFMatcher().knnMatch's loop (main.py:70-71). */
+/* Kernel shape of the int8 16x16x64 matcher (impl 1): 0 = by query count (default), 1 =
+ * the LDS-ring kernel (queries stationary, 2-8 tiles per wave, DB through LDS) -- the one
+ * shape since round 6; 2 (the register-streamed kernel, 2x slower at every measured size,
+ * EXPERIMENTS.md) is refused with SOD_EINVAL.  Replaces cv2.BFMatcher().knnMatch's loop
+ * (main.py:70-71). */
 int sod_match_set_kernel(sod_ctx* ctx, int kernel);
 /* 1 when the device's cos / sin (a restatement of glibc 2.35's x86_64 FMA-variant sin / cos,
  * glibc_trig.h) equal this host's libm bit for bit -- the math.cos / math.sin that

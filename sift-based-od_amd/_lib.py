@@ -385,7 +385,7 @@ class Context:
                                            s.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p)))
         return s, c
 
-    KERNELS = {"auto": 0, "ring": 1, "streamed": 2}
+    KERNELS = {"auto": 0, "ring": 1}
 
     OPTIONS = ("match_qt", "match_pf", "match_pair", "hough_fused", "select_multi", "sift_stream_mask",
                "sift_sort_max", "sift_desc_range_max", "sift_layer_split", "sift_side_mask",
@@ -405,9 +405,8 @@ class Context:
         return v.value
 
     def set_match_kernel(self, kernel):
-        """Kernel shape of the int8 matcher: "auto" (by query count, default), "ring" (LDS
-        ring, large query sets) or "streamed" (a 512-query group per wave, small sets);
-        results are identical."""
+        """Kernel shape of the int8 matcher: "auto" (by query count, default) or "ring" (the LDS
+        ring kernel, the only shape since round 6); results are identical."""
         self._chk(self._L.sod_match_set_kernel(self._h, self.KERNELS[kernel] if isinstance(kernel, str)
                                                else int(kernel)))
 

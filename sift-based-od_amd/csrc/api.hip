@@ -1078,8 +1078,11 @@ int sod_glibc_sincos(sod_ctx* ctx, int64_t n, const double* x, double* s, double
 
 int sod_match_set_kernel(sod_ctx* ctx, int kernel) {
   if (!ctx) return SOD_EINVAL;
-  if (kernel < 0 || kernel > 2)
-    return sod_fail(ctx, SOD_EINVAL, "kernel must be 0 (by query count), 1 (LDS ring) or 2 (streamed)");
+  if (kernel == 2)
+    return sod_fail(ctx, SOD_EINVAL, "the register-streamed kernel (2) was removed in round 6: "
+                                     "2x slower than the LDS ring at every size");
+  if (kernel < 0 || kernel > 1)
+    return sod_fail(ctx, SOD_EINVAL, "kernel must be 0 (by query count) or 1 (LDS ring)");
   ctx->mkernel = kernel;
   return SOD_OK;
 }

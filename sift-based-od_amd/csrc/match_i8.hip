@@ -1147,6 +1147,9 @@ int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db
   return SOD_OK;
 }
 
+// words per query of one shared-threshold slot (t2 + the two best-row words)
+int64_t sod_thr_words(const sod_ctx*) { return kThrWords; }
+
 // Query tiles per wave for the 16x16x64 kernel.  A work-group holds 8*QT tiles; the chip is
 // filled by splitting the DB into chunks, and every chunk restarts its queries' top-2 (the
 // dense early phase), so fewer queries per work-group buy longer chunks and no padding tiles
@@ -1212,10 +1215,6 @@ int launch_match_i8(sod_ctx* ctx) {
   const int64_t max_st = ((int64_t)1 << 30) / (wide ? w::kStageBytes : kStageBytes);
   if (st_per_split > max_st) st_per_split = max_st;
   split = cdiv(nstages, st_per_split);
-  // small query sets: the register-streamed kernel (match_s.hip); st_per_split then counts
-  // subtiles of a DB range
-  const bool use_s = !wide && sod_match_use_s(ctx);
-  if (use_s) sod_match_s_geometry(ctx, &split, &st_per_split);
   ctx->split = (int)split;
   SOD_TRY(sod_reserve(ctx, ctx->cd1, (size_t)nq_pad));
   SOD_TRY(sod_reserve(ctx, ctx->cd2, (size_t)nq_pad));
@@ -1251,10 +1250,7 @@ int launch_match_i8(sod_ctx* ctx) {
   const int seedload = split <= 64 ? 1 : 0;   // see match_unit (SOD_I8_SEEDLOAD)
   hipEvent_t eb, ee;
   SOD_TRY(sod_match_events(ctx, &eb, &ee));
-  if (use_s)
-    SOD_TRY(launch_match_s_kernel(ctx, ks, eb, ee, pd1, pidx, pd2, gthr, split, st_per_split));
-  else if (wide)
-  {
+  if (wide) {
 #define SOD_LAUNCH_I8W(Q)                                                                     \
     hipExtLaunchKernelGGL(match_i8w_kernel<Q>, dim3((unsigned)(qblocks * split)), dim3(w::NT), 0, \
                           ks, eb, ee, 0, ctx->dbpack.p, reinterpret_cast<const int*>(ctx->dn.p),  \

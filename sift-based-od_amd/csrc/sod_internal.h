@@ -99,7 +99,7 @@ struct sod_ctx {
   sod_opts opt;                 // sod_set_option
   bool last_timed = false;      // the last matcher launch recorded begin / end events
   int mkernel = 0;              // impl 1's kernel shape (sod_match_set_kernel): 0 = by query count,
-                                // 1 = LDS ring (match_i8.hip), 2 = register-streamed (match_s.hip)
+                                // 1 = LDS ring (match_i8.hip; the only shape since round 6)
 
   // ---- database (keypoints replicated, descriptors = shard) ----
   int64_t n_total = 0;          // keypoints in the whole DB
@@ -433,13 +433,7 @@ int launch_find_rows_i8(sod_ctx* ctx, const float* flo, const float* fhi, const 
                         int32_t* found);
 int launch_pack_i8(sod_ctx* ctx, const void* dsrc, int dtype, int64_t n, bool db);
 int launch_match_i8(sod_ctx* ctx);
-// small query sets (match_s.hip): the register-streamed kernel, its launch geometry, and the
-// shared-threshold words per query of one partial-result slot (both int8 kernels' layouts fit)
-bool sod_match_use_s(const sod_ctx* ctx);
-void sod_match_s_geometry(const sod_ctx* ctx, int64_t* split, int64_t* sub_per_split);
-int launch_match_s_kernel(sod_ctx* ctx, hipStream_t ks, hipEvent_t eb, hipEvent_t ee, float* pd1,
-                          int32_t* pidx, float* pd2, int32_t* gthr, int64_t split,
-                          int64_t sub_per_split);
+// shared-threshold words per query of one partial-result slot
 int64_t sod_thr_words(const sod_ctx* ctx);
 // matcher-input writers call these around their writes; the match launchers around the
 // kernel (see sod_ctx::mstream)

@@ -905,6 +905,8 @@ def test_set_option_validation(ctx):
     else:
         with pytest.raises(_lib.SodError):
             ctx.set_option("trig_exact", 1)
+    with pytest.raises(_lib.SodError):            # the streamed kernel was removed (round 6)
+        ctx.set_match_kernel(2)
     with _lib.Context(0) as other:
         other.set_option("debug_sync", 1)
         ctx.set_option("debug_sync", 0)

@@ -47,7 +47,7 @@ def _stages_vs_oracle(ctx, db, qs, idx1, good, bins, run_affine=True, post=True)
 
 
 def _set_kernel(ctx, kernel, paired_qt):
-    """"auto" / "streamed" (match_s.hip), or "paired": the ring kernel with paired waves
+    """"auto", or "paired": the ring kernel with paired waves
     (option match_pair = 2) at paired_qt query tiles per wave -- the same queries per
     work-group as the default pick, each wave of a pair taking every other subtile."""
     if kernel == "paired":
@@ -58,14 +58,14 @@ def _set_kernel(ctx, kernel, paired_qt):
         ctx.set_match_kernel(kernel)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "streamed", "paired"])
+@pytest.mark.parametrize("kernel", ["auto", "paired"])
 def test_c2_full_match_and_hough(ctx, kernel):
     """configs[1]: 10k x 100k -- every query's trainIdx, d1, d2 and ratio decision against
     the oracle; the chunks are short (4-8 k rows), so the shared thresholds, the seed pass and
     its read-back (<= 64 chunks) and QT 4 are all in play."""
     db = synthetic.make_database(100, 1000, seed=0)
     qs = synthetic.make_queries(10000, seed=1, db_seed=0, kp_per_image=1000)
-    _set_kernel(ctx, kernel, 8)     # "streamed": match_s.hip (20 query groups x 12 ranges)
+    _set_kernel(ctx, kernel, 8)
     ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
     ctx.upload_db(db.des)
     ctx.upload_queries(qs.des, qs.kp)
@@ -81,14 +81,14 @@ def test_c2_full_match_and_hough(ctx, kernel):
     _stages_vs_oracle(ctx, db, qs, idx1, good, 15)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "streamed", "paired"])
+@pytest.mark.parametrize("kernel", ["auto", "paired"])
 def test_one_query_image_1m(ctx, kernel):
     """main.py's real use: ONE query image (500 keypoints) against a 1M-row DB -- 2 query
     tiles per wave, 124+ DB chunks per query block (no seed read-back); every query against
     the oracle, then the Hough / affine stages."""
     db = synthetic.make_database(1000, 1000, seed=0, workers=8)
     qs = synthetic.make_queries(500, seed=11, db_seed=0, kp_per_image=1000, planted_frac=0.5)
-    _set_kernel(ctx, kernel, 4)     # "streamed": one 512-query group over 256 DB ranges
+    _set_kernel(ctx, kernel, 4)
     ctx.set_keypoints(db.kp, db.img, db.centroid, db.size)
     ctx.upload_db(db.des)
     ctx.upload_queries(qs.des, qs.kp)

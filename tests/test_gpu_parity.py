@@ -40,22 +40,6 @@ def test_matcher_golden(ctx, name, impl):
     ctx.set_impl("bf16")
 
 
-@pytest.mark.parametrize("name", CASES)
-def test_matcher_golden_streamed(ctx, name):
-    """The golden matcher cases on the register-streamed int8 kernel (match_s.hip)."""
-    g = golden(name)
-    ctx.set_impl("i8")
-    ctx.set_match_kernel("streamed")
-    load_case(ctx, g)
-    ctx.match()
-    ctx.ratio(0.75)
-    idx1, d1, d2, good = ctx.match_result()
-    assert np.array_equal(idx1, g["idx1"])
-    assert np.array_equal(d1.view(np.uint32), g["d1"].view(np.uint32))
-    assert np.array_equal(d2.view(np.uint32), g["d2"].view(np.uint32))
-    assert np.array_equal(good, g["good"])
-
-
 @pytest.mark.parametrize("impl", IMPLS)
 def test_matcher_edges(ctx, impl):
     g = golden("matcher_edges")
@@ -72,12 +56,12 @@ def test_matcher_edges(ctx, impl):
 
 @pytest.mark.parametrize("nq,ndb,seed", [(1, 2, 0), (17, 1000, 1), (500, 1000, 4), (700, 4099, 2),
                                          (513, 77777, 5), (3000, 60000, 3), (500, 400000, 6)])
-def test_streamed_matcher_vs_oracle(ctx, nq, ndb, seed):
-    """The register-streamed kernel (match_s.hip: a 512-query group per wave, the DB split
-    into up to 256 ranges that exchange top-2 lists) bit for bit against the oracle: one
-    query, partial groups (17, 513), ranges of a few subtiles (1 000 rows over 256 work-
-    groups), exact duplicates of DB rows (d1 = 0) and DB rows repeated in other ranges
-    (cross-range ties: the lowest trainIdx wins), and the matcher_edges golden."""
+def test_matcher_shapes_vs_oracle(ctx, nq, ndb, seed):
+    """The ring matcher bit for bit against the oracle on edge shapes (the cases written for
+    round 5's register-streamed kernel, removed in round 6): one query, partial query tiles
+    (17, 513), DB chunks of a few subtiles (1 000 rows), exact duplicates of DB rows (d1 = 0)
+    and DB rows repeated in far chunks (cross-chunk ties: the lowest trainIdx wins), two
+    launches on the same slots, and the matcher_edges golden."""
     rng = np.random.default_rng(seed)
     db = synthetic.sift_like_descriptors(rng, ndb)
     q = synthetic.sift_like_descriptors(rng, nq)
@@ -89,10 +73,9 @@ def test_streamed_matcher_vs_oracle(ctx, nq, ndb, seed):
         db[h:h + n] = db[:n]                       # the same rows in two far ranges
         q[k:k + min(n, nq - k)] = db[:min(n, nq - k)]
     ctx.set_impl("i8")
-    ctx.set_match_kernel("streamed")
     ctx.upload_db(db)
     ctx.upload_queries(q)
-    for _ in range(2):        # the second launch reuses the reset list slots
+    for _ in range(2):        # the second launch reuses the reset threshold slots
         ctx.match()
     ctx.ratio(0.75)
     idx1, d1, d2, good = ctx.match_result()
@@ -164,24 +147,20 @@ def test_matcher_vs_oracle(ctx, nq, ndb, seed, impl):
     assert np.array_equal(good, orc.ratio_test(f1, f2))
 
 
-@pytest.mark.parametrize("qt", ["2", "2f", "4", "8", "4p", "8p", "w1", "w2", "streamed"])
+@pytest.mark.parametrize("qt", ["2", "2f", "4", "8", "4p", "8p", "w1", "w2"])
 def test_matcher_query_tiles_shared_thresholds(ctx, qt):
     """int8 matcher with each query-tile count per wave (option match_qt; "4p" / "8p": paired
     waves, option match_pair = 2, each wave of a pair taking every other subtile; "2f": 2 tiles
     with the LDS fragments read two subtiles ahead (option match_pf = 2: the inline-asm reads'
     counted waits then leave the next subtile's reads in flight); "w1" / "w2":
-    the 32x32x32 kernel, impl i8w, at 1 / 2 tiles of 32 queries per wave; "streamed": the
-    register-streamed kernel, match_s.hip, whose DB ranges exchange top-2 lists) over a DB split into
+    the 32x32x32 kernel, impl i8w, at 1 / 2 tiles of 32 queries per wave) over a DB split into
     many chunks, so the chunks exchange prefilter thresholds mid-run: DB rows duplicated far
     apart (other chunks) make exact distance ties ACROSS chunks -- a shared threshold must
     keep them (lowest trainIdx wins), and queries equal to a DB row (d1 = 0) or near one,
     including runs of equal rows inside a chunk's seed stage."""
-    if qt == "streamed":
-        ctx.set_match_kernel("streamed")
-    else:
-        ctx.set_option("match_qt", int(qt.strip("pwf")))
-        ctx.set_option("match_pair", 2 if qt.endswith("p") else 1)
-        ctx.set_option("match_pf", 2 if qt.endswith("f") else 1)
+    ctx.set_option("match_qt", int(qt.strip("pwf")))
+    ctx.set_option("match_pair", 2 if qt.endswith("p") else 1)
+    ctx.set_option("match_pf", 2 if qt.endswith("f") else 1)
     rng = np.random.default_rng(31)
     ndb, nq = 150000, 2000
     db = synthetic.sift_like_descriptors(rng, ndb)
