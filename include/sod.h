@@ -66,14 +66,16 @@ int sod_match_times(sod_ctx* ctx, int n, float* ms);
  * the host exchange's upload), 6 all-gather of the candidates (or its upload)].  The matcher
  * entry is 0 when the step's launch was not timed (sod_set_match_timing stride > 1). */
 int sod_last_stage_ms(sod_ctx* ctx, float* ms_out, int n);
-/* Stage events (the bounds sod_last_stage_ms reads) on (1, the default) or off (0): each is
- * a marker packet on the tail's critical path, so a timed loop turns them off.  With them
- * off, sod_last_stage_ms reports 0 for the stages after the matcher. */
+/* Stage events (the bounds sod_last_stage_ms reads) on (1) or off (0, the default since
+ * round 6): each is a marker packet on the tail's critical path (~5 us before the next
+ * kernel; one query image's chain carried ~30 us of them).  With them off, sod_last_stage_ms
+ * reports 0 for the stages after the matcher. */
 int sod_set_stage_timing(sod_ctx* ctx, int on);
-/* Begin / end events of every `on`-th int8 matcher launch, counted from this call (1, the
- * default: every launch; 0: none; sod_match_times and sod_last_match_ms read the recorded
- * ones): a dispatch that records an event delays its stream's next kernel by ~5 us, a share
- * of a one-image step.  An untimed matcher-stream launch is joined by a marker event. */
+/* Begin / end events of every `on`-th int8 matcher launch, counted from this call (1: every
+ * launch; 0: none, the default since round 6; sod_match_times and sod_last_match_ms read the
+ * recorded ones): a dispatch that records an event delays its stream's next kernel by ~5 us,
+ * a share of a one-image step.  An untimed matcher-stream launch is joined by a marker
+ * event. */
 int sod_set_match_timing(sod_ctx* ctx, int on);
 /* Matcher streams with sod_match_set_overlap / sod_set_cu_reserve: 1 (default) = one stream
  * for both partial-result slots; 2 = one per slot, so consecutive launches overlap at their

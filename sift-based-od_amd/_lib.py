@@ -96,22 +96,34 @@ class Results(C.Structure):
                 ("final_pose", C.POINTER(C.c_double))]
 
 
-class _Mem:
-    """An __array_interface__ over host memory at an address (np.array(...) copies it)."""
-    __slots__ = ("__array_interface__",)
-
-    def __init__(self, addr, shape, typestr):
-        self.__array_interface__ = {"data": (addr, True), "shape": shape, "typestr": typestr,
-                                    "version": 3}
-
-
-def _arr(addr, n, typestr, width=0):
-    """A numpy copy of n elements (rows of `width`) at a host address (staging memory is
-    reused by the next fetch)."""
-    shape = (n, width) if width else (n,)
-    if n <= 0 or not addr:
-        return np.zeros(shape, np.dtype(typestr))
-    return np.array(_Mem(addr, shape, typestr))
+def _gather(spec):
+    """{name: numpy array} for (name, address, rows, typestr, width) records of host memory:
+    the arrays' byte ranges are merged into runs (the staging buffer holds most of them back to
+    back) and each run is copied ONCE, the arrays being views of that copy -- one memmove and a
+    view per array instead of a copy per array (~2x less Python time per results read)."""
+    out, rng = {}, []
+    for name, addr, n, typestr, width in spec:
+        dt = np.dtype(typestr)
+        cnt = n * (width or 1)
+        if n <= 0 or not addr:
+            out[name] = np.zeros((n, width) if width else (max(n, 0),), dt)
+        else:
+            rng.append((addr, addr + cnt * dt.itemsize, name, dt, cnt, n, width))
+    rng.sort()
+    i = 0
+    while i < len(rng):
+        lo, hi = rng[i][0], rng[i][1]
+        j = i + 1
+        while j < len(rng) and rng[j][0] <= hi + 4096:   # (gaps: alignment padding)
+            hi = max(hi, rng[j][1])
+            j += 1
+        raw = np.empty(hi - lo, np.uint8)
+        C.memmove(raw.ctypes.data, lo, hi - lo)
+        for addr, _, name, dt, cnt, n, width in rng[i:j]:
+            v = np.frombuffer(raw, dt, cnt, addr - lo)
+            out[name] = v.reshape(n, width) if width else v
+        i = j
+    return out
 
 
 # sod_results read in one go: every field as a plain number (pointers as addresses)
@@ -545,32 +557,44 @@ class Context:
         self._chk(self._L.sod_results_fetch(self._h, mask, C.byref(rs)))
         r = np.frombuffer(rs, _RES_DTYPE)[0].tolist()   # (values in field order)
         r = dict(zip(_RES_DTYPE.names, r))
-        out = {}
+        # (name, address, rows, typestr, width) of every array to return
+        V, M = r["n_valid"], r["n_members"]
+        spec = []
         if mask & 1:
             n = r["nq"]
-            out["match"] = (_arr(r["idx1"], n, "<i4"), _arr(r["d1"], n, "<f4"),
-                            _arr(r["d2"], n, "<f4"), _arr(r["good"], n, "|b1"))
-        V, M = r["n_valid"], r["n_members"]
+            spec += [("idx1", r["idx1"], n, "<i4", 0), ("d1", r["d1"], n, "<f4", 0),
+                     ("d2", r["d2"], n, "<f4", 0), ("good", r["good"], n, "|b1", 0)]
         if r["selected"]:
-            out["valid"] = {"keys": _arr(r["keys"], V, "<i4", 4), "votes": _arr(r["votes"], V, "<i4"),
-                            "offsets": _arr(r["offsets"], V + 1, "<i8"),
-                            "members": _arr(r["members"], M, "<i4"),
-                            "means": _arr(r["means"], V, "<f8", 6)}
+            spec += [("keys", r["keys"], V, "<i4", 4), ("votes", r["votes"], V, "<i4", 0),
+                     ("offsets", r["offsets"], V + 1, "<i8", 0),
+                     ("members", r["members"], M, "<i4", 0), ("means", r["means"], V, "<f8", 6)]
         if r["affined"]:
-            out["affine"] = {"survived": _arr(r["survived"], V, "|b1"),
-                             "votes": _arr(r["affine_votes"], V, "<i4"),
-                             "params": _arr(r["params"], V, "<f8", 6),
-                             "alive": _arr(r["alive"], M, "|b1")}
+            spec += [("survived", r["survived"], V, "|b1", 0),
+                     ("affine_votes", r["affine_votes"], V, "<i4", 0),
+                     ("params", r["params"], V, "<f8", 6), ("alive", r["alive"], M, "|b1", 0)]
         if r["post"]:
             nb, npos, nori = r["n_bins"], r["n_pos"], r["n_ori"]
-            out["post"] = {"bin_index": _arr(r["bin_index"], nb, "<i4"),
-                           "pos_off": _arr(r["pos_off"], npos + 1, "<i4"),
-                           "pos_members": _arr(r["pos_members"], nb, "<i4"),
-                           "ori_pos_off": _arr(r["ori_pos_off"], npos + 1, "<i4"),
-                           "ori_off": _arr(r["ori_off"], nori + 1, "<i4"),
-                           "ori_members": _arr(r["ori_members"], nb, "<i4"),
-                           "final_orientation": _arr(r["final_orientation"], npos, "<f8"),
-                           "final_pose": _arr(r["final_pose"], npos, "<f8", 6)}
+            spec += [("bin_index", r["bin_index"], nb, "<i4", 0),
+                     ("pos_off", r["pos_off"], npos + 1, "<i4", 0),
+                     ("pos_members", r["pos_members"], nb, "<i4", 0),
+                     ("ori_pos_off", r["ori_pos_off"], npos + 1, "<i4", 0),
+                     ("ori_off", r["ori_off"], nori + 1, "<i4", 0),
+                     ("ori_members", r["ori_members"], nb, "<i4", 0),
+                     ("final_orientation", r["final_orientation"], npos, "<f8", 0),
+                     ("final_pose", r["final_pose"], npos, "<f8", 6)]
+        a = _gather(spec)
+        out = {}
+        if mask & 1:
+            out["match"] = (a["idx1"], a["d1"], a["d2"], a["good"])
+        if r["selected"]:
+            out["valid"] = {k: a[k] for k in ("keys", "votes", "offsets", "members", "means")}
+        if r["affined"]:
+            out["affine"] = {"survived": a["survived"], "votes": a["affine_votes"],
+                             "params": a["params"], "alive": a["alive"]}
+        if r["post"]:
+            out["post"] = {k: a[k] for k in ("bin_index", "pos_off", "pos_members", "ori_pos_off",
+                                             "ori_off", "ori_members", "final_orientation",
+                                             "final_pose")}
         return out
 
     def pipeline(self, query_shape, bins=15, ratio=0.75, vote_threshold=5, affine_threshold=4,
@@ -604,7 +628,7 @@ class Context:
         return out
 
     def set_match_timing(self, on):
-        """Matcher launch events (sod_set_match_timing; default on = every launch): False / 0
+        """Matcher launch events (sod_set_match_timing; default off): True = every launch, False / 0
         records none, an int s every s-th launch from now on."""
         stride = int(on) if not isinstance(on, bool) else (1 if on else 0)
         self._chk(self._L.sod_set_match_timing(self._h, stride))
@@ -626,7 +650,8 @@ class Context:
         self._chk(self._L.sod_set_matcher_streams(self._h, int(n)))
 
     def set_stage_timing(self, on):
-        """Record the per-stage events read by stage_ms (default on; off in timed loops)."""
+        """Record the per-stage events read by stage_ms (default off: each event delays the
+        stream's next kernel)."""
         self._chk(self._L.sod_set_stage_timing(self._h, 1 if on else 0))
 
     STAGES = ("match_kernel", "merge_ratio", "hough_vote", "select", "affine", "allreduce",

@@ -277,7 +277,8 @@ struct sod_ctx {
   hipEvent_t ev_matched_p = nullptr;   // the last matcher launch's completion event
   hipEvent_t ev_done[2] = {nullptr, nullptr};   // each slot's last matcher-stream completion
   hipStream_t mstream_of(int slot) const { return mtwo && slot ? mstream2 : mstream; }
-  bool stage_timing = true;   // sod_set_stage_timing: ev[2..5] around the tail stages
+  bool stage_timing = false;  // sod_set_stage_timing: events around the tail stages (off by
+                              // default: each is a marker packet that delays the next kernel)
   bool post_exact = true;     // sod_set_post_exact: survivors' x / y means redone with glibc
                               // (only while !trig_exact)
   // the device's cos / sin (glibc_trig.h) equal the host's libm bit for bit (checked once per
@@ -295,7 +296,7 @@ struct sod_ctx {
   bool merge_norec[2] = {false, false};   // a slot's last merge released it without an event
   // sod_set_match_timing: begin/end events of every match_stride-th int8 matcher launch
   // (0: none); mlaunch counts the launches since the last setting
-  int match_stride = 1;
+  int match_stride = 0;
   int64_t mlaunch = 0;
   // sod_set_cu_reserve: the top `reserved_cus` CU-mask bits (cu_reserve per XCD, mask bit i
   // is on XCD i % 8) run the context / side streams; the matcher stream gets the rest

@@ -116,3 +116,23 @@ def test_numpy_matmul_probe():
             want = (fma(m0, x, m1 * y) if got == 1 else fma(m1, y, m0 * x) if got == 2
                     else m0 * x + m1 * y)
             assert v == want
+
+
+def test_results_gather_views():
+    """_lib._gather (sod_results_fetch's host read): arrays at host addresses, merged into
+    runs copied once, come back equal to their sources -- runs of adjacent arrays, a far
+    one, empty and null entries, 2-D rows."""
+    import numpy as np
+    a = np.arange(40, dtype=np.int32)
+    b = np.arange(12, dtype=np.float64).reshape(2, 6) * 0.5
+    far = np.array([True, False, True])
+    base = a.ctypes.data
+    spec = [("x", base, 10, "<i4", 0), ("y", base + 40, 5, "<i4", 4), ("b", b.ctypes.data, 2, "<f8", 6),
+            ("f", far.ctypes.data, 3, "|b1", 0), ("e", base, 0, "<i4", 0), ("n", 0, 0, "<f8", 6)]
+    out = _lib._gather(spec)
+    assert np.array_equal(out["x"], a[:10])
+    assert np.array_equal(out["y"], a[10:30].reshape(5, 4))
+    assert np.array_equal(out["b"], b) and np.array_equal(out["f"], far)
+    assert out["e"].shape == (0,) and out["n"].shape == (0, 6)
+    a[:] = -1                                   # copies, not views of the source memory
+    assert out["x"][0] == 0

@@ -570,6 +570,7 @@ def test_matcher_overlap_equals_serial(use_comm, reserve, affine):
             c.comm_init(1, 0, _lib.unique_id())
         c.set_keypoints(db.kp, db.img, db.centroid, db.size)
         c.upload_db(db.des)
+        c.set_match_timing(True)                # (off by default)
         got = []
         for qs in qsets:
             c.upload_queries(qs.des, qs.kp)

@@ -129,7 +129,7 @@ int run(const char* data, const i32x4* in, int* out, unsigned long long* clk) {
   CK(hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost));
   for (int b = 0; b < nwg; ++b) ghz += (double)h[2 * b] / (double)h[2 * b + 1] * 0.1 / nwg;
   const double ops = (double)nwg * 4 * (2.0 * iters * 8 * 2 * QT) * 32768.0;
-  printf("%-8.8s data, mode %d (%s): %.3f ms per launch (last 20 of %d) = %.2f POP/s = %.1f %% of "
+  printf("%-14.14s data, mode %d (%s): %.3f ms per launch (last 20 of %d) = %.2f POP/s = %.1f %% of "
          "5 POP/s; last launch's clock %.2f GHz\n", data, MODE,
          MODE == 0 ? "MFMA only" : MODE == 1 ? "MFMA + prefilter" : MODE == 2 ? "MFMA + 2-subtile windows" : "MFMA + 4-subtile windows", last, nlaunch, ops / (last * 1e-3) / 1e15,
          ops / (last * 1e-3) / 5e15 * 100.0, ghz);
@@ -156,9 +156,8 @@ int main(int argc, char** argv) {
     }
     fclose(f);
     CK(hipMemcpy(in, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    if (run<0>(argv[1], in, out, clk) || run<1>(argv[1], in, out, clk) ||
-        run<2>(argv[1], in, out, clk) || run<3>(argv[1], in, out, clk))
-      return 1;
+    if (run<0>(argv[1], in, out, clk) || run<1>(argv[1], in, out, clk)) return 1;
+    if (argc > 2) return 0;   // (a second argument: the file's lines only)
   }
   srand(12345);
   for (auto& v : h) v = (rand() & 0xffff) | ((rand() & 0xffff) << 16);

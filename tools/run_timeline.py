@@ -1,0 +1,63 @@
+"""Main.run for one query image (500 keypoints) against the 1M-row DB, split into its host
+phases (median of 200 runs): the pipeline enqueue (ctypes call + C++ enqueue), the results
+fetch (wait for the device + the staging read + numpy arrays), final_pose_from_arrays and
+the rest of Main.run; the device step alone (enqueue -> synchronize, no read) beside it.
+    python tools/run_timeline.py [n_images_in_db] [queries]"""
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import sod_pkg  # noqa: E402
+
+sod_pkg.load()
+from sift_based_od_amd import Main, SiftDatabase, _lib, synthetic  # noqa: E402
+from sift_based_od_amd.pipeline import POS_FACTOR  # noqa: E402
+from sift_based_od_amd.postprocessing import final_pose_from_arrays  # noqa: E402
+
+
+def main():
+    nimg = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+    nq = int(sys.argv[2]) if len(sys.argv) > 2 else 500
+    db = synthetic.make_database(nimg, 1000, seed=0, workers=8)
+    qs = synthetic.make_queries(nq, seed=7, db_seed=0, kp_per_image=1000, n_objects=1)
+    bins = (32, 32, 8, 12)
+    c = _lib.Context(0)
+    c.set_impl("i8")
+    m = Main(c)
+    m.set_database(SiftDatabase(db.des, db.kp, db.img, db.centroid, db.size))
+    m.get_query_features(qs.des, qs.kp, qs.shape)
+    for _ in range(50):
+        m.run(bins)
+    c.synchronize()
+    parts = ("match", "valid", "affine", "post")
+    ph = {k: [] for k in ("enqueue", "fetch", "final_pose", "run_total", "device_step")}
+    for _ in range(200):
+        t0 = time.perf_counter()
+        c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
+                   stage=parts)
+        t1 = time.perf_counter()
+        r = c.results(parts=parts)
+        t2 = time.perf_counter()
+        final_pose_from_arrays(r["post"])
+        t3 = time.perf_counter()
+        ph["enqueue"].append(t1 - t0)
+        ph["fetch"].append(t2 - t1)
+        ph["final_pose"].append(t3 - t2)
+        t0 = time.perf_counter()
+        m.run(bins)
+        ph["run_total"].append(time.perf_counter() - t0)
+        c.synchronize()
+        t0 = time.perf_counter()
+        c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True)
+        c.synchronize()
+        ph["device_step"].append(time.perf_counter() - t0)
+    for k, v in ph.items():
+        print("  %-12s median %.4f ms  min %.4f ms" % (k, 1e3 * float(np.median(v)), 1e3 * min(v)))
+
+
+if __name__ == "__main__":
+    main()
