@@ -1,4 +1,4 @@
-"""Benchmark of the sift-based-OD hot path on MI355X (driver contract: see DESIGN.md §Bench).
+"""Benchmark of the sift-based-OD hot path on MI355X (driver contract: DESIGN.md § 6).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \

@@ -912,3 +912,34 @@ def test_set_option_validation(ctx):
         other.set_option("debug_sync", 1)
         ctx.set_option("debug_sync", 0)
         assert other.get_option("debug_sync") == 1
+
+
+@pytest.mark.parametrize("case", ["no_good_matches", "no_valid_bins", "one_query"])
+def test_main_run_empty_stages(case):
+    """Main.run (the staged one-transfer read, main.py's sequence in one enqueue) on edge
+    sizes: nothing passes the ratio test, no bin reaches the vote threshold, one query -- the
+    results equal the stage-by-stage getters' and the final pose list is empty when nothing
+    survives."""
+    nq = 1 if case == "one_query" else 600
+    db = synthetic.make_database(3, 400, seed=41)
+    qs = synthetic.make_queries(nq, seed=42, db_seed=41, kp_per_image=400, planted_frac=0.6,
+                                n_objects=1)
+    ratio = 0.0 if case == "no_good_matches" else 0.75
+    vthr = 10 ** 6 if case == "no_valid_bins" else 5
+    m = sod.Main()
+    m.set_database(sod.SiftDatabase(db.des, db.kp, db.img, db.centroid, db.size))
+    m.get_query_features(qs.des, qs.kp, qs.shape)
+    out = m.run(15, vote_threshold=vthr, affine_threshold=4, ratio=ratio)
+    c = m.ctx
+    idx1, d1, d2, good = c.match_result()
+    assert np.array_equal(out["idx1"], idx1) and np.array_equal(out["good"], good)
+    v = c.valid_result()
+    for k in ("keys", "votes", "offsets", "members"):
+        assert np.array_equal(out["valid"][k], v[k]), k
+    a = c.affine_result()
+    assert np.array_equal(out["affine"]["survived"], a["survived"])
+    if case == "no_good_matches":
+        assert not good.any()
+    if case in ("no_good_matches", "no_valid_bins"):
+        assert len(out["valid"]["keys"]) == 0 and m.final_pose == []
+    assert len(m.final_pose) == len(out["post"]["final_pose"])
