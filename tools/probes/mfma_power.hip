@@ -105,6 +105,68 @@ __global__ __launch_bounds__(512, 1) void probe(const i32x4* __restrict__ in, in
   }
 }
 
+// the same for the 32x32x32 shape (impl i8w's): 4 tiles of 32 queries per wave (the ring's
+// 128 queries), a 32-row "subtile" = 4 k-steps x 4 tiles = 16 MFMAs (twice the work of the
+// 16x16x64 subtile), tile-major with the previous tile's prefilter beside the current tile's
+// chain (two max3 chains over its 16 values + combine + compare: 8 VALU + ballot); MODE 1 adds
+// that prefilter
+typedef __attribute__((ext_vector_type(16))) int i32x16;
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void probe_w(const i32x4* __restrict__ in, int* out, int iters,
+                                                  unsigned long long* clk) {
+  const int lane = threadIdx.x & 63;
+  i32x4 bq[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bq[t][k] = in[(4 * t + k) * 64 + lane];
+  i32x4 a[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[u][k] = in[(16 + 4 * u + k) * 64 + lane];
+  i32x16 c;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) c[i] = in[(32 + i / 4) * 64 + lane][i & 3];
+  i32x16 accp = c;
+  int thr = INT_MAX - 1, hits = 0;
+  unsigned long long t0 = 0, r0 = 0;
+  if (threadIdx.x == 0) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        i32x16 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u & 3][0], bq[t][0], MODE ? c : accp, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u & 3][1], bq[t][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u & 3][2], bq[t][2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u & 3][3], bq[t][3], acc, 0, 0, 0);
+        if constexpr (MODE == 1) {
+          const int ma = max(max(max(max(max(max(accp[0], accp[1]), accp[2]), accp[3]), accp[4]), accp[5]), accp[6]);
+          const int mb = max(max(max(max(max(max(accp[7], accp[8]), accp[9]), accp[10]), accp[11]), accp[12]), accp[13]);
+          const int m = max(max(ma, mb), max(accp[14], accp[15]));
+          if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= thr) != 0, 0)) ++hits;
+        }
+        accp = acc;
+      }
+    }
+  }
+  int s = hits;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += accp[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if (threadIdx.x == 0) {
+    clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
+    clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
+template <int MODE>
+int run_w(const char* data, const i32x4* in, int* out, unsigned long long* clk);
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 template <int MODE>
@@ -136,6 +198,33 @@ int run(const char* data, const i32x4* in, int* out, unsigned long long* clk) {
   return 0;
 }
 
+template <int MODE>
+int run_w(const char* data, const i32x4* in, int* out, unsigned long long* clk) {
+  const int iters = 1000, nwg = 256;   // same op count per launch as the 16x16x64 probe
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<unsigned long long> h(2 * nwg);
+  const int nlaunch = 440;
+  float last = 0;
+  double ghz = 0;
+  for (int rep = 0; rep < nlaunch; ++rep) {
+    if (rep == nlaunch - 20) CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL((probe_w<MODE>), dim3(nwg), dim3(512), 0, 0, in, out, iters, clk);
+  }
+  CK(hipEventRecord(e1, 0));
+  CK(hipDeviceSynchronize());
+  CK(hipEventElapsedTime(&last, e0, e1));
+  last /= 20;
+  CK(hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost));
+  for (int b = 0; b < nwg; ++b) ghz += (double)h[2 * b] / (double)h[2 * b + 1] * 0.1 / nwg;
+  const double ops = (double)nwg * 4 * (2.0 * iters * 8 * 16) * 65536.0;
+  printf("%-14.14s data, 32x32x32 %s: %.3f ms per launch = %.2f POP/s = %.1f %% of 5 POP/s; "
+         "clock %.2f GHz\n", data, MODE ? "MFMA + prefilter" : "MFMA only", last,
+         ops / (last * 1e-3) / 1e15, ops / (last * 1e-3) / 5e15 * 100.0, ghz);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int nvec = 64 * 64;
   i32x4* in;
@@ -156,6 +245,12 @@ int main(int argc, char** argv) {
     }
     fclose(f);
     CK(hipMemcpy(in, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    if (argc > 2 && argv[2][0] == 'w') {   // "w": the 32x32x32 shape against 16x16x64
+      if (run<1>(argv[1], in, out, clk) || run_w<0>(argv[1], in, out, clk) ||
+          run_w<1>(argv[1], in, out, clk))
+        return 1;
+      return 0;
+    }
     if (run<0>(argv[1], in, out, clk) || run<1>(argv[1], in, out, clk)) return 1;
     if (argc > 2) return 0;   // (a second argument: the file's lines only)
   }
