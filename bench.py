@@ -598,8 +598,10 @@ def main():
     # contributed -- every rank holds the same merged result, so each counts all shards and
     # its own count must agree with the others'
     cinfo = comm.info() if comm is not None else None
-    winners = np.bincount((idx1 // n_shard).astype(np.int64), minlength=world).tolist()
-    good_winners = np.bincount((idx1[good] // n_shard).astype(np.int64), minlength=world).tolist()
+    real = (idx1 >= 0) & (idx1 < world * n_shard)       # (a DB row, not a sentinel)
+    winners = np.bincount((idx1[real] // n_shard).astype(np.int64), minlength=world).tolist()
+    good_winners = np.bincount((idx1[real & good] // n_shard).astype(np.int64),
+                               minlength=world).tolist()
     rank_rec = D.gather_json({"rank": rank, "comm": cinfo, "shard_winners": winners,
                               "own_shard_winners": winners[rank],
                               "shard_good_winners": good_winners})
