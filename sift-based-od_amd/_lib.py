@@ -96,30 +96,33 @@ class Results(C.Structure):
                 ("final_pose", C.POINTER(C.c_double))]
 
 
+_I4, _I8, _F4, _F8, _B1 = (np.dtype(t) for t in ("<i4", "<i8", "<f4", "<f8", "|b1"))
+
+
 def _gather(spec):
-    """{name: numpy array} for (name, address, rows, typestr, width) records of host memory:
+    """{name: numpy array} for (name, address, rows, dtype, width) records of host memory:
     the arrays' byte ranges are merged into runs (the staging buffer holds most of them back to
     back) and each run is copied ONCE, the arrays being views of that copy -- one memmove and a
-    view per array instead of a copy per array (~2x less Python time per results read)."""
-    out, rng = {}, []
-    for name, addr, n, typestr, width in spec:
-        dt = np.dtype(typestr)
-        cnt = n * (width or 1)
+    view per array instead of a copy per array."""
+    out, items = {}, []
+    for name, addr, n, dt, width in spec:
+        cnt = n * width if width else n
         if n <= 0 or not addr:
             out[name] = np.zeros((n, width) if width else (max(n, 0),), dt)
         else:
-            rng.append((addr, addr + cnt * dt.itemsize, name, dt, cnt, n, width))
-    rng.sort()
-    i = 0
-    while i < len(rng):
-        lo, hi = rng[i][0], rng[i][1]
+            items.append((addr, addr + cnt * dt.itemsize, name, dt, cnt, n, width))
+    items.sort()
+    i, last = 0, len(items)
+    while i < last:
+        lo, hi = items[i][0], items[i][1]
         j = i + 1
-        while j < len(rng) and rng[j][0] <= hi + 4096:   # (gaps: alignment padding)
-            hi = max(hi, rng[j][1])
+        while j < last and items[j][0] <= hi + 4096:   # (gaps: alignment padding)
+            if items[j][1] > hi:
+                hi = items[j][1]
             j += 1
         raw = np.empty(hi - lo, np.uint8)
         C.memmove(raw.ctypes.data, lo, hi - lo)
-        for addr, _, name, dt, cnt, n, width in rng[i:j]:
+        for addr, _, name, dt, cnt, n, width in items[i:j]:
             v = np.frombuffer(raw, dt, cnt, addr - lo)
             out[name] = v.reshape(n, width) if width else v
         i = j
@@ -132,6 +135,51 @@ _RES_DTYPE = np.dtype({"names": [f for f, _ in Results._fields_],
                                    ("<i8" if t is C.c_int64 else "<i4") for _, t in Results._fields_],
                        "offsets": [getattr(Results, f).offset for f, _ in Results._fields_],
                        "itemsize": C.sizeof(Results)})
+
+
+def _results_from_struct(rs, mask):
+    """sod_results (the parts in ``mask``) as Context.results' dict of numpy arrays."""
+    r = np.frombuffer(rs, _RES_DTYPE)[0].tolist()   # (values in field order)
+    r = dict(zip(_RES_DTYPE.names, r))
+    # (name, address, rows, typestr, width) of every array to return
+    V, M = r["n_valid"], r["n_members"]
+    spec = []
+    if mask & 1:
+        n = r["nq"]
+        spec += [("idx1", r["idx1"], n, _I4, 0), ("d1", r["d1"], n, _F4, 0),
+                 ("d2", r["d2"], n, _F4, 0), ("good", r["good"], n, _B1, 0)]
+    if r["selected"]:
+        spec += [("keys", r["keys"], V, _I4, 4), ("votes", r["votes"], V, _I4, 0),
+                 ("offsets", r["offsets"], V + 1, _I8, 0),
+                 ("members", r["members"], M, _I4, 0), ("means", r["means"], V, _F8, 6)]
+    if r["affined"]:
+        spec += [("survived", r["survived"], V, _B1, 0),
+                 ("affine_votes", r["affine_votes"], V, _I4, 0),
+                 ("params", r["params"], V, _F8, 6), ("alive", r["alive"], M, _B1, 0)]
+    if r["post"]:
+        nb, npos, nori = r["n_bins"], r["n_pos"], r["n_ori"]
+        spec += [("bin_index", r["bin_index"], nb, _I4, 0),
+                 ("pos_off", r["pos_off"], npos + 1, _I4, 0),
+                 ("pos_members", r["pos_members"], nb, _I4, 0),
+                 ("ori_pos_off", r["ori_pos_off"], npos + 1, _I4, 0),
+                 ("ori_off", r["ori_off"], nori + 1, _I4, 0),
+                 ("ori_members", r["ori_members"], nb, _I4, 0),
+                 ("final_orientation", r["final_orientation"], npos, _F8, 0),
+                 ("final_pose", r["final_pose"], npos, _F8, 6)]
+    a = _gather(spec)
+    out = {}
+    if mask & 1:
+        out["match"] = (a["idx1"], a["d1"], a["d2"], a["good"])
+    if r["selected"]:
+        out["valid"] = {k: a[k] for k in ("keys", "votes", "offsets", "members", "means")}
+    if r["affined"]:
+        out["affine"] = {"survived": a["survived"], "votes": a["affine_votes"],
+                         "params": a["params"], "alive": a["alive"]}
+    if r["post"]:
+        out["post"] = {k: a[k] for k in ("bin_index", "pos_off", "pos_members", "ori_pos_off",
+                                         "ori_off", "ori_members", "final_orientation",
+                                         "final_pose")}
+    return out
 
 
 # name -> (restype, argtypes); must mirror include/sod.h exactly (tests check the symbols)
@@ -555,47 +603,7 @@ class Context:
             mask |= self.RES[p]
         rs = Results()
         self._chk(self._L.sod_results_fetch(self._h, mask, C.byref(rs)))
-        r = np.frombuffer(rs, _RES_DTYPE)[0].tolist()   # (values in field order)
-        r = dict(zip(_RES_DTYPE.names, r))
-        # (name, address, rows, typestr, width) of every array to return
-        V, M = r["n_valid"], r["n_members"]
-        spec = []
-        if mask & 1:
-            n = r["nq"]
-            spec += [("idx1", r["idx1"], n, "<i4", 0), ("d1", r["d1"], n, "<f4", 0),
-                     ("d2", r["d2"], n, "<f4", 0), ("good", r["good"], n, "|b1", 0)]
-        if r["selected"]:
-            spec += [("keys", r["keys"], V, "<i4", 4), ("votes", r["votes"], V, "<i4", 0),
-                     ("offsets", r["offsets"], V + 1, "<i8", 0),
-                     ("members", r["members"], M, "<i4", 0), ("means", r["means"], V, "<f8", 6)]
-        if r["affined"]:
-            spec += [("survived", r["survived"], V, "|b1", 0),
-                     ("affine_votes", r["affine_votes"], V, "<i4", 0),
-                     ("params", r["params"], V, "<f8", 6), ("alive", r["alive"], M, "|b1", 0)]
-        if r["post"]:
-            nb, npos, nori = r["n_bins"], r["n_pos"], r["n_ori"]
-            spec += [("bin_index", r["bin_index"], nb, "<i4", 0),
-                     ("pos_off", r["pos_off"], npos + 1, "<i4", 0),
-                     ("pos_members", r["pos_members"], nb, "<i4", 0),
-                     ("ori_pos_off", r["ori_pos_off"], npos + 1, "<i4", 0),
-                     ("ori_off", r["ori_off"], nori + 1, "<i4", 0),
-                     ("ori_members", r["ori_members"], nb, "<i4", 0),
-                     ("final_orientation", r["final_orientation"], npos, "<f8", 0),
-                     ("final_pose", r["final_pose"], npos, "<f8", 6)]
-        a = _gather(spec)
-        out = {}
-        if mask & 1:
-            out["match"] = (a["idx1"], a["d1"], a["d2"], a["good"])
-        if r["selected"]:
-            out["valid"] = {k: a[k] for k in ("keys", "votes", "offsets", "members", "means")}
-        if r["affined"]:
-            out["affine"] = {"survived": a["survived"], "votes": a["affine_votes"],
-                             "params": a["params"], "alive": a["alive"]}
-        if r["post"]:
-            out["post"] = {k: a[k] for k in ("bin_index", "pos_off", "pos_members", "ori_pos_off",
-                                             "ori_off", "ori_members", "final_orientation",
-                                             "final_pose")}
-        return out
+        return _results_from_struct(rs, mask)
 
     def pipeline(self, query_shape, bins=15, ratio=0.75, vote_threshold=5, affine_threshold=4,
                  x_factor=128.0, y_factor=128.0, run_affine=True, stage=()):

@@ -127,8 +127,9 @@ def test_results_gather_views():
     b = np.arange(12, dtype=np.float64).reshape(2, 6) * 0.5
     far = np.array([True, False, True])
     base = a.ctypes.data
-    spec = [("x", base, 10, "<i4", 0), ("y", base + 40, 5, "<i4", 4), ("b", b.ctypes.data, 2, "<f8", 6),
-            ("f", far.ctypes.data, 3, "|b1", 0), ("e", base, 0, "<i4", 0), ("n", 0, 0, "<f8", 6)]
+    i4, f8, b1 = np.dtype("<i4"), np.dtype("<f8"), np.dtype("|b1")
+    spec = [("x", base, 10, i4, 0), ("y", base + 40, 5, i4, 4), ("b", b.ctypes.data, 2, f8, 6),
+            ("f", far.ctypes.data, 3, b1, 0), ("e", base, 0, i4, 0), ("n", 0, 0, f8, 6)]
     out = _lib._gather(spec)
     assert np.array_equal(out["x"], a[:10])
     assert np.array_equal(out["y"], a[10:30].reshape(5, 4))

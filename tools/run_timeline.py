@@ -34,7 +34,8 @@ def main():
         m.run(bins)
     c.synchronize()
     parts = ("match", "valid", "affine", "post")
-    ph = {k: [] for k in ("enqueue", "fetch", "final_pose", "run_total", "device_step")}
+    ph = {k: [] for k in ("enqueue", "fetch", "final_pose", "run_total", "device_step",
+                          "fetch_after_sync", "fetch_c_only")}
     for _ in range(200):
         t0 = time.perf_counter()
         c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
@@ -55,6 +56,39 @@ def main():
         c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True)
         c.synchronize()
         ph["device_step"].append(time.perf_counter() - t0)
+        # the read alone, the device idle (a sleep, not synchronize: any API call makes the
+        # staged results stale): host work of sod_results_fetch + the Python arrays
+        c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
+                   stage=parts)
+        time.sleep(0.002)
+        t0 = time.perf_counter()
+        c.results(parts=parts)
+        ph["fetch_after_sync"].append(time.perf_counter() - t0)
+        c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
+                   stage=parts)
+        time.sleep(0.002)
+        rs = _lib.Results()
+        mask = sum(c.RES[p] for p in parts)
+        t0 = time.perf_counter()
+        c._L.sod_results_fetch(c._h, mask, _lib.C.byref(rs))
+        ph["fetch_c_only"].append(time.perf_counter() - t0)
+    # the Python side of the read, piece by piece (the device idle, results staged)
+    rs = _lib.Results()
+    mask = sum(c.RES[p] for p in parts)
+    c._L.sod_results_fetch(c._h, mask, _lib.C.byref(rs))
+    r = dict(zip(_lib._RES_DTYPE.names, np.frombuffer(rs, _lib._RES_DTYPE)[0].tolist()))
+    lo = min(r[k] for k in ("idx1", "d1", "d2", "good") if r[k])
+    nbytes = 9 * r["nq"] + 4096
+    pinned = np.empty(nbytes, np.uint8)
+    plain = np.ones(nbytes, np.uint8)
+    for name, fn in (("memmove_pinned_10KB", lambda: _lib.C.memmove(pinned.ctypes.data, lo, nbytes)),
+                     ("memmove_plain_10KB", lambda: _lib.C.memmove(pinned.ctypes.data, plain.ctypes.data, nbytes))):
+        ts = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        ph[name] = ts
     for k, v in ph.items():
         print("  %-12s median %.4f ms  min %.4f ms" % (k, 1e3 * float(np.median(v)), 1e3 * min(v)))
 
