@@ -101,31 +101,29 @@ _I4, _I8, _F4, _F8, _B1 = (np.dtype(t) for t in ("<i4", "<i8", "<f4", "<f8", "|b
 
 def _gather(spec):
     """{name: numpy array} for (name, address, rows, dtype, width) records of host memory:
-    the arrays' byte ranges are merged into runs (the staging buffer holds most of them back to
-    back) and each run is copied ONCE, the arrays being views of that copy -- one memmove and a
-    view per array instead of a copy per array."""
-    out, items = {}, []
+    consecutive records whose byte ranges ascend with gaps under a page (the staging buffer
+    holds most arrays back to back, 16-byte aligned) form one run, each run is copied ONCE and
+    its arrays are views of that copy.  (A gap under 4 096 bytes between two mapped ranges
+    touches no page outside them, so reading it is safe.)"""
+    out, runs, run = {}, [], None
     for name, addr, n, dt, width in spec:
-        cnt = n * width if width else n
         if n <= 0 or not addr:
             out[name] = np.zeros((n, width) if width else (max(n, 0),), dt)
-        else:
-            items.append((addr, addr + cnt * dt.itemsize, name, dt, cnt, n, width))
-    items.sort()
-    i, last = 0, len(items)
-    while i < last:
-        lo, hi = items[i][0], items[i][1]
-        j = i + 1
-        while j < last and items[j][0] <= hi + 4096:   # (gaps: alignment padding)
-            if items[j][1] > hi:
-                hi = items[j][1]
-            j += 1
-        raw = np.empty(hi - lo, np.uint8)
-        C.memmove(raw.ctypes.data, lo, hi - lo)
-        for addr, _, name, dt, cnt, n, width in items[i:j]:
-            v = np.frombuffer(raw, dt, cnt, addr - lo)
-            out[name] = v.reshape(n, width) if width else v
-        i = j
+            continue
+        cnt = n * width if width else n
+        end = addr + cnt * dt.itemsize
+        if run is None or addr < run[0] or addr - run[1] >= 4096:
+            run = [addr, end]
+            runs.append(run)
+        elif end > run[1]:
+            run[1] = end
+        run.append((name, addr - run[0], dt, cnt, (n, width) if width else None))
+    fb = np.frombuffer
+    for run in runs:
+        raw = fb((C.c_uint8 * (run[1] - run[0])).from_address(run[0]), np.uint8).copy()
+        for name, off, dt, cnt, shape in run[2:]:
+            v = fb(raw, dt, cnt, off)
+            out[name] = v.reshape(shape) if shape else v
     return out
 
 
@@ -135,47 +133,55 @@ _RES_DTYPE = np.dtype({"names": [f for f, _ in Results._fields_],
                                    ("<i8" if t is C.c_int64 else "<i4") for _, t in Results._fields_],
                        "offsets": [getattr(Results, f).offset for f, _ in Results._fields_],
                        "itemsize": C.sizeof(Results)})
+_RF = {f: i for i, f in enumerate(_RES_DTYPE.names)}
+
+
+def _res_table(rows):
+    # (output name, pointer field, count field, count + k, dtype, width) -> field positions
+    return tuple((name, _RF[ptr], _RF[cnt], k, dt, w) for name, ptr, cnt, k, dt, w in rows)
+
+
+# the staging buffer's arrays first, in its order, then the host-decoded ones (keys, votes
+# and the post-processing vectors live in separate host allocations)
+_RES_MATCH = _res_table([("idx1", "idx1", "nq", 0, _I4, 0), ("d1", "d1", "nq", 0, _F4, 0),
+                         ("d2", "d2", "nq", 0, _F4, 0), ("good", "good", "nq", 0, _B1, 0)])
+_RES_VALID = _res_table([("offsets", "offsets", "n_valid", 1, _I8, 0),
+                         ("members", "members", "n_members", 0, _I4, 0),
+                         ("means", "means", "n_valid", 0, _F8, 6)])
+_RES_AFFINE = _res_table([("survived", "survived", "n_valid", 0, _B1, 0),
+                          ("affine_votes", "affine_votes", "n_valid", 0, _I4, 0),
+                          ("params", "params", "n_valid", 0, _F8, 6),
+                          ("alive", "alive", "n_members", 0, _B1, 0)])
+_RES_KEYS = _res_table([("keys", "keys", "n_valid", 0, _I4, 4),
+                        ("votes", "votes", "n_valid", 0, _I4, 0)])
+_RES_POST = _res_table([("bin_index", "bin_index", "n_bins", 0, _I4, 0),
+                        ("pos_off", "pos_off", "n_pos", 1, _I4, 0),
+                        ("pos_members", "pos_members", "n_bins", 0, _I4, 0),
+                        ("ori_pos_off", "ori_pos_off", "n_pos", 1, _I4, 0),
+                        ("ori_off", "ori_off", "n_ori", 1, _I4, 0),
+                        ("ori_members", "ori_members", "n_bins", 0, _I4, 0),
+                        ("final_orientation", "final_orientation", "n_pos", 0, _F8, 0),
+                        ("final_pose", "final_pose", "n_pos", 0, _F8, 6)])
+_SEL, _AFF, _POST = _RF["selected"], _RF["affined"], _RF["post"]
 
 
 def _results_from_struct(rs, mask):
     """sod_results (the parts in ``mask``) as Context.results' dict of numpy arrays."""
     r = np.frombuffer(rs, _RES_DTYPE)[0].tolist()   # (values in field order)
-    r = dict(zip(_RES_DTYPE.names, r))
-    # (name, address, rows, typestr, width) of every array to return
-    V, M = r["n_valid"], r["n_members"]
-    spec = []
-    if mask & 1:
-        n = r["nq"]
-        spec += [("idx1", r["idx1"], n, _I4, 0), ("d1", r["d1"], n, _F4, 0),
-                 ("d2", r["d2"], n, _F4, 0), ("good", r["good"], n, _B1, 0)]
-    if r["selected"]:
-        spec += [("keys", r["keys"], V, _I4, 4), ("votes", r["votes"], V, _I4, 0),
-                 ("offsets", r["offsets"], V + 1, _I8, 0),
-                 ("members", r["members"], M, _I4, 0), ("means", r["means"], V, _F8, 6)]
-    if r["affined"]:
-        spec += [("survived", r["survived"], V, _B1, 0),
-                 ("affine_votes", r["affine_votes"], V, _I4, 0),
-                 ("params", r["params"], V, _F8, 6), ("alive", r["alive"], M, _B1, 0)]
-    if r["post"]:
-        nb, npos, nori = r["n_bins"], r["n_pos"], r["n_ori"]
-        spec += [("bin_index", r["bin_index"], nb, _I4, 0),
-                 ("pos_off", r["pos_off"], npos + 1, _I4, 0),
-                 ("pos_members", r["pos_members"], nb, _I4, 0),
-                 ("ori_pos_off", r["ori_pos_off"], npos + 1, _I4, 0),
-                 ("ori_off", r["ori_off"], nori + 1, _I4, 0),
-                 ("ori_members", r["ori_members"], nb, _I4, 0),
-                 ("final_orientation", r["final_orientation"], npos, _F8, 0),
-                 ("final_pose", r["final_pose"], npos, _F8, 6)]
-    a = _gather(spec)
+    sel, aff, post = r[_SEL], r[_AFF], r[_POST]
+    tables = (_RES_MATCH if mask & 1 else ()) + (_RES_VALID if sel else ()) + \
+        (_RES_AFFINE if aff else ()) + (_RES_KEYS if sel else ()) + (_RES_POST if post else ())
+    a = _gather([(name, r[p], r[c] + k, dt, w) for name, p, c, k, dt, w in tables])
     out = {}
     if mask & 1:
         out["match"] = (a["idx1"], a["d1"], a["d2"], a["good"])
-    if r["selected"]:
-        out["valid"] = {k: a[k] for k in ("keys", "votes", "offsets", "members", "means")}
-    if r["affined"]:
+    if sel:
+        out["valid"] = {"keys": a["keys"], "votes": a["votes"], "offsets": a["offsets"],
+                        "members": a["members"], "means": a["means"]}
+    if aff:
         out["affine"] = {"survived": a["survived"], "votes": a["affine_votes"],
                          "params": a["params"], "alive": a["alive"]}
-    if r["post"]:
+    if post:
         out["post"] = {k: a[k] for k in ("bin_index", "pos_off", "pos_members", "ori_pos_off",
                                          "ori_off", "ori_members", "final_orientation",
                                          "final_pose")}

@@ -121,7 +121,7 @@ def test_numpy_matmul_probe():
 def test_results_gather_views():
     """_lib._gather (sod_results_fetch's host read): arrays at host addresses, merged into
     runs copied once, come back equal to their sources -- runs of adjacent arrays, a far
-    one, empty and null entries, 2-D rows."""
+    one, empty and null entries, 2-D rows, records that step back inside or before a run."""
     import numpy as np
     a = np.arange(40, dtype=np.int32)
     b = np.arange(12, dtype=np.float64).reshape(2, 6) * 0.5
@@ -129,9 +129,11 @@ def test_results_gather_views():
     base = a.ctypes.data
     i4, f8, b1 = np.dtype("<i4"), np.dtype("<f8"), np.dtype("|b1")
     spec = [("x", base, 10, i4, 0), ("y", base + 40, 5, i4, 4), ("b", b.ctypes.data, 2, f8, 6),
-            ("f", far.ctypes.data, 3, b1, 0), ("e", base, 0, i4, 0), ("n", 0, 0, f8, 6)]
+            ("f", far.ctypes.data, 3, b1, 0), ("e", base, 0, i4, 0), ("n", 0, 0, f8, 6),
+            ("back", base + 8, 3, i4, 0), ("x2", base + 4, 2, i4, 0)]   # (before the run)
     out = _lib._gather(spec)
     assert np.array_equal(out["x"], a[:10])
+    assert list(out["back"]) == [2, 3, 4] and list(out["x2"]) == [1, 2]
     assert np.array_equal(out["y"], a[10:30].reshape(5, 4))
     assert np.array_equal(out["b"], b) and np.array_equal(out["f"], far)
     assert out["e"].shape == (0,) and out["n"].shape == (0, 6)

@@ -19,6 +19,14 @@ from sift_based_od_amd.pipeline import POS_FACTOR  # noqa: E402
 from sift_based_od_amd.postprocessing import final_pose_from_arrays  # noqa: E402
 
 
+def spin(sec):
+    # wait with the CPU busy (a sleep lets the core idle and cools its caches: the reads after
+    # it would measure the wake-up, not the read)
+    t = time.perf_counter() + sec
+    while time.perf_counter() < t:
+        pass
+
+
 def main():
     nimg = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
     nq = int(sys.argv[2]) if len(sys.argv) > 2 else 500
@@ -35,7 +43,8 @@ def main():
     c.synchronize()
     parts = ("match", "valid", "affine", "post")
     ph = {k: [] for k in ("enqueue", "fetch", "final_pose", "run_total", "device_step",
-                          "fetch_after_sync", "fetch_c_only")}
+                          "fetch_after_sync", "fetch_c_only", "fetch_c_match", "fetch_c_again",
+                          "sync_idle", "sync_first", "enqueue_after_idle")}
     for _ in range(200):
         t0 = time.perf_counter()
         c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
@@ -56,22 +65,52 @@ def main():
         c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True)
         c.synchronize()
         ph["device_step"].append(time.perf_counter() - t0)
-        # the read alone, the device idle (a sleep, not synchronize: any API call makes the
+        # the read alone, the device idle (a busy wait, not synchronize: any API call makes the
         # staged results stale): host work of sod_results_fetch + the Python arrays
         c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
                    stage=parts)
-        time.sleep(0.002)
+        spin(0.002)
         t0 = time.perf_counter()
         c.results(parts=parts)
         ph["fetch_after_sync"].append(time.perf_counter() - t0)
         c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
                    stage=parts)
-        time.sleep(0.002)
+        spin(0.002)
         rs = _lib.Results()
         mask = sum(c.RES[p] for p in parts)
         t0 = time.perf_counter()
         c._L.sod_results_fetch(c._h, mask, _lib.C.byref(rs))
         ph["fetch_c_only"].append(time.perf_counter() - t0)
+        # the same read of the matches alone (no key decode, no post-processing walk), then an
+        # idle sod_synchronize (set_dev + three stream queries)
+        c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
+                   stage=parts)
+        spin(0.002)
+        t0 = time.perf_counter()
+        c._L.sod_results_fetch(c._h, 1, _lib.C.byref(rs))
+        ph["fetch_c_match"].append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        c._L.sod_results_fetch(c._h, 1, _lib.C.byref(rs))
+        ph["fetch_c_again"].append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        c._L.sod_synchronize(c._h)
+        ph["sync_idle"].append(time.perf_counter() - t0)
+        # the first stream query after a finished pipeline, and an enqueue that follows a
+        # finished pipeline with no query in between
+        c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
+                   stage=parts)
+        spin(0.002)
+        t0 = time.perf_counter()
+        c._L.sod_synchronize(c._h)
+        ph["sync_first"].append(time.perf_counter() - t0)
+        c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
+                   stage=parts)
+        spin(0.002)
+        t0 = time.perf_counter()
+        c.pipeline(m.rgb_query.shape, bins, 0.75, 5, 4, POS_FACTOR * 4.0, POS_FACTOR * 4.0, True,
+                   stage=parts)
+        ph["enqueue_after_idle"].append(time.perf_counter() - t0)
+        c.synchronize()
     # the Python side of the read, piece by piece (the device idle, results staged)
     rs = _lib.Results()
     mask = sum(c.RES[p] for p in parts)
