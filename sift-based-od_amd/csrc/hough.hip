@@ -893,17 +893,6 @@ __global__ __launch_bounds__(256) void members_kernel(
 // Same outputs as the multi-kernel path: vbin, scal[0] = V, voff, scal[1], members.
 constexpr int kSmallT = 1024;
 constexpr int kSmallQ = 2048;
-#ifdef SOD_SEL_STAMP
-// diagnostic build only: s_memrealtime (100 MHz) at the phase boundaries of the last 64 launches
-__device__ unsigned long long g_selst[64][5];
-__device__ unsigned int g_selst_n;
-__device__ unsigned long long g_fust[64][8];   // hough_small_kernel phase boundaries
-__device__ unsigned int g_fust_n;
-#define SEL_STAMP(i) \
-  if (tid == 0) st[i] = __builtin_amdgcn_s_memrealtime();
-#else
-#define SEL_STAMP(i)
-#endif
 constexpr int kSmallV = 2048;   // valid bins whose (bin, count, first touch, offset) stay in LDS
 
 __global__ __launch_bounds__(kSmallT) void select_small_kernel(
@@ -919,10 +908,6 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
   __shared__ int64_t carry64_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr int kW = kSmallT / 64;
-#ifdef SOD_SEL_STAMP
-  unsigned long long st[5] = {0, 0, 0, 0, 0};
-#endif
-  SEL_STAMP(0)
   if (tid == 0) {
     carry_s = 0;
     carry64_s = 0;
@@ -963,7 +948,6 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
     __syncthreads();
   }
   const int64_t V = carry_s;
-  SEL_STAMP(1)
   // 2. member offsets
   const bool in_lds = V <= kSmallV;
   for (int64_t v0 = 0; v0 < V; v0 += kSmallT) {
@@ -1005,7 +989,6 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
     voff[V] = carry64_s;
   }
   __syncthreads();   // voff (global) written above is read by other waves below
-  SEL_STAMP(2)
   // 3. members in query order, one wave per bin
   for (int64_t v = w; v < V; v += kW) {
     const uint32_t lb = in_lds ? vb_lb[v] : vbin[v];
@@ -1033,15 +1016,6 @@ __global__ __launch_bounds__(kSmallT) void select_small_kernel(
       got += __popcll(bal);
     }
   }
-#ifdef SOD_SEL_STAMP
-  __syncthreads();
-  SEL_STAMP(3)
-  if (tid == 0) {
-    const unsigned k = atomicAdd(&g_selst_n, 1u) % 64u;
-    for (int i = 0; i < 4; ++i) g_selst[k][i] = st[i];
-    g_selst[k][4] = (unsigned long long)V;
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1152,14 +1126,6 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
   __shared__ int64_t carry64_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr int kW = kFusedT / 64;
-#ifdef SOD_SEL_STAMP
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // [7]: emission start
-#define FU_STAMP(i) \
-  if (tid == 0) st[i] = __builtin_amdgcn_s_memrealtime();
-#else
-#define FU_STAMP(i)
-#endif
-  FU_STAMP(0)
   for (int i = tid; i < kFusedHash; i += kFusedT) {
     hk[i] = kNoKey;
     hn[i] = 0u;
@@ -1216,7 +1182,6 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
     }
   }
   __syncthreads();
-  FU_STAMP(1)
   // the voting queries, in query order (the votes' ordinals follow it)
   for (int64_t q0 = 0; q0 < nq; q0 += kFusedT) {
     const int64_t q = q0 + tid;
@@ -1240,7 +1205,6 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
   }
   const uint32_t nv = carry_s;
   __syncthreads();
-  FU_STAMP(2)
   if (tid == 0) carry_s = 0;
   // 2. one thread per vote (voting query i, slot s): its bin's count and first touch from 16
   //    hash lookups; the first touch of a bin with >= thr votes sets bit s of vfm[i]
@@ -1258,7 +1222,6 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
     }
   }
   __syncthreads();
-  FU_STAMP(3)
   // valid bins in first-touch order (voting query, then slot): the first valid index of each
   // voting query = the scan of the masks' popcounts (nv <= kFusedT: one round) ...
   {
@@ -1280,7 +1243,6 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
     }
     if (i < nv) vbase[i] = off + x - n;
     if (tid == 0) carry_s = tot;
-    FU_STAMP(7)
   }
   __syncthreads();
   // ... and every valid-first vote writes its bin there, one thread per vote
@@ -1308,7 +1270,6 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
   }
   __syncthreads();
   const int64_t V = carry_s;
-  FU_STAMP(4)
   // 3. member offsets (exclusive scan of the counts, in valid order)
   for (int64_t v0 = 0; v0 < V; v0 += kFusedT) {
     const int64_t v = v0 + tid;
@@ -1344,7 +1305,6 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
     voff[V] = carry64_s;
   }
   __syncthreads();   // voff (global) past the LDS copy is read by other waves below
-  FU_STAMP(5)
   // 4. members in query order, one wave per bin from its first voting query, with the affine
   //    inputs of each member
   for (int64_t v = w; v < V; v += kW) {
@@ -1383,19 +1343,11 @@ __global__ __launch_bounds__(kFusedT) void hough_small_kernel(
   // 5. the guard records listed above: their count to the slot the host reads, and the append
   //    counter back to 0 for the next launch (hist_kernel's handover)
   __syncthreads();
-  FU_STAMP(6)
   if (tid == 0) {
     const uint32_t g = __hip_atomic_load(&gstat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     gstat[1] = g;
     gstat[0] = 0u;
   }
-#ifdef SOD_SEL_STAMP
-  if (tid == 0) {
-    const unsigned k = atomicAdd(&g_fust_n, 1u) % 64u;
-    for (int i = 0; i < 8; ++i) g_fust[k][i] = st[i];
-  }
-#endif
-#undef FU_STAMP
 }
 
 // (tx, ty, alpha, qx, qy) of the poses of the members of listed valid bins, for the host's
@@ -2531,11 +2483,3 @@ int launch_affine(sod_ctx* ctx, int64_t nb_host, bool count_on_device, const int
   return SOD_OK;
 }
 
-#ifdef SOD_SEL_STAMP
-extern "C" int sod_debug_selstamps(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_selst), sizeof(g_selst)) == hipSuccess ? 0 : 1;
-}
-extern "C" int sod_debug_fusedstamps(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fust), sizeof(g_fust)) == hipSuccess ? 0 : 1;
-}
-#endif

@@ -486,17 +486,6 @@ __device__ __forceinline__ void chain_cols1(const float* T, const float* cur, fl
     case 15: F<15>(__VA_ARGS__); break; default: F<16>(__VA_ARGS__); break;             \
   }
 
-#ifdef SOD_SIFT_STAMP
-// diagnostic build only: s_memrealtime (100 MHz) at each phase of the small-octave chain
-__device__ unsigned long long g_sift_stamps[256];
-#define SIFT_STAMP(i)                                                              \
-  {                                                                                \
-    const int i_ = (i);                                                            \
-    if (threadIdx.x == 0 && i_ < 256) g_sift_stamps[i_] = __builtin_amdgcn_s_memrealtime(); \
-  }
-#else
-#define SIFT_STAMP(i)
-#endif
 
 // barrier for LDS traffic only: the pyramid's global stores drain in the background (no
 // pass of the chain reads them back)
@@ -520,9 +509,6 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
   __shared__ float kk[kMaxLayers][kMaxTaps];
   __shared__ int tabx[kTabMax + 2 * kMaxR], taby[kTabMax + 2 * kMaxR];
   const int L = P.L, tid = threadIdx.x;
-  int stamp = 0;
-  (void)stamp;
-  SIFT_STAMP(stamp++)
   for (int t = tid; t < kMaxLayers * kMaxTaps; t += 1024) kk[t / kMaxTaps][t % kMaxTaps] = kern[t];
   for (int o = o0; o < P.n; ++o) {
     const Oct& q = P.o[o];
@@ -556,7 +542,6 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
       else
         SOD_CHAIN_CASES(chain_rows, cur, T, w, h, kk[i], tabx, taby, tid)
       lds_barrier();
-      SIFT_STAMP(stamp++)
       float* dst = g0 + (size_t)np * i;
       float* dg = dogs + q.d + (size_t)np * (i - 1);
       if (np <= 1024)
@@ -565,7 +550,6 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
         SOD_CHAIN_CASES(chain_cols, T, cur, nxt, dst, dg, Dg[i - 1], i == L ? Bl : nullptr, w, h,
                         kk[i], tabx, taby, tid)
       lds_barrier();
-      SIFT_STAMP(stamp++)
       float* t2 = cur;
       cur = nxt;
       nxt = t2;
@@ -598,7 +582,6 @@ __global__ __launch_bounds__(1024) void small_octaves_kernel(float* __restrict__
       }
     }
     lds_barrier();
-    SIFT_STAMP(stamp++)
   }
 }
 
@@ -2120,8 +2103,3 @@ int sod_sift_to_queries(sod_ctx* ctx) {
 
 }  // extern "C"
 
-#ifdef SOD_SIFT_STAMP
-extern "C" int sod_debug_sift_stamps(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sift_stamps), 256 * 8) == hipSuccess ? 0 : 1;
-}
-#endif
