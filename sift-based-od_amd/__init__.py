@@ -48,9 +48,3 @@ __all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid
            "find_max_orientation", "get_final_pose", "run_query_batch", "sift_query_batch", "HostComm", "RcclComm", "FileHostComm", "FileStore", "run_sharded",
            "shard_range", "SIFT", "SIFT_create", "bgr_to_gray"]
 
-
-def __getattr__(name):   # deprecated names, resolved (with a warning) on first use
-    if name == "TorchHostComm":
-        from . import sharded
-        return sharded.TorchHostComm
-    raise AttributeError("module %r has no attribute %r" % (__name__, name))

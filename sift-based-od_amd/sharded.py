@@ -312,40 +312,6 @@ class FileHostComm(HostComm):
         super().__init__(store.world, store.rank, allgather, allreduce)
 
 
-class _TorchHostComm(HostComm):
-    """HostComm over a torch.distributed process group -- DEPRECATED (round 4 removed it from
-    the exports; kept one release as ``sharded.TorchHostComm`` with a DeprecationWarning).
-    Use :class:`FileHostComm` (no PyTorch) or a :class:`HostComm` over your own collectives."""
-
-    def __init__(self, group=None):
-        import torch
-        import torch.distributed as dist
-
-        def allgather(a):
-            t = torch.from_numpy(np.ascontiguousarray(a))
-            out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
-            dist.all_gather(out, t, group=group)
-            return [o.numpy() for o in out]
-
-        def allreduce(a, op):
-            t = torch.from_numpy(np.ascontiguousarray(a))
-            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MIN,
-                            group=group)
-            return t.numpy()
-
-        super().__init__(dist.get_world_size(group), dist.get_rank(group), allgather, allreduce)
-
-
-def __getattr__(name):
-    if name == "TorchHostComm":
-        import warnings
-        warnings.warn("sharded.TorchHostComm is deprecated and will be removed: use FileHostComm "
-                      "(no PyTorch) or HostComm over your own collectives", DeprecationWarning,
-                      stacklevel=2)
-        return _TorchHostComm
-    raise AttributeError("module %r has no attribute %r" % (__name__, name))
-
-
 def run_sharded(ctx, comm, shard, query_shape, bins, ratio=0.75, vote_threshold=5,
                 affine_threshold=4, x_factor=128.0, y_factor=128.0, run_affine=True):
     """One query image over the sharded database.  ``shard`` = (lo, hi) global rows held

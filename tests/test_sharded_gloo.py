@@ -259,13 +259,11 @@ def test_file_store_keeps_unrelated_files(tmp_path):
     assert sorted(os.listdir(path)) == ["abc_def", "data.npz", "gen2", "notes.txt"]
 
 
-def test_torch_host_comm_deprecated_shim():
-    """TorchHostComm left the exports in round 4: the old names still resolve, with a
-    DeprecationWarning, to a HostComm over torch.distributed."""
+def test_torch_host_comm_removed():
+    """TorchHostComm left the exports in round 4 and its deprecated alias in round 6: the name
+    no longer resolves (FileHostComm, or a HostComm over the caller's own collectives)."""
     import sift_based_od_amd as pkg
     from sift_based_od_amd import sharded
-    with pytest.warns(DeprecationWarning):
-        cls = sharded.TorchHostComm
-    assert issubclass(cls, sharded.HostComm)
-    with pytest.warns(DeprecationWarning):
-        assert pkg.TorchHostComm is cls
+    for mod in (pkg, sharded):
+        with pytest.raises(AttributeError):
+            getattr(mod, "TorchHostComm")
