@@ -188,6 +188,26 @@ def _results_from_struct(rs, mask):
     return out
 
 
+def _load_resparse():
+    """The C results reader (csrc/resparse.c, built beside libsod.so), or None: then
+    _results_from_struct reads them (same dict; SOD_RESPARSE=0 forces the Python reader)."""
+    if os.environ.get("SOD_RESPARSE", "1") == "0":
+        return None
+    import importlib.util
+    import sysconfig
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        "_resparse" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if not os.path.exists(path):
+        return None
+    spec = importlib.util.spec_from_file_location("_resparse", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_RESPARSE = _load_resparse()
+
+
 # name -> (restype, argtypes); must mirror include/sod.h exactly (tests check the symbols)
 SIGNATURES = {
     "sod_abi_version": (C.c_int, []),
@@ -609,6 +629,8 @@ class Context:
             mask |= self.RES[p]
         rs = Results()
         self._chk(self._L.sod_results_fetch(self._h, mask, C.byref(rs)))
+        if _RESPARSE is not None:
+            return _RESPARSE.results(C.addressof(rs), mask)
         return _results_from_struct(rs, mask)
 
     def pipeline(self, query_shape, bins=15, ratio=0.75, vote_threshold=5, affine_threshold=4,

@@ -139,3 +139,72 @@ def test_results_gather_views():
     assert out["e"].shape == (0,) and out["n"].shape == (0, 6)
     a[:] = -1                                   # copies, not views of the source memory
     assert out["x"][0] == 0
+
+
+def _fake_results(rng, nq, V, M, nb, npos, nori, selected, affined, post, nulls=()):
+    """A sod_results pointing into one random host buffer (kept alive by the caller)."""
+    import numpy as np
+    buf = rng.integers(0, 256, 1 << 18, dtype=np.uint8)
+    buf[1::7] &= 1     # (bool arrays read 0/1 bytes from the device; any byte here is fine)
+    o = [buf.ctypes.data]
+
+    def take(n):
+        a = o[0]
+        o[0] += (n + 15) & ~15
+        return a
+    rs = _lib.Results()
+    arr = np.frombuffer(rs, _lib._RES_DTYPE).copy()
+    for k, v in {"nq": nq, "selected": selected, "n_valid": V, "n_members": M,
+                 "affined": affined, "post": post, "n_bins": nb, "n_pos": npos,
+                 "n_ori": nori}.items():
+        arr[0][k] = v
+    sizes = {"idx1": nq * 4, "d1": nq * 4, "d2": nq * 4, "good": nq, "keys": V * 16,
+             "votes": V * 4, "offsets": (V + 1) * 8, "members": M * 4, "means": V * 48,
+             "survived": V, "affine_votes": V * 4, "params": V * 48, "alive": M,
+             "bin_index": nb * 4, "pos_off": (npos + 1) * 4, "pos_members": nb * 4,
+             "ori_pos_off": (npos + 1) * 4, "ori_off": (nori + 1) * 4, "ori_members": nb * 4,
+             "final_orientation": npos * 8, "final_pose": npos * 48}
+    for k, s in sizes.items():
+        arr[0][k] = 0 if k in nulls else take(s)
+    ctypes.memmove(ctypes.addressof(rs), arr.ctypes.data, ctypes.sizeof(rs))
+    return rs, buf
+
+
+def test_resparse_equals_python_reader():
+    """The C results reader (csrc/resparse.c) returns what _results_from_struct returns: the
+    same dict / tuple structure, dtypes, shapes and values, as copies -- over every part mask,
+    empty parts, null pointers and zero counts."""
+    import numpy as np
+    assert _lib._RESPARSE is not None, "_resparse not built (make -C sift-based-od_amd/csrc)"
+    rng = np.random.default_rng(5)
+
+    def same(a, b):
+        assert type(a) is type(b)
+        if isinstance(a, dict):
+            assert list(a) == list(b)
+            for k in a:
+                same(a[k], b[k])
+        elif isinstance(a, tuple):
+            assert len(a) == len(b)
+            for x, y in zip(a, b):
+                same(x, y)
+        else:
+            assert a.dtype == b.dtype and a.shape == b.shape, (a.dtype, b.dtype, a.shape, b.shape)
+            assert a.tobytes() == b.tobytes()
+    cases = [(500, 40, 400, 12, 5, 7, 1, 1, 1, ()), (500, 40, 400, 12, 5, 7, 1, 0, 0, ()),
+             (500, 0, 0, 0, 0, 0, 1, 1, 1, ()), (0, 3, 5, 3, 1, 1, 1, 1, 1, ()),
+             (17, 9, 20, 4, 2, 3, 1, 1, 1, ("members", "final_pose", "d2")),
+             (1, 1, 1, 1, 1, 1, 0, 0, 0, ())]
+    for case in cases:
+        rs, buf = _fake_results(rng, *case)
+        for mask in (1, 2, 3, 7, 15):
+            want = _lib._results_from_struct(rs, mask)
+            got = _lib._RESPARSE.results(ctypes.addressof(rs), mask)
+            same(got, want)
+        got = _lib._RESPARSE.results(ctypes.addressof(rs), 15)
+        before = {k: v.copy() for k, v in got.get("valid", {}).items()}
+        buf[:] = 0                                   # copies, not views of the source
+        for k, v in before.items():
+            assert np.array_equal(got["valid"][k], v)
+    with pytest.raises(ValueError):
+        _lib._RESPARSE.results(0, 15)
