@@ -347,6 +347,8 @@ def unique_id():
 class Context:
     """One libsod context = one GPU (HIP device ``device``) driven by this thread."""
 
+    _pargs_key = _pargs = None   # (Context.pipeline's last argument struct)
+
     def __init__(self, device=0):
         self._L = lib()
         h = c_ctx()
@@ -638,19 +640,29 @@ class Context:
         """The whole path in one enqueue (sod_pipeline_enqueue); ``stage``: result parts
         ("match", "valid", "affine", "post") staged right behind it, so that the next
         ``results()`` of those parts only waits."""
-        a = PipelineArgs()
-        for p in stage:
-            a.stage_parts |= self.RES[p]
-        a.ratio = float(ratio)
-        a.query_h, a.query_w = int(query_shape[0]), int(query_shape[1])
-        for i, v in enumerate(bins4(bins)):
-            a.bins[i] = int(v)
-        a.vote_threshold = int(vote_threshold)
-        a.affine_threshold = int(affine_threshold)
-        a.x_factor, a.y_factor = float(x_factor), float(y_factor)
-        a.run_affine = 1 if run_affine else 0
+        # the argument struct of the last call is reused when every argument is equal (a run
+        # of images: its ~15 field writes sit before the matcher launch); the key holds
+        # immutable values (bins4's tuple, the stage tuple), never a caller's mutable object
+        b4 = bins4(bins)
+        key = (query_shape[0], query_shape[1], b4, ratio, vote_threshold, affine_threshold,
+               x_factor, y_factor, run_affine, tuple(stage))
+        if key == self._pargs_key:
+            a = self._pargs
+        else:
+            a = PipelineArgs()
+            for p in stage:
+                a.stage_parts |= self.RES[p]
+            a.ratio = float(ratio)
+            a.query_h, a.query_w = int(query_shape[0]), int(query_shape[1])
+            for i, v in enumerate(b4):
+                a.bins[i] = v
+            a.vote_threshold = int(vote_threshold)
+            a.affine_threshold = int(affine_threshold)
+            a.x_factor, a.y_factor = float(x_factor), float(y_factor)
+            a.run_affine = 1 if run_affine else 0
+            self._pargs_key, self._pargs = key, a
         self._chk(self._L.sod_pipeline_enqueue(self._h, C.byref(a)))
-        self.bins = bins4(bins)
+        self.bins = b4
 
     def last_match_ms(self):
         v = C.c_float()

@@ -208,3 +208,38 @@ def test_resparse_equals_python_reader():
             assert np.array_equal(got["valid"][k], v)
     with pytest.raises(ValueError):
         _lib._RESPARSE.results(0, 15)
+
+
+def test_pipeline_args_reused_only_when_equal():
+    """Context.pipeline reuses its argument struct when every argument equals the last
+    call's, and rebuilds it when any differs (a stub library records what the C side gets)."""
+    seen = []
+
+    class Stub:
+        def sod_pipeline_enqueue(self, h, a):
+            seen.append(bytes(a._obj))
+            return 0
+    c = object.__new__(_lib.Context)
+    c._L, c._h = Stub(), None
+    bins = [32, 32, 8, 12]
+    calls = [((480, 640), bins, 0.75, ("match",)), ((480, 640), bins, 0.75, ("match",)),
+             ((480, 640), bins, 0.8, ("match",)), ((480, 640), 15, 0.8, ("match", "post")),
+             ((481, 640), 15, 0.8, ("match", "post")), ((481, 640), bins, 0.8, ("match", "post"))]
+    for shape, b, r, st in calls:
+        c.pipeline(shape, b, r, stage=st)
+    snap = [(shape, _lib.bins4(b), r, st) for shape, b, r, st in calls]
+    bins[3] = 6                                   # the caller's list mutated in place
+    c.pipeline((481, 640), bins, 0.8, stage=("match", "post"))
+    want = []
+    for shape, b, r, st in snap + [((481, 640), (32, 32, 8, 6), 0.8, ("match", "post"))]:
+        a = _lib.PipelineArgs()
+        for p in st:
+            a.stage_parts |= c.RES[p]
+        a.ratio, a.query_h, a.query_w = r, shape[0], shape[1]
+        for i, v in enumerate(_lib.bins4(b)):
+            a.bins[i] = v
+        a.vote_threshold, a.affine_threshold, a.x_factor, a.y_factor = 5, 4, 128.0, 128.0
+        a.run_affine = 1
+        want.append(bytes(a))
+    assert seen == want
+    assert c.bins == (32, 32, 8, 6)
