@@ -27,6 +27,7 @@ import numpy as np
 from . import _lib
 from .database import Keypoints, SiftDatabase
 from .hough import hough_table_from_tuples, posebins_from_device
+from .postprocessing import final_pose_from_arrays
 from .sift_helpers import keypoints_from_arrays
 
 POS_FACTOR = 32   # main.py:141
@@ -373,7 +374,6 @@ class Main:
         if run_affine:
             out["affine"] = r["affine"]
         if post_process:
-            from .postprocessing import final_pose_from_arrays
             out["post"] = r["post"]
             self.final_pose = final_pose_from_arrays(out["post"])
         self._match = (idx1, good)

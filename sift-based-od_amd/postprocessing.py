@@ -117,5 +117,4 @@ def get_final_pose(pose_cluster, final_orientation_list):
 
 def final_pose_from_arrays(r):
     """The device result's ``final_pose`` rows as main.py's tuples."""
-    return [((float(p[0]), float(p[1])), float(p[2]), float(p[3]), (float(p[4]), float(p[5])))
-            for p in r["final_pose"]]
+    return [((p[0], p[1]), p[2], p[3], (p[4], p[5])) for p in r["final_pose"].tolist()]
