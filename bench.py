@@ -294,7 +294,8 @@ def main_path_extras(dev, impl, c3_data, names=("C1", "C2", "C3", "IMG1")):
     the enqueue to matches, valid bins, affine results, post-processing and ``final_pose``
     on the host (every result read back, any boundary-guard resolve included) -- the
     per-image time main.py sees.  C3 and IMG1 (one query image of 500 keypoints, main.py's
-    regime) use the bench's 1M-row DB; ``fused_run_ms`` is the median of 20 runs."""
+    regime) use the bench's 1M-row DB; ``fused_run_ms`` is the median of 100 runs (C3: 20)
+    after half as many warm-up runs."""
     from sift_based_od_amd import Main, SiftDatabase
     out = {}
     cases = {
@@ -336,9 +337,12 @@ def main_path_extras(dev, impl, c3_data, names=("C1", "C2", "C3", "IMG1")):
         for _ in range(reps):
             for k, v in staged().items():
                 stages[k] = stages.get(k, 0.0) + v / reps
-        m.run(bins)
+        # warm (clock ramp, buffers), then the median of 100 runs (20 at C3's ~4 ms)
+        nrun = 20 if name == "C3" else 100
+        for _ in range(nrun // 2):
+            m.run(bins)
         runs = []
-        for _ in range(20):
+        for _ in range(nrun):
             t0 = time.perf_counter()
             m.run(bins)
             runs.append((time.perf_counter() - t0) * 1000.0)
