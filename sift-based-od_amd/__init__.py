@@ -38,6 +38,7 @@ from .postprocessing import (dfs, find_max_orientation, get_final_pose,  # noqa:
 from .sharded import FileHostComm, FileStore, HostComm, RcclComm, run_sharded, shard_range  # noqa: F401
 from .batch import run_query_batch, sift_query_batch  # noqa: F401
 from .sift import SIFT, SIFT_create, bgr_to_gray  # noqa: F401
+from .constants import REFERENCE, ReferenceConstants  # noqa: F401
 
 __all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid", "make_kp",
            "make_temp_kp", "unpack_sift_octave", "PoseBin", "BFMatcher", "DMatch", "knn2",
@@ -46,5 +47,5 @@ __all__ = ["Keypoints", "SiftDatabase", "centroid_of", "KeyPoint", "get_centroid
            "AffineParameters", "Calc_x", "Ext_Params", "Gen_A", "Gen_b", "remove_outliers",
            "verify_bins", "Main", "dfs", "group_position", "group_orientation",
            "find_max_orientation", "get_final_pose", "run_query_batch", "sift_query_batch", "HostComm", "RcclComm", "FileHostComm", "FileStore", "run_sharded",
-           "shard_range", "SIFT", "SIFT_create", "bgr_to_gray"]
+           "shard_range", "SIFT", "SIFT_create", "bgr_to_gray", "REFERENCE", "ReferenceConstants"]
 

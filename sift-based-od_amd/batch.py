@@ -8,8 +8,9 @@ from __future__ import annotations
 import numpy as np
 
 from .database import Keypoints
+from .constants import REFERENCE
 
-POS_FACTOR = 32    # main.py:141
+POS_FACTOR = REFERENCE.pos_factor   # main.py:141
 
 
 def run_query_batch(ctx, images, bins=15, ratio=0.75, vote_threshold=5, affine_threshold=4,

@@ -25,12 +25,13 @@ import gc
 import numpy as np
 
 from . import _lib
+from .constants import REFERENCE
 from .database import Keypoints, SiftDatabase
 from .hough import hough_table_from_tuples, posebins_from_device
 from .postprocessing import final_pose_from_arrays
 from .sift_helpers import keypoints_from_arrays
 
-POS_FACTOR = 32   # main.py:141
+POS_FACTOR = REFERENCE.pos_factor   # main.py:141
 
 
 class _Shape:
